@@ -1,0 +1,200 @@
+"""Headline benchmark: vectorised racing-env steps on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs-per-gpu E] [--no-cpu-baseline]
+
+Workload = BASELINE.json configs[2] ("65536 parallel single-agent envs,
+1xMI355X"): the reference's seed-1 track pool (train.py:67-80:
+random.seed(1); np.random.seed(1); gen_tracks(N, seed=1); widths
+randint(6, 10); track_id = env index), 11 sensors, uniform random actions
+generated on the device, gymnasium next-step autoreset.  One bench "step" =
+one env step of every env (random actions + rx_step).  With N GPUs
+(torch.distributed.run, one rank per GPU) every rank owns 65,536 envs of a
+N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
+
+Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel
+(k_rays, the raycast), timed live with HIP events on the stream the kernels
+run on; ``cpu_baseline`` times oracle/np_env.py -- the reference's NumPy step
+restated (bit-exact vs the reference's golden vectors) -- on this host.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+FP64_VALU_PEAK_TF = 78.6  # MI355X FP64 vector peak (AMD spec)
+RAY_FLOPS_PER_SEG = 13    # 2 sub, 3 dotp, 3 cross, 3 v1.v3, 2 div per ray x segment
+RAYS_BYTES_PER_ENV = 24 + 11 * 4   # k_rays algorithmic HBM bytes/env: read x,y,angle (f64), write 11 f32 obs
+STEP_BYTES_PER_ENV = 218           # whole step, SURVEY.md §8(d)
+
+
+def seed1_pool(n_total):
+    """train.py:67-80 track pool for n_total envs (rx.track.gen_tracks == reference, memoised)."""
+    from rx.track import gen_tracks
+    random.seed(1)
+    np.random.seed(1)
+    pool = gen_tracks(num_tracks=n_total, seed=1)
+    widths = [np.random.randint(6, 10) for _ in range(n_total)]
+    return pool, widths
+
+
+def cpu_baseline(pool, widths, budget_s=15.0, n_envs=16):
+    """The reference's CPU execution model (NumPy step per env, sequential loop,
+    16 envs = configs/base_config.py num_envs) on one host core, bounded in time."""
+    from oracle.np_env import NpRacingEnv, NpSyncVectorEnv, NpTrack
+    from rx.track import TrackGeometry
+    envs = []
+    geo = {}
+    for i in range(n_envs):
+        key = (id(pool[i]), widths[i])
+        if key not in geo:
+            g = TrackGeometry(pool[i], widths[i])
+            geo[key] = NpTrack(g.waypoints, g.normals, g.segment_cache["starts"], g.segment_cache["v2"],
+                               g.track_width, g.get_start_pos())
+        envs.append(NpRacingEnv(geo[key], 11))
+    venv = NpSyncVectorEnv(envs)
+    venv.reset()
+    rng = np.random.default_rng(0)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        a = np.stack([rng.uniform(-1, 1, n_envs), rng.uniform(0, 1, n_envs)], 1).astype(np.float32)
+        venv.step(a)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(steps * n_envs / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/np_env.py NumPy restatement, {n_envs} envs x {steps} sequential steps "
+                      f"({steps * n_envs} env-steps, {dt:.1f} s), seed-1 pool, random actions, 1 host core"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs-per-gpu", type=int, default=65536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rx.vector_env import RacingVectorEnv
+    E = args.envs_per_gpu
+    n_total = E * world
+    pool, widths = seed1_pool(n_total)
+    lo, hi = rank * E, (rank + 1) * E
+    env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step")
+    n_slots = len(env.tracks)
+    S_of_env = 2 * np.diff(env.tracks.arrays()["wp_off"])[env.track_of_env]
+    ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))
+
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    scale = torch.tensor([2.0, 1.0], device=dev)
+    shift = torch.tensor([-1.0, 0.0], device=dev)
+    actions = torch.empty((E, 2), device=dev)
+
+    def one_step(ev=None):
+        torch.rand((E, 2), generator=gen, device=dev, out=actions)
+        actions.mul_(scale).add_(shift)
+        if ev is None:
+            env.step_device(actions)
+        else:
+            ev[0].record()
+            env.step_device(actions, phases=1)
+            ev[1].record()
+            env.step_device(actions, phases=2)
+            ev[2].record()
+
+    env.reset_device()
+    for _ in range(args.warmup):
+        one_step()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(events[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    ep = env.episode_stats()
+
+    if rank == 0:
+        value = n_total * args.steps / elapsed
+        achieved_gbs = RAYS_BYTES_PER_ENV * E / (ray_ms * 1e-3) / 1e9
+        achieved_tf = ray_flops_per_launch / (ray_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_rays.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": "env-steps/sec (whole node) @65536 envs",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "configs[2]: 65536 single-agent racing envs per GPU (seed-1 gen_tracks pool, "
+                                   "11 sensors, uniform random device actions, next-step autoreset)",
+                       "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
+                       "parallelism": f"env shards x{world}, no collective in the step"},
+            "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                         "traffic": traffic, "bytes_per_env": RAYS_BYTES_PER_ENV,
+                         "avg_launch_ms": round(ray_ms, 5)},
+            "compute_roofline": {"bound": "valu_fp64", "kernel": "k_rays", "achieved": round(achieved_tf, 3),
+                                 "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TF,
+                                 "flops_per_launch": ray_flops_per_launch},
+            "kernels_ms": {"k_dyn1": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
+            "episodes_ended": ep[2],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(pool, widths, budget_s=args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/* rx.h -- C ABI of the MI355X racing-env engine (librx.so).
+ *
+ * The reference (LucasHJin/self-play-racing) is pure Python and has no FFI; its
+ * hot path is the per-env Gymnasium step loop that agent/ppo.py drives through
+ * gymnasium.vector.SyncVectorEnv.  This header is the boundary a maintainer
+ * binds (ctypes stub: INTEGRATION.md) to replace that loop with one batched
+ * device call.  Each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Every function returns RX_OK (0) or a negative RX_E* code; rx_last_error()
+ *    returns a thread-local message for the last failure on this thread.
+ *  - "dev" pointers are device memory owned by the CALLER (e.g. torch tensors);
+ *    the library never frees them.  Host arrays are read during the call only.
+ *  - Work is enqueued on the caller's stream (a hipStream_t passed as void*,
+ *    NULL = the legacy default stream) with no host synchronisation, so the
+ *    step can sit inside a captured hipGraph.
+ *  - One host thread per handle; handles are independent (one per GPU rank).
+ *  - Agents: A = 1 (environment/racing_env.py RacingEnv) or A = 2
+ *    (environment/multi_racing_env.py MultiRacingEnv with 2 cars).
+ *    Observation width D = n_sensors + 4 + 4*(A-1)   (racing_env.py:37-42,
+ *    multi_racing_env.py:204).
+ *  - All env arithmetic is binary64 in the reference's operation order; see
+ *    DESIGN.md §Parity for the two libm calls (sin/cos, pow(x,2)) whose
+ *    results may differ from glibc's by 1 ulp.
+ */
+#ifndef RX_H_
+#define RX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RX_OK 0
+#define RX_EINVAL (-1)   /* bad argument / shape / state */
+#define RX_EHIP (-2)     /* HIP runtime error */
+#define RX_ENOMEM (-3)   /* device allocation failed */
+#define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
+
+#define RX_ABI_VERSION 1
+
+/* state flag bits (rx_state.flags, per agent) */
+#define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
+#define RX_F_FINISHED 2u     /* Car.finished                     racing_env.py:147 */
+#define RX_F_CP25 4u         /* checkpoints[0.25]                racing_env.py:21-25 */
+#define RX_F_CP50 8u         /* checkpoints[0.50] */
+#define RX_F_CP75 16u        /* checkpoints[0.75] */
+#define RX_F_HAS_CRASHED 32u /* agents_data['has_crashed']       multi_racing_env.py:313,358-360 */
+/* env flag bits (rx_state.env_flags, per env) */
+#define RX_EF_PENDING_RESET 1u /* episode ended last step: next-step autoreset */
+
+/* autoreset modes (gymnasium 1.x SyncVectorEnv: NEXT_STEP is its default) */
+#define RX_AUTORESET_NEXT_STEP 0 /* step after a terminal one resets, reward 0 */
+#define RX_AUTORESET_SAME_STEP 1 /* terminal step returns the reset obs (SB3 style) */
+#define RX_AUTORESET_DISABLED 2  /* caller resets explicitly (rx_reset) */
+
+/* info columns (rx_io.info, f64 [N][A][RX_INFO_W]) */
+#define RX_INFO_W 4
+#define RX_INFO_SPEED 0          /* info['speed']          racing_env.py:80 */
+#define RX_INFO_PROGRESS 1       /* info['progress'] (1.0 once finished) :81,158-159 */
+#define RX_INFO_PROGRESS_DELTA 2 /* info['progress_delta'] :157 (single-agent) */
+#define RX_INFO_PLACEMENT 3      /* info['placement'] (0 = none) multi_racing_env.py:425 */
+
+typedef struct rx_env rx_env;
+
+typedef struct {
+  int32_t n_envs;          /* N */
+  int32_t n_agents;        /* A: 1 or 2 */
+  int32_t n_sensors;       /* rays per agent (11 in train.py:47-49,94-101) */
+  int32_t max_steps;       /* truncation, 3000 (racing_env.py:162) */
+  int32_t autoreset;       /* RX_AUTORESET_* */
+  int32_t device;          /* HIP device ordinal */
+  uint64_t seed;           /* device RNG (two-car start-slot shuffle) */
+  double sensor_half_cone; /* pi/3 (racing_env.py:45) or pi/2 (multi_racing_env.py:50) */
+  double speed_weight;     /* RacingEnv.speed_weight, 8.0 (racing_env.py:9,26) */
+} rx_config;
+
+/* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
+ * agent-minor: element e*A + a.  Mirrors Car (car.py:15-24), RacingEnv
+ * (racing_env.py:17-26), MultiRacingEnv.agents_data (multi_racing_env.py:
+ * 186-191) and RecordEpisodeStatistics' episode counters. */
+typedef struct {
+  double* x;             /* [N*A] */
+  double* y;             /* [N*A] */
+  double* angle;         /* [N*A] */
+  double* vx;            /* [N*A] */
+  double* vy;            /* [N*A] */
+  double* progress;      /* [N*A] Car.progress */
+  double* last_progress; /* [N*A] */
+  double* last_steering; /* [N*A] */
+  int32_t* finished_step;/* [N*A] -1 = None (A==2 only; may be NULL for A==1) */
+  uint8_t* flags;        /* [N*A] RX_F_* */
+  int32_t* steps;        /* [N] */
+  int32_t* track;        /* [N] track slot (read-only for the kernels; set by rx_assign) */
+  uint8_t* env_flags;    /* [N] RX_EF_* */
+  double* ep_return;     /* [N] episode return of agent 0 */
+  int32_t* ep_length;    /* [N] */
+  const double* speed_weight; /* [N] per-env RacingEnv.speed_weight, or NULL = rx_config.speed_weight */
+} rx_state;
+
+/* One step's inputs/outputs, caller-owned device memory.  NULL = not wanted
+ * (except actions/obs, which are required). */
+typedef struct {
+  const float* actions;  /* [N][A][2] float32, as the Box(float32) action space */
+  float* obs;            /* [N][A][D] float32 */
+  float* reward;         /* [N][A] float32 (rollout buffer dtype, agent/ppo.py:116-117) */
+  double* reward64;      /* [N][A] float64 (SyncVectorEnv's reward dtype) */
+  uint8_t* terminated;   /* [N] */
+  uint8_t* truncated;    /* [N] */
+  float* done_f32;       /* [N] float(terminated | truncated): next_done, agent/ppo.py:120 */
+  double* info;          /* [N][A][RX_INFO_W] */
+  uint8_t* ep_done;      /* [N] an episode ended this step (infos['_episode']) */
+  double* ep_stats;      /* [3] += (sum return, sum length, count) of episodes ended */
+} rx_io;
+
+const char* rx_last_error(void);
+int rx_abi_version(void);
+
+/* Create/destroy a handle.  Replaces gym.vector.SyncVectorEnv([...]) construction,
+ * agent/ppo.py:70,85-95. */
+int rx_create(const rx_config* cfg, rx_env** out);
+int rx_destroy(rx_env* h);
+
+/* Host copy of the sensor angle offsets the kernels use: [n_sensors] =
+ * np.linspace(-half_cone, half_cone, n_sensors) (racing_env.py:45). */
+int rx_sensor_angles(const rx_env* h, double* out);
+
+/* Track table (host arrays, copied to the device).  Replaces the per-env
+ * Track.__init__ geometry (environment/track.py:61-148): slot k has
+ * W_k = wp_off[k+1]-wp_off[k] waypoints and 2*W_k boundary segments.
+ *   wp_off int32 [n+1];  wp, nrm f64 [Wtot][2];
+ *   seg f64 [2*Wtot][4] = (start.x, start.y, v2.x, v2.y): left boundary
+ *       segments then right ones, per slot (track.py:134-148);
+ *   meta f64 [n][8] = start x, y, angle (Track.get_start_pos, track.py:154-157),
+ *       track_width, max_track_distance (track.py:88-91), normals[0].x,
+ *       normals[0].y, 0. */
+int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* nrm,
+                     const double* seg, const double* meta);
+
+/* Assign a track slot to every env (host int32 [N]); also written to
+ * state.track.  Replaces Track(track_pool, track_id, track_width) per env
+ * (train.py:47-49,94-101).  Groups envs by slot so a wavefront shares one
+ * track (segment loads become scalar/broadcast). */
+int rx_assign(rx_env* h, const int32_t* track_of_env);
+
+/* Bind the caller-owned device state (pointers are kept until re-bound). */
+int rx_bind_state(rx_env* h, const rx_state* st);
+
+int rx_set_speed_weight(rx_env* h, double speed_weight);
+
+/* Reset envs (mask: device uint8 [N], NULL = all).  Replaces
+ * SyncVectorEnv.reset -> RacingEnv.reset (racing_env.py:86-102) /
+ * MultiRacingEnv.reset (multi_racing_env.py:118-153).  Writes obs (and zeros
+ * reward/terminated/truncated/done_f32 of the reset envs when given). */
+int rx_reset(rx_env* h, const uint8_t* mask, const rx_io* io, void* stream);
+
+/* One vectorised step.  Replaces SyncVectorEnv.step -> RecordEpisodeStatistics
+ * -> RacingEnv.step (racing_env.py:104-167) / SelfPlayWrapper.step ->
+ * MultiRacingEnv.step (multi_racing_env.py:213-269), with the configured
+ * autoreset semantics. */
+int rx_step(rx_env* h, const rx_io* io, void* stream);
+
+/* rx_step split into its two kernels, for per-kernel timing with stream
+ * events: phases bit 0 = dynamics/reward/done/autoreset (k_dyn), bit 1 =
+ * raycast observations (k_rays).  rx_step == phases 3.  Running bit 1 alone
+ * recomputes the ray observations of the current state. */
+#define RX_PHASE_DYNAMICS 1
+#define RX_PHASE_RAYS 2
+int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
+
+/* GAE (agent/ppo.py:134-154), float32, bit-exact lane-per-env recurrence.
+ * rewards/values/dones [T][N]; next_value/next_done [N]; adv/returns [T][N]. */
+int rx_gae(int32_t T, int32_t N, const float* rewards, const float* values, const float* dones,
+           const float* next_value, const float* next_done, double gamma, double gae_lambda, float* advantages,
+           float* returns, void* stream);
+
+/* Same recurrence evaluated as a wavefront-parallel affine scan over T
+ * (chunks of T per lane, combined with a 64-lane prefix scan): for few envs
+ * and long horizons.  Not bit-exact (different association); |error| <=
+ * ~1e-6 * max|A| (tests/test_gae_gpu.py). */
+int rx_gae_scan(int32_t T, int32_t N, const float* rewards, const float* values, const float* dones,
+                const float* next_value, const float* next_done, double gamma, double gae_lambda, float* advantages,
+                float* returns, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RX_H_ */

@@ -1,0 +1,312 @@
+// rx_api.cpp -- C ABI (include/rx.h): handle lifetime, argument validation,
+// track-table upload, env->wavefront grouping, launches.
+//
+// Everything that allocates or copies synchronously (rx_upload_tracks,
+// rx_assign) happens outside the step path; rx_reset / rx_step / rx_gae only
+// enqueue kernels on the caller's stream, so they can be graph-captured.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "rx.h"
+#include "rx_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define RX_HIP(call)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) return fail(RX_EHIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+template <class T>
+int upload(DevBuf<T>& b, const T* host, size_t n) {
+  if (n > b.n) {
+    b.release();
+    if (hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+      b.p = nullptr;
+      return fail(RX_ENOMEM, "hipMalloc(%zu bytes) failed", n * sizeof(T));
+    }
+    b.n = n;
+  }
+  if (n) RX_HIP(hipMemcpy(b.p, host, n * sizeof(T), hipMemcpyHostToDevice));
+  return RX_OK;
+}
+
+}  // namespace
+
+struct rx_env {
+  rx_config cfg{};
+  int D = 0;
+  // track table
+  int32_t n_tracks = 0;
+  std::vector<int32_t> wp_off_h;
+  DevBuf<int32_t> wp_off;
+  DevBuf<double> wp, nrm, seg, meta;
+  // assignment
+  bool assigned = false;
+  DevBuf<int32_t> perm;
+  DevBuf<rx_wave> dyn_waves, ray_waves;
+  int32_t n_dyn_waves = 0, n_ray_waves = 0;
+  DevBuf<double> rel_angles;
+  std::vector<double> rel_angles_h;
+  // state
+  bool bound = false;
+  rx_state st{};
+  uint64_t calls = 0;
+};
+
+extern "C" {
+
+const char* rx_last_error(void) { return g_err.c_str(); }
+int rx_abi_version(void) { return RX_ABI_VERSION; }
+
+int rx_create(const rx_config* cfg, rx_env** out) {
+  if (!cfg || !out) return fail(RX_EINVAL, "rx_create: null argument");
+  *out = nullptr;
+  if (cfg->n_envs <= 0) return fail(RX_EINVAL, "n_envs must be > 0 (got %d)", cfg->n_envs);
+  if (cfg->n_agents != 1 && cfg->n_agents != 2) return fail(RX_EINVAL, "n_agents must be 1 or 2 (got %d)", cfg->n_agents);
+  if (cfg->n_sensors <= 0 || cfg->n_sensors > 256) return fail(RX_EINVAL, "n_sensors out of range (%d)", cfg->n_sensors);
+  if (cfg->max_steps <= 0) return fail(RX_EINVAL, "max_steps must be > 0");
+  if (cfg->autoreset < RX_AUTORESET_NEXT_STEP || cfg->autoreset > RX_AUTORESET_DISABLED)
+    return fail(RX_EINVAL, "bad autoreset mode %d", cfg->autoreset);
+  if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
+    return fail(RX_EINVAL, "n_envs * n_agents * n_sensors overflows int32");
+  int ndev = 0;
+  RX_HIP(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(RX_EINVAL, "device %d not present (%d devices)", cfg->device, ndev);
+  RX_HIP(hipSetDevice(cfg->device));
+  rx_env* h = new rx_env();
+  h->cfg = *cfg;
+  if (!(h->cfg.speed_weight == h->cfg.speed_weight)) h->cfg.speed_weight = 8.0;
+  h->D = cfg->n_sensors + 4 + 4 * (cfg->n_agents - 1);
+  // sensor angles = np.linspace(-c, c, n) (racing_env.py:45, multi_racing_env.py:50):
+  // numpy computes start + i*step with step = (stop-start)/(n-1), and sets the
+  // last element to stop exactly.
+  {
+    const int n = cfg->n_sensors;
+    std::vector<double> rel(n);
+    const double start = -cfg->sensor_half_cone, stop = cfg->sensor_half_cone;
+    if (n == 1) {
+      rel[0] = start;
+    } else {
+      const double div = (double)(n - 1);
+      const double delta = stop - start;
+      const double step = delta / div;
+      for (int i = 0; i < n; ++i) rel[i] = (double)i * step + start;
+      rel[n - 1] = stop;
+    }
+    h->rel_angles_h = rel;
+    int rc = upload(h->rel_angles, rel.data(), rel.size());
+    if (rc) {
+      delete h;
+      return rc;
+    }
+  }
+  *out = h;
+  return RX_OK;
+}
+
+int rx_sensor_angles(const rx_env* h, double* out) {
+  if (!h || !out) return fail(RX_EINVAL, "rx_sensor_angles: null argument");
+  std::copy(h->rel_angles_h.begin(), h->rel_angles_h.end(), out);
+  return RX_OK;
+}
+
+int rx_destroy(rx_env* h) {
+  if (!h) return RX_OK;
+  (void)hipSetDevice(h->cfg.device);
+  h->wp_off.release();
+  h->wp.release();
+  h->nrm.release();
+  h->seg.release();
+  h->meta.release();
+  h->perm.release();
+  h->dyn_waves.release();
+  h->ray_waves.release();
+  h->rel_angles.release();
+  delete h;
+  return RX_OK;
+}
+
+int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* nrm,
+                     const double* seg, const double* meta) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (n_tracks <= 0 || !wp_off || !wp || !nrm || !seg || !meta) return fail(RX_EINVAL, "rx_upload_tracks: bad arguments");
+  if (wp_off[0] != 0) return fail(RX_EINVAL, "wp_off[0] must be 0");
+  for (int k = 0; k < n_tracks; ++k) {
+    const int W = wp_off[k + 1] - wp_off[k];
+    if (W < 2) return fail(RX_EINVAL, "track %d has %d waypoints (need >= 2)", k, W);
+    if (!(meta[8 * k + 3] >= 0)) return fail(RX_EINVAL, "track %d width invalid", k);
+    if (!(meta[8 * k + 4] > 0)) return fail(RX_EINVAL, "track %d max_track_distance must be > 0", k);
+  }
+  const size_t Wt = (size_t)wp_off[n_tracks];
+  RX_HIP(hipSetDevice(h->cfg.device));
+  int rc;
+  if ((rc = upload(h->wp_off, wp_off, (size_t)n_tracks + 1))) return rc;
+  if ((rc = upload(h->wp, wp, 2 * Wt))) return rc;
+  if ((rc = upload(h->nrm, nrm, 2 * Wt))) return rc;
+  if ((rc = upload(h->seg, seg, 8 * Wt))) return rc;
+  if ((rc = upload(h->meta, meta, 8 * (size_t)n_tracks))) return rc;
+  h->wp_off_h.assign(wp_off, wp_off + n_tracks + 1);
+  h->n_tracks = n_tracks;
+  h->assigned = false;  // slots may have changed meaning: require rx_assign again
+  return RX_OK;
+}
+
+int rx_assign(rx_env* h, const int32_t* track_of_env) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (h->n_tracks <= 0) return fail(RX_ESTATE, "rx_assign before rx_upload_tracks");
+  if (!track_of_env) return fail(RX_EINVAL, "track_of_env is null");
+  const int N = h->cfg.n_envs, A = h->cfg.n_agents, R = h->cfg.n_sensors;
+  for (int e = 0; e < N; ++e)
+    if (track_of_env[e] < 0 || track_of_env[e] >= h->n_tracks)
+      return fail(RX_EINVAL, "env %d assigned to track %d (have %d)", e, track_of_env[e], h->n_tracks);
+  // group envs by slot (stable: env order inside a slot is preserved)
+  std::vector<int32_t> perm(N);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return track_of_env[a] < track_of_env[b]; });
+  std::vector<rx_wave> dyn, ray;
+  int g0 = 0;
+  while (g0 < N) {
+    const int k = track_of_env[perm[g0]];
+    int g1 = g0;
+    while (g1 < N && track_of_env[perm[g1]] == k) ++g1;
+    const int ng = g1 - g0;
+    for (int s = 0; s < ng; s += 64) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(64, ng - s)});
+    const long long tasks = (long long)ng * A * R;
+    for (long long s = 0; s < tasks; s += 64)
+      ray.push_back(rx_wave{k, g0, (int32_t)s, (int32_t)std::min<long long>(64, tasks - s)});
+    g0 = g1;
+  }
+  RX_HIP(hipSetDevice(h->cfg.device));
+  int rc;
+  if ((rc = upload(h->perm, perm.data(), perm.size()))) return rc;
+  if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
+  if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
+  h->n_dyn_waves = (int32_t)dyn.size();
+  h->n_ray_waves = (int32_t)ray.size();
+  h->assigned = true;
+  if (h->bound && h->st.track) RX_HIP(hipMemcpy(h->st.track, track_of_env, N * sizeof(int32_t), hipMemcpyHostToDevice));
+  return RX_OK;
+}
+
+int rx_bind_state(rx_env* h, const rx_state* st) {
+  if (!h || !st) return fail(RX_EINVAL, "rx_bind_state: null argument");
+  if (!st->x || !st->y || !st->angle || !st->vx || !st->vy || !st->progress || !st->last_progress ||
+      !st->last_steering || !st->flags || !st->steps || !st->track || !st->env_flags || !st->ep_return ||
+      !st->ep_length)
+    return fail(RX_EINVAL, "rx_bind_state: every state array except finished_step is required");
+  if (h->cfg.n_agents == 2 && !st->finished_step) return fail(RX_EINVAL, "rx_bind_state: finished_step required for 2 agents");
+  h->st = *st;
+  h->bound = true;
+  return RX_OK;
+}
+
+int rx_set_speed_weight(rx_env* h, double w) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (!(w == w)) return fail(RX_EINVAL, "speed_weight is NaN");
+  h->cfg.speed_weight = w;
+  return RX_OK;
+}
+
+static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
+  if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (!io) return fail(RX_EINVAL, "io is null");
+  if (h->n_tracks <= 0) return fail(RX_ESTATE, "no track table (rx_upload_tracks)");
+  if (!h->assigned) return fail(RX_ESTATE, "no env assignment (rx_assign)");
+  if (!h->bound) return fail(RX_ESTATE, "no state bound (rx_bind_state)");
+  if (!io->obs) return fail(RX_EINVAL, "io->obs is required");
+  if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
+  rx_kargs a{};
+  a.tr = rx_track_view{h->wp_off.p, h->wp.p, h->nrm.p, h->seg.p, h->meta.p};
+  a.st = h->st;
+  a.io = *io;
+  a.dyn_waves = h->dyn_waves.p;
+  a.ray_waves = h->ray_waves.p;
+  a.perm = h->perm.p;
+  a.rel_angles = h->rel_angles.p;
+  a.reset_mask = mask;
+  a.n_dyn_waves = h->n_dyn_waves;
+  a.n_ray_waves = h->n_ray_waves;
+  a.n_sensors = h->cfg.n_sensors;
+  a.D = h->D;
+  a.max_steps = h->cfg.max_steps;
+  a.autoreset = h->cfg.autoreset;
+  a.mode = mode;
+  a.speed_weight = h->cfg.speed_weight;
+  a.seed = h->cfg.seed;
+  a.call = ++h->calls;
+  if (!(phases & RX_PHASE_DYNAMICS)) a.n_dyn_waves = 0;
+  if (!(phases & RX_PHASE_RAYS)) a.n_ray_waves = 0;
+  const int rc = rx_launch_step(&a, h->cfg.n_agents, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_reset(rx_env* h, const uint8_t* mask, const rx_io* io, void* stream) {
+  return launch(h, io, RX_MODE_RESET, mask, stream);
+}
+
+int rx_step(rx_env* h, const rx_io* io, void* stream) { return launch(h, io, RX_MODE_STEP, nullptr, stream); }
+
+int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream) {
+  return launch(h, io, RX_MODE_STEP, nullptr, stream, phases);
+}
+
+static int gae(int32_t T, int32_t N, const float* r, const float* v, const float* d, const float* nv, const float* nd,
+               double gamma, double lam, float* adv, float* ret, int scan, void* stream) {
+  if (T <= 0 || N <= 0) return fail(RX_EINVAL, "rx_gae: T=%d N=%d must be > 0", T, N);
+  if (!r || !v || !d || !nv || !nd || !adv || !ret) return fail(RX_EINVAL, "rx_gae: null buffer");
+  if ((long long)T * N > 0x7fffffffffffLL) return fail(RX_EINVAL, "rx_gae: T*N too large");
+  // agent/ppo.py:149,151: c["gamma"] * nnt is float32(gamma) * nnt; the Python
+  // double product gamma*lambda is rounded to float32 once.
+  const float g = (float)gamma;
+  const float gl = (float)(gamma * lam);
+  const int rc = rx_launch_gae(T, N, r, v, d, nv, nd, g, gl, adv, ret, scan, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "gae launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_gae(int32_t T, int32_t N, const float* r, const float* v, const float* d, const float* nv, const float* nd,
+           double gamma, double lam, float* adv, float* ret, void* stream) {
+  return gae(T, N, r, v, d, nv, nd, gamma, lam, adv, ret, 0, stream);
+}
+
+int rx_gae_scan(int32_t T, int32_t N, const float* r, const float* v, const float* d, const float* nv,
+                const float* nd, double gamma, double lam, float* adv, float* ret, void* stream) {
+  return gae(T, N, r, v, d, nv, nd, gamma, lam, adv, ret, 1, stream);
+}
+
+}  // extern "C"

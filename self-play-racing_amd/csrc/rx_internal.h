@@ -1,0 +1,55 @@
+// rx_internal.h -- kernel argument block shared by rx_api.cpp (host) and
+// rx_kernels.hip (device).  Not part of the public ABI (include/rx.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rx.h"
+
+#define RX_MODE_STEP 0
+#define RX_MODE_RESET 1
+
+// One wavefront's work item: 64 consecutive tasks of ONE track slot.
+//  dyn waves: lane -> env perm[perm_start + lane], lane < count
+//  ray waves: lane -> task task_start + lane (task = env_local*A*R + agent*R + ray),
+//             env = perm[perm_start + env_local]
+struct rx_wave {
+  int32_t track;
+  int32_t perm_start;
+  int32_t task_start;
+  int32_t count;
+};
+
+struct rx_track_view {
+  const int32_t* wp_off;  // [n+1]
+  const double* wp;       // [Wtot][2]
+  const double* nrm;      // [Wtot][2]
+  const double* seg;      // [2*Wtot][4]
+  const double* meta;     // [n][8]
+};
+
+struct rx_kargs {
+  rx_track_view tr;
+  rx_state st;
+  rx_io io;
+  const rx_wave* dyn_waves;
+  const rx_wave* ray_waves;
+  const int32_t* perm;
+  const double* rel_angles;   // [n_sensors]
+  const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
+  int32_t n_dyn_waves;
+  int32_t n_ray_waves;
+  int32_t n_sensors;
+  int32_t D;
+  int32_t max_steps;
+  int32_t autoreset;
+  int32_t mode;
+  int32_t pad_;
+  double speed_weight;
+  uint64_t seed;
+  uint64_t call;
+};
+
+extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, hipStream_t s);
+extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
+                             const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);

@@ -1,0 +1,781 @@
+// rx_kernels.hip -- batched racing-env step + GAE kernels for gfx950 (MI355X).
+//
+// Design:
+//  * Envs are grouped by track slot on the host (rx_assign); every wavefront
+//    works on ONE slot, so the track's waypoints/segments are wave-uniform and
+//    are read with scalar loads (s_load) into SGPRs: no LDS staging, no bank
+//    conflicts, and the VALU ops take the segment coordinates as SGPR
+//    operands.  The wave tables (WaveEntry) are built once per assignment.
+//  * k_dyn: one lane per env.  Car dynamics, progress/collision argmins over the
+//    waypoints (all 5 query points -- centre + 4 corners -- in ONE pass over
+//    the wave-uniform waypoint stream), reward, done, autoreset, episode stats,
+//    and the non-ray observation columns.
+//  * k_rays: one lane per (env, agent, ray): 11x more lanes than envs, so even
+//    65,536 envs give ~11 waves per SIMD for latency hiding.  Exact,
+//    division-free hit test per segment (derivation in DESIGN.md §Raycast);
+//    one f64 division per HIT segment only.
+//  * Arithmetic: binary64, the reference's operation order, compiled with
+//    -ffp-contract=off; explicit FMAs only where the reference calls np.dot.
+//    sin/cos = rx_sincos (correctly rounded), pow(x,2) = x*x (rx_math.h).
+//  * k_gae / k_gae_scan: agent/ppo.py:134-154 in float32.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rx.h"
+#include "rx_internal.h"
+#include "rx_math.h"
+
+#define RX_TWO_PI 6.283185307179586  // 2*np.pi, environment/car.py:54
+#define RX_MAX_SPEED 30.0
+#define RX_DT 0.05
+#define RX_MAX_RANGE 50.0
+
+namespace {
+
+struct Car {
+  double x, y, angle, vx, vy, progress;
+  bool crashed;
+};
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// f32 np.clip with Python-float bounds (stays float32 under NEP 50)
+__device__ __forceinline__ float clipf(float a, float lo, float hi) {
+  float y = a < lo ? lo : a;
+  return y > hi ? hi : y;
+}
+
+// Car.get_corners -- environment/car.py:26-43, given cos/sin of the angle
+__device__ __forceinline__ void corners(double x, double y, double c, double s, double cx[4], double cy[4]) {
+  // local (2,1), (2,-1), (-2,-1), (-2,1): products by +-2 / +-1 are exact
+  cx[0] = (c * 2.0 + (-s) * 1.0) + x;
+  cy[0] = (s * 2.0 + c * 1.0) + y;
+  cx[1] = (c * 2.0 + (-s) * -1.0) + x;
+  cy[1] = (s * 2.0 + c * -1.0) + y;
+  cx[2] = (c * -2.0 + (-s) * -1.0) + x;
+  cy[2] = (s * -2.0 + c * -1.0) + y;
+  cx[3] = (c * -2.0 + (-s) * 1.0) + x;
+  cy[3] = (s * -2.0 + c * 1.0) + y;
+}
+
+// Argmin over a wave-uniform waypoint stream for NP query points per lane
+// (Track.closest_waypoint_idx, environment/track.py:150-152: array `**2` is a
+// square, first index on ties).  act[p] masks points whose car is frozen.
+template <int NP>
+__device__ __forceinline__ void argmin_pts(const double2* __restrict__ wp, int W, const double px[NP],
+                                           const double py[NP], int idx[NP]) {
+  double best[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    best[p] = __builtin_inf();
+    idx[p] = 0;
+  }
+#pragma unroll 2
+  for (int i = 0; i < W; ++i) {
+    const double2 w = wp[i];  // uniform address -> s_load_dwordx4
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      double dx = w.x - px[p], dy = w.y - py[p];
+      double d = dx * dx + dy * dy;
+      bool lt = d < best[p];
+      best[p] = lt ? d : best[p];
+      idx[p] = lt ? i : idx[p];
+    }
+  }
+}
+
+// Car.update -- environment/car.py:45-80, minus the argmins (done by the
+// caller for all cars of the lane in one pass).  Returns cos/sin of the new
+// angle and the 4 corners.
+__device__ __forceinline__ void car_kinematics(Car& c, double steering, double throttle, double cs[2],
+                                               double cx[4], double cy[4]) {
+  double angular_velocity = steering * 3.0;
+  double ang = c.angle + (angular_velocity * RX_DT);
+  ang = rx_pymod(ang, RX_TWO_PI);
+  double s, co;
+  rx_sincos(ang, &s, &co);
+  double vf = c.vx * co + c.vy * s;
+  double vl = c.vx * (-s) + c.vy * co;
+  double accel_forward = throttle * 10.0;
+  vf = (vf + (accel_forward * RX_DT)) * 0.985;
+  vl = (vl * 0.85) * 0.9;
+  double vx = vf * co - vl * s;
+  double vy = vf * s + vl * co;
+  double speed = __builtin_sqrt(rx_sq(vx) + rx_sq(vy));
+  if (speed > RX_MAX_SPEED) {
+    double scale = RX_MAX_SPEED / speed;
+    vx *= scale;
+    vy *= scale;
+  }
+  c.angle = ang;
+  c.vx = vx;
+  c.vy = vy;
+  c.x = c.x + (vx * RX_DT);
+  c.y = c.y + (vy * RX_DT);
+  cs[0] = co;
+  cs[1] = s;
+  corners(c.x, c.y, co, s, cx, cy);
+}
+
+// Track.check_collision for one corner given its argmin -- track.py:163-171
+__device__ __forceinline__ bool corner_out(const double2* __restrict__ wp, const double2* __restrict__ nrm, int idx,
+                                           double cx, double cy, double width) {
+  double2 w = wp[idx];
+  double2 n = nrm[idx];
+  double px = cx - w.x, py = cy - w.y;
+  double dist = __builtin_fabs(rx_dot2_np(px, py, n.x, n.y));
+  return dist > width;
+}
+
+__device__ __forceinline__ double speed_of(double vx, double vy) { return __builtin_sqrt(rx_sq(vx) + rx_sq(vy)); }
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// ============================================================ k_dyn, A == 1
+// RacingEnv.step / reset (environment/racing_env.py:86-167) for one env per
+// lane, plus RecordEpisodeStatistics and SyncVectorEnv autoreset.
+__global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (wave >= a.n_dyn_waves) return;
+  const rx_wave we = a.dyn_waves[wave];
+  const int lane = threadIdx.x & 63;
+  const int k = uniform(we.track);
+  const int wp0 = uniform(a.tr.wp_off[k]);
+  const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
+  const double2* __restrict__ wp = reinterpret_cast<const double2*>(a.tr.wp) + wp0;
+  const double2* __restrict__ nrm = reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
+  const double* __restrict__ meta = a.tr.meta + 8 * k;
+  const double width = meta[3];
+  if (lane >= we.count) return;
+  const int e = a.perm[we.perm_start + lane];
+
+  const rx_state& S = a.st;
+  uint8_t ef = S.env_flags[e];
+  uint8_t fl = S.flags[e];
+  Car c{S.x[e], S.y[e], S.angle[e], S.vx[e], S.vy[e], S.progress[e], (fl & RX_F_CRASHED) != 0};
+  double last_steering = S.last_steering[e];
+  bool do_reset;
+  if (a.mode == RX_MODE_RESET)
+    do_reset = (a.reset_mask == nullptr) || a.reset_mask[e];
+  else
+    do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
+  const bool stepping = (a.mode == RX_MODE_STEP) && !do_reset;
+
+  double reward = 0.0, pd = 0.0;
+  bool term = false, trunc = false;
+  int steps = S.steps[e];
+  // ---------------------------------------------------------------- step
+  // Lanes that step run the argmin loop together; reset lanes are masked.
+  bool moving = stepping && !c.crashed;
+  double cs[2], cx[4], cy[4];
+  double steering = 0.0;
+  if (stepping) {
+    const float2 act = reinterpret_cast<const float2*>(a.io.actions)[e];
+    steering = (double)clipf(act.x, -1.0f, 1.0f);  // racing_env.py:106
+    double throttle = (double)clipf(act.y, 0.0f, 1.0f);
+    last_steering = steering;
+    if (moving) car_kinematics(c, steering, throttle, cs, cx, cy);
+  }
+  if (moving) {
+    double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
+    double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
+    int idx[5];
+    argmin_pts<5>(wp, W, px, py, idx);
+    c.progress = (double)idx[0] / (double)W;  // track.py:159-161
+    bool out = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out = out || corner_out(wp, nrm, idx[q + 1], cx[q], cy[q], width);
+    c.crashed = out;
+  }
+  if (stepping) {
+    steps += 1;
+    const double last_progress = S.last_progress[e];
+    const double p = c.progress;
+    pd = p - last_progress;  // racing_env.py:112-116
+    if (last_progress > 0.9 && p < 0.1)
+      pd = (1.0 - last_progress) + p;
+    else if (last_progress < 0.1 && p > 0.9)
+      pd = -((1.0 - p) + last_progress);
+    double r = pd * 200;
+    if (!(fl & RX_F_CP25) && 0.25 <= p && p < 0.35) { fl |= RX_F_CP25; r += 20; }
+    if ((fl & RX_F_CP25) && !(fl & RX_F_CP50) && 0.50 <= p && p < 0.60) { fl |= RX_F_CP50; r += 20; }
+    if ((fl & RX_F_CP50) && !(fl & RX_F_CP75) && 0.75 <= p && p < 0.85) { fl |= RX_F_CP75; r += 20; }
+    if (!c.crashed && pd > 0) {  // :137-140
+      double ratio = rx_clip(speed_of(c.vx, c.vy) / RX_MAX_SPEED, 0.0, 1.0);
+      r += ratio * (S.speed_weight ? S.speed_weight[e] : a.speed_weight);
+    }
+    if (c.crashed) r -= 60;
+    const uint8_t all_cp = RX_F_CP25 | RX_F_CP50 | RX_F_CP75;
+    if ((fl & all_cp) == all_cp && last_progress > 0.9 && p < 0.1 && pd > 0) {  // :145-150
+      fl |= RX_F_FINISHED;
+      r += 100;
+      double tb = 200 - ((double)steps / 10);
+      if (tb > 0) r += tb;
+    }
+    fl = (uint8_t)((fl & ~RX_F_CRASHED) | (c.crashed ? RX_F_CRASHED : 0));
+    reward = r;
+    term = c.crashed || (fl & RX_F_FINISHED);
+    trunc = steps >= a.max_steps;
+    // RecordEpisodeStatistics.step
+    double epr = S.ep_return[e] + r;
+    int epl = S.ep_length[e] + 1;
+    S.ep_return[e] = epr;
+    S.ep_length[e] = epl;
+    const bool ended = term || trunc;
+    if (a.io.ep_done) a.io.ep_done[e] = ended;
+    if (ended && a.io.ep_stats) {
+      atomicAdd(&a.io.ep_stats[0], epr);
+      atomicAdd(&a.io.ep_stats[1], (double)epl);
+      atomicAdd(&a.io.ep_stats[2], 1.0);
+    }
+    if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
+    if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;  // reset AFTER the outputs
+  } else if (a.io.ep_done) {
+    a.io.ep_done[e] = 0;
+  }
+  // info of the stepped state (racing_env.py:77-84,156-159)
+  if (a.io.info) {
+    double* inf = a.io.info + (size_t)e * RX_INFO_W;
+    inf[RX_INFO_SPEED] = speed_of(c.vx, c.vy);
+    inf[RX_INFO_PROGRESS] = (fl & RX_F_FINISHED) ? 1.0 : c.progress;
+    inf[RX_INFO_PROGRESS_DELTA] = pd;
+    inf[RX_INFO_PLACEMENT] = 0.0;
+  }
+  // ---------------------------------------------------------------- reset
+  if (do_reset) {  // RacingEnv.reset + Car.reset, racing_env.py:86-102, car.py:17-24
+    c.x = meta[0];
+    c.y = meta[1];
+    c.angle = meta[2];
+    c.vx = 0.0;
+    c.vy = 0.0;
+    c.progress = 0.0;
+    c.crashed = false;
+    fl = 0;
+    steps = 0;
+    last_steering = 0.0;
+    ef &= (uint8_t)~RX_EF_PENDING_RESET;
+    S.ep_return[e] = 0.0;
+    S.ep_length[e] = 0;
+    if (a.io.info && (a.mode == RX_MODE_RESET || a.autoreset == RX_AUTORESET_NEXT_STEP)) {
+      double* inf = a.io.info + (size_t)e * RX_INFO_W;
+      inf[RX_INFO_SPEED] = 0.0;
+      inf[RX_INFO_PROGRESS] = 0.0;
+      inf[RX_INFO_PROGRESS_DELTA] = 0.0;
+    }
+  }
+  if (stepping || do_reset) {
+    S.x[e] = c.x;
+    S.y[e] = c.y;
+    S.angle[e] = c.angle;
+    S.vx[e] = c.vx;
+    S.vy[e] = c.vy;
+    S.progress[e] = c.progress;
+    S.last_progress[e] = c.progress;  // racing_env.py:165 (0.0 after reset)
+    S.last_steering[e] = last_steering;
+    S.steps[e] = steps;
+    S.flags[e] = fl;
+    S.env_flags[e] = ef;
+  }
+  // ---------------------------------------------------------------- outputs
+  const bool wrote_step = stepping;  // reset-by-NEXT_STEP / explicit reset: reward 0, term = trunc = False
+  const float rf = wrote_step ? (float)reward : 0.0f;
+  if (a.io.reward) a.io.reward[e] = rf;
+  if (a.io.reward64) a.io.reward64[e] = wrote_step ? reward : 0.0;
+  const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
+  if (a.io.terminated) a.io.terminated[e] = t_out;
+  if (a.io.truncated) a.io.truncated[e] = u_out;
+  if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  // non-ray observation columns of the CURRENT state (racing_env.py:58-75)
+  {
+    double s, co;
+    rx_sincos(c.angle, &s, &co);
+    double vf = c.vx * co + c.vy * s;
+    double vl = (-c.vx) * s + c.vy * co;
+    float* o = a.io.obs + (size_t)e * a.D + a.n_sensors;
+    o[0] = (float)rx_clip(vf / RX_MAX_SPEED, -1.0, 1.0);
+    o[1] = (float)rx_clip(vl / RX_MAX_SPEED, -1.0, 1.0);
+    o[2] = (float)rx_clip(0.0 / 3.0, -1.0, 1.0);  // angular_velocity is always 0
+    o[3] = (float)last_steering;
+  }
+}
+
+// ============================================================ k_dyn, A == 2
+// MultiRacingEnv.step / reset (environment/multi_racing_env.py:118-269), one
+// env (both cars) per lane.
+__device__ double multi_reward(Car& c, uint8_t& fl, int32_t& finished_step, double last_progress, int steps) {
+  // MultiRacingEnv.calc_reward -- multi_racing_env.py:155-196
+  double p = c.progress;
+  double pd = p - last_progress;
+  if (last_progress > 0.9 && p < 0.1)
+    pd = (1.0 - last_progress) + p;
+  else if (last_progress < 0.1 && p > 0.9)
+    pd = -((1.0 - p) + last_progress);
+  double r = 0.0;
+  r += pd * 200;
+  if (!c.crashed && pd > 0) {
+    double ratio = rx_clip(speed_of(c.vx, c.vy) / RX_MAX_SPEED, 0.0, 1.0);
+    r += ratio * 18;
+  }
+  if (!(fl & RX_F_CP25) && 0.25 <= p && p < 0.35) { fl |= RX_F_CP25; r += 25; }
+  if ((fl & RX_F_CP25) && !(fl & RX_F_CP50) && 0.50 <= p && p < 0.60) { fl |= RX_F_CP50; r += 25; }
+  if ((fl & RX_F_CP50) && !(fl & RX_F_CP75) && 0.75 <= p && p < 0.85) { fl |= RX_F_CP75; r += 25; }
+  const uint8_t all_cp = RX_F_CP25 | RX_F_CP50 | RX_F_CP75;
+  if ((fl & all_cp) == all_cp && last_progress > 0.9 && p < 0.1 && pd > 0) {
+    fl |= RX_F_FINISHED;
+    finished_step = steps;
+    double tb = 300 - ((double)steps / 15);
+    r += 100 + (tb > 0 ? tb : 0.0);
+  }
+  if (c.crashed && !(fl & RX_F_HAS_CRASHED)) {
+    r -= 160;
+    fl |= RX_F_HAS_CRASHED;
+  }
+  return r;
+}
+
+// MultiCar.rectangles_intersect -- environment/multi_car.py:16-43
+__device__ __forceinline__ bool rect_intersect(const double ax[4], const double ay[4], const double bx[4],
+                                               const double by[4]) {
+  double axx[4], axy[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    axx[i] = -(ay[i + 1] - ay[i]);
+    axy[i] = ax[i + 1] - ax[i];
+    axx[2 + i] = -(by[i + 1] - by[i]);
+    axy[2 + i] = bx[i + 1] - bx[i];
+  }
+  bool sep = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double amax = -__builtin_inf(), amin = __builtin_inf(), bmax = -__builtin_inf(), bmin = __builtin_inf();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double pa = rx_dot2_np(ax[c], ay[c], axx[q], axy[q]);
+      double pb = rx_dot2_np(bx[c], by[c], axx[q], axy[q]);
+      amax = pa > amax ? pa : amax;
+      amin = pa < amin ? pa : amin;
+      bmax = pb > bmax ? pb : bmax;
+      bmin = pb < bmin ? pb : bmin;
+    }
+    sep = sep || (amax < bmin || bmax < amin);
+  }
+  return !sep;
+}
+
+__global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (wave >= a.n_dyn_waves) return;
+  const rx_wave we = a.dyn_waves[wave];
+  const int lane = threadIdx.x & 63;
+  const int k = uniform(we.track);
+  const int wp0 = uniform(a.tr.wp_off[k]);
+  const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
+  const double2* __restrict__ wp = reinterpret_cast<const double2*>(a.tr.wp) + wp0;
+  const double2* __restrict__ nrm = reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
+  const double* __restrict__ meta = a.tr.meta + 8 * k;
+  const double width = meta[3];
+  const double maxd = meta[4];
+  if (lane >= we.count) return;
+  const int e = a.perm[we.perm_start + lane];
+  const rx_state& S = a.st;
+
+  uint8_t ef = S.env_flags[e];
+  Car c[2];
+  uint8_t fl[2];
+  double last_steering[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = 2 * e + q;
+    fl[q] = S.flags[i];
+    c[q] = Car{S.x[i], S.y[i], S.angle[i], S.vx[i], S.vy[i], S.progress[i], (fl[q] & RX_F_CRASHED) != 0};
+    last_steering[q] = S.last_steering[i];
+  }
+  bool do_reset;
+  if (a.mode == RX_MODE_RESET)
+    do_reset = (a.reset_mask == nullptr) || a.reset_mask[e];
+  else
+    do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
+  const bool stepping = (a.mode == RX_MODE_STEP) && !do_reset;
+  int steps = S.steps[e];
+  double rw[2] = {0.0, 0.0};
+  int place[2] = {0, 0};
+  bool term = false, trunc = false;
+  if (stepping) {
+    const float4 act = reinterpret_cast<const float4*>(a.io.actions)[e];
+    const float av[4] = {act.x, act.y, act.z, act.w};
+    double cx[2][4], cy[2][4], cs[2][2];
+    bool mv[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // multi_racing_env.py:215-220
+      last_steering[q] = (double)clipf(av[2 * q], -1.0f, 1.0f);
+      const float thr = clipf((av[2 * q + 1] + 1.0f) / 2.0f, 0.0f, 1.0f);
+      mv[q] = !c[q].crashed;
+      if (mv[q]) car_kinematics(c[q], last_steering[q], (double)thr, cs[q], cx[q], cy[q]);
+    }
+    if (mv[0] || mv[1]) {
+      double px[10], py[10];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        px[5 * q] = c[q].x;
+        py[5 * q] = c[q].y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          px[5 * q + 1 + j] = cx[q][j];
+          py[5 * q + 1 + j] = cy[q][j];
+        }
+      }
+      int idx[10];
+      argmin_pts<10>(wp, W, px, py, idx);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (!mv[q]) continue;
+        c[q].progress = (double)idx[5 * q] / (double)W;
+        bool out = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out = out || corner_out(wp, nrm, idx[5 * q + 1 + j], cx[q][j], cy[q][j], width);
+        c[q].crashed = out;
+      }
+    }
+    // car-car contact, multi_racing_env.py:222-231 (corners of the current state)
+    {
+      double ax[4], ay[4], bx[4], by[4], s0, c0, s1, c1;
+      rx_sincos(c[0].angle, &s0, &c0);
+      rx_sincos(c[1].angle, &s1, &c1);
+      corners(c[0].x, c[0].y, c0, s0, ax, ay);
+      corners(c[1].x, c[1].y, c1, s1, bx, by);
+      if (rect_intersect(ax, ay, bx, by)) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          c[q].vx *= 0.92;
+          c[q].vy *= 0.92;
+          rw[q] = -5.0;
+        }
+      }
+    }
+    steps += 1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = 2 * e + q;
+      fl[q] = (uint8_t)((fl[q] & ~RX_F_CRASHED) | (c[q].crashed ? RX_F_CRASHED : 0));
+      int32_t fs = S.finished_step[i];
+      double r = multi_reward(c[q], fl[q], fs, S.last_progress[i], steps);
+      S.finished_step[i] = fs;
+      rw[q] = r + rw[q];  // calc_reward(i) + touching_penalties[i]
+    }
+    const bool any_fin = (fl[0] & RX_F_FINISHED) || (fl[1] & RX_F_FINISHED);
+    const bool all_crash = c[0].crashed && c[1].crashed;
+    term = any_fin || all_crash;
+    trunc = steps >= a.max_steps;
+    if (term || trunc) {  // place(), multi_racing_env.py:198-211,252-259
+      double sc[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int fs = S.finished_step[2 * e + q];
+        double v = (double)((fl[q] & RX_F_FINISHED) ? 10000 : 0) + c[q].progress * 100;
+        v = v + (double)(c[q].crashed ? 0 : 10);
+        v = v + 1.0 / (double)(fs > 0 ? fs : 10000);
+        sc[q] = v;
+      }
+      const int first = (sc[1] >= sc[0]) ? 1 : 0;  // sort(reverse=True): ties -> larger idx first
+      place[first] = 1;
+      place[1 - first] = 2;
+      rw[first] += 250;
+    }
+    double epr = S.ep_return[e] + rw[0];
+    int epl = S.ep_length[e] + 1;
+    S.ep_return[e] = epr;
+    S.ep_length[e] = epl;
+    const bool ended = term || trunc;
+    if (a.io.ep_done) a.io.ep_done[e] = ended;
+    if (ended && a.io.ep_stats) {
+      atomicAdd(&a.io.ep_stats[0], epr);
+      atomicAdd(&a.io.ep_stats[1], (double)epl);
+      atomicAdd(&a.io.ep_stats[2], 1.0);
+    }
+    if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
+    if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;
+  } else if (a.io.ep_done) {
+    a.io.ep_done[e] = 0;
+  }
+  if (a.io.info) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      double* inf = a.io.info + (size_t)(2 * e + q) * RX_INFO_W;
+      const bool keep = stepping;
+      inf[RX_INFO_SPEED] = keep ? speed_of(c[q].vx, c[q].vy) : 0.0;
+      inf[RX_INFO_PROGRESS] = keep ? ((fl[q] & RX_F_FINISHED) ? 1.0 : c[q].progress) : 0.0;
+      inf[RX_INFO_PROGRESS_DELTA] = 0.0;
+      inf[RX_INFO_PLACEMENT] = keep ? (double)place[q] : 0.0;
+    }
+  }
+  if (do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
+    const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.call << 32) ^ (uint64_t)e));
+    const int first = (int)(h & 1ull);  // agent_order[0] after np.random.shuffle([0, 1])
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double offset = ((double)((first == q) ? 0 : 1) - 0.5) * 3.5;
+      c[q].x = meta[0] + meta[5] * offset;
+      c[q].y = meta[1] + meta[6] * offset;
+      c[q].angle = meta[2];
+      c[q].vx = c[q].vy = 0.0;
+      c[q].progress = 0.0;
+      c[q].crashed = false;
+      fl[q] = 0;
+      last_steering[q] = 0.0;
+      S.finished_step[2 * e + q] = -1;
+    }
+    steps = 0;
+    ef &= (uint8_t)~RX_EF_PENDING_RESET;
+    S.ep_return[e] = 0.0;
+    S.ep_length[e] = 0;
+  }
+  if (stepping || do_reset) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = 2 * e + q;
+      S.x[i] = c[q].x;
+      S.y[i] = c[q].y;
+      S.angle[i] = c[q].angle;
+      S.vx[i] = c[q].vx;
+      S.vy[i] = c[q].vy;
+      S.progress[i] = c[q].progress;
+      S.last_progress[i] = c[q].progress;
+      S.last_steering[i] = last_steering[q];
+      S.flags[i] = fl[q];
+    }
+    S.steps[e] = steps;
+    S.env_flags[e] = ef;
+  }
+  const bool wrote_step = stepping;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (a.io.reward) a.io.reward[2 * e + q] = wrote_step ? (float)rw[q] : 0.0f;
+    if (a.io.reward64) a.io.reward64[2 * e + q] = wrote_step ? rw[q] : 0.0;
+  }
+  const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
+  if (a.io.terminated) a.io.terminated[e] = t_out;
+  if (a.io.truncated) a.io.truncated[e] = u_out;
+  if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  // non-ray observation columns, multi_racing_env.py:226-271
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const Car& me = c[q];
+    const Car& o = c[1 - q];
+    double s, co;
+    rx_sincos(me.angle, &s, &co);
+    double vf = me.vx * co + me.vy * s;
+    double vl = (-me.vx) * s + me.vy * co;
+    double rx_ = o.x - me.x, ry_ = o.y - me.y;
+    double lrx = rx_ * co + ry_ * s;
+    double lry = (-rx_) * s + ry_ * co;
+    double rvx = o.vx - me.vx, rvy = o.vy - me.vy;
+    double lvx = rvx * co + rvy * s;
+    double lvy = (-rvx) * s + rvy * co;
+    float* ob = a.io.obs + (size_t)(2 * e + q) * a.D + a.n_sensors;
+    ob[0] = (float)rx_clip(vf / RX_MAX_SPEED, -1.0, 1.0);
+    ob[1] = (float)rx_clip(vl / RX_MAX_SPEED, -1.0, 1.0);
+    ob[2] = (float)rx_clip(0.0 / 3.0, -1.0, 1.0);
+    ob[3] = (float)last_steering[q];
+    ob[4] = (float)rx_clip(lrx / maxd, -1.0, 1.0);
+    ob[5] = (float)rx_clip(lry / maxd, -1.0, 1.0);
+    ob[6] = (float)rx_clip(lvx / RX_MAX_SPEED, -1.0, 1.0);
+    ob[7] = (float)rx_clip(lvy / RX_MAX_SPEED, -1.0, 1.0);
+  }
+}
+
+// ============================================================ k_rays
+// Track.raycast (environment/track.py:173-199) -- and for A == 2
+// MultiTrack.raycast_with_cars (multi_track.py:5-44) -- one lane per
+// (env, agent, ray).
+//
+// Exact division-free hit test.  With D = |dotp|, C = sgn(dotp)*cross,
+// N = sgn(dotp)*dot (sign flips are exact, and IEEE division is sign-symmetric,
+// so t = cross/dotp = C/D and s = dot/dotp = N/D bit for bit):
+//   valid  <=> D > 1e-10
+//   t >= 0 <=> C >= 0          (no underflow: |C| >= 1e-32 when nonzero here)
+//   s >= 0 <=> N >= 0
+//   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
+// (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
+// range its rounding cannot cross the threshold).  Only hit segments divide.
+template <int A>
+__global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (wave >= a.n_ray_waves) return;
+  const rx_wave we = a.ray_waves[wave];
+  const int lane = threadIdx.x & 63;
+  const int k = uniform(we.track);
+  const int wp0 = uniform(a.tr.wp_off[k]);
+  const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
+  const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+  if (lane >= we.count) return;
+  const int R = a.n_sensors;
+  const int task = we.task_start + lane;
+  const int env_local = task / (A * R);
+  const int rem = task - env_local * (A * R);
+  const int q = rem / R;
+  const int ray = rem - q * R;
+  const int e = a.perm[we.perm_start + env_local];
+  const int i = A * e + q;
+  const double ox = a.st.x[i], oy = a.st.y[i];
+  const double theta = a.st.angle[i] + a.rel_angles[ray];  // racing_env.py:50
+  double sn, cs;
+  rx_sincos(theta, &sn, &cs);
+  const double v3x = -sn, v3y = cs;
+  double best = __builtin_inf();
+#pragma unroll 4
+  for (int j = 0; j < S_; ++j) {
+    const double4 g = seg[j];  // wave-uniform -> s_load_dwordx8
+    const double v1x = ox - g.x, v1y = oy - g.y;
+    const double dotp = g.z * v3x + g.w * v3y;
+    const double cross = g.z * v1y - g.w * v1x;
+    const double dot = v1x * v3x + v1y * v3y;
+    const double D = __builtin_fabs(dotp);
+    const bool neg = dotp < 0.0;
+    const double C = neg ? -cross : cross;
+    const double N = neg ? -dot : dot;
+    const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
+    if (hit) {
+      const double t = C / D;
+      best = t < best ? t : best;
+    }
+  }
+  double dist = (best == __builtin_inf()) ? RX_MAX_RANGE : best;
+  if (A == 2) {
+    const int o = A * e + (1 - q);
+    const double ocx = a.st.x[o], ocy = a.st.y[o];
+    const double dx = ocx - ox, dy = ocy - oy;
+    double min_car = RX_MAX_RANGE;
+    if (!(__builtin_sqrt(rx_dot2_np(dx, dy, dx, dy)) < 0.5)) {  // multi_track.py:12-14
+      double os, oc, qx[4], qy[4];
+      rx_sincos(a.st.angle[o], &os, &oc);
+      corners(ocx, ocy, oc, os, qx, qy);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {  // ray_seg_intersection, multi_track.py:28-44
+        const double sx = qx[m], sy = qy[m], ex = qx[(m + 1) & 3], ey = qy[(m + 1) & 3];
+        const double v1x = ox - sx, v1y = oy - sy;
+        const double v2x = ex - sx, v2y = ey - sy;
+        const double dotp = rx_dot2_np(v2x, v2y, v3x, v3y);
+        if (!(__builtin_fabs(dotp) < 1e-10)) {
+          const double t = (v2x * v1y - v2y * v1x) / dotp;
+          const double s = rx_dot2_np(v1x, v1y, v3x, v3y) / dotp;
+          if (t >= 0 && 0 <= s && s <= 1 && t < min_car) min_car = t;
+        }
+      }
+    }
+    dist = (min_car < dist) ? min_car : dist;
+  }
+  a.io.obs[(size_t)i * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
+}
+
+// ============================================================ GAE
+// PPO.compute_advantages, agent/ppo.py:134-154: float32, no FMA, lane = env.
+__global__ __launch_bounds__(256) void k_gae(int T, int N, const float* __restrict__ r, const float* __restrict__ v,
+                                             const float* __restrict__ d, const float* __restrict__ nv,
+                                             const float* __restrict__ nd, float g, float gl,
+                                             float* __restrict__ adv, float* __restrict__ ret) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float run = 0.0f;
+  float nnt = 1.0f - nd[n];
+  float nvv = nv[n];
+#pragma unroll 8
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t o = (size_t)t * N + n;
+    const float vt = v[o];
+    const float delta = (r[o] + (g * nnt) * nvv) - vt;
+    run = delta + (gl * nnt) * run;
+    adv[o] = run;
+    ret[o] = run + vt;
+    nnt = 1.0f - d[o];
+    nvv = vt;
+  }
+}
+
+// Wavefront-prefix variant: one wave per env; lane l owns the time chunk
+// [l*L, (l+1)*L).  Pass 1: each lane composes its chunk's affine map
+// A_in = alpha + beta * A_out (backwards).  Pass 2: a 64-lane suffix scan of
+// the maps gives every lane its incoming A_out.  Pass 3: the chunk is replayed
+// with the reference recurrence from that carry-in.
+__global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __restrict__ r,
+                                                  const float* __restrict__ v, const float* __restrict__ d,
+                                                  const float* __restrict__ nv, const float* __restrict__ nd, float g,
+                                                  float gl, float* __restrict__ adv, float* __restrict__ ret) {
+  const int n = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (n >= N) return;
+  const int lane = threadIdx.x & 63;
+  const int L = (T + 63) / 64;
+  const int t0 = lane * L;
+  const int t1 = min(T, t0 + L);
+  auto nnt_at = [&](int t) -> float {  // next_nonterminal used at time t
+    return (t == T - 1) ? 1.0f - nd[n] : 1.0f - d[(size_t)(t + 1) * N + n];
+  };
+  auto nv_at = [&](int t) -> float { return (t == T - 1) ? nv[n] : v[(size_t)(t + 1) * N + n]; };
+  float alpha = 0.0f, beta = 1.0f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const size_t o = (size_t)t * N + n;
+    const float nnt = nnt_at(t);
+    const float delta = (r[o] + (g * nnt) * nv_at(t)) - v[o];
+    const float c = gl * nnt;
+    alpha = delta + c * alpha;
+    beta = c * beta;
+  }
+  // inclusive suffix scan of maps: S_l = M_l o M_{l+1} o ... o M_63
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float ao = __shfl_down(alpha, off, 64);
+    const float bo = __shfl_down(beta, off, 64);
+    if (lane + off < 64) {
+      alpha = alpha + beta * ao;
+      beta = beta * bo;
+    }
+  }
+  float carry = __shfl_down(alpha, 1, 64);  // A_out(l) = S_{l+1}(0)
+  if (lane == 63) carry = 0.0f;
+  float run = carry;
+  for (int t = t1 - 1; t >= t0; --t) {
+    const size_t o = (size_t)t * N + n;
+    const float nnt = nnt_at(t);
+    const float vt = v[o];
+    const float delta = (r[o] + (g * nnt) * nv_at(t)) - vt;
+    run = delta + (gl * nnt) * run;
+    adv[o] = run;
+    ret[o] = run + vt;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ launchers
+extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, hipStream_t s) {
+  const dim3 blk(256);
+  if (a->n_dyn_waves > 0) {
+    const dim3 grd((a->n_dyn_waves + 3) / 4);
+    if (n_agents == 1)
+      hipLaunchKernelGGL(k_dyn1, grd, blk, 0, s, *a);
+    else
+      hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
+  }
+  if (a->n_ray_waves > 0) {
+    const dim3 grd((a->n_ray_waves + 3) / 4);
+    if (n_agents == 1)
+      hipLaunchKernelGGL(k_rays<1>, grd, blk, 0, s, *a);
+    else
+      hipLaunchKernelGGL(k_rays<2>, grd, blk, 0, s, *a);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
+                             const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s) {
+  if (scan) {
+    hipLaunchKernelGGL(k_gae_scan, dim3((N + 3) / 4), dim3(256), 0, s, T, N, r, v, d, nv, nd, g, gl, adv, ret);
+  } else {
+    hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, s, T, N, r, v, d, nv, nd, g, gl, adv, ret);
+  }
+  return (int)hipGetLastError();
+}

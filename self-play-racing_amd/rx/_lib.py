@@ -1,0 +1,117 @@
+"""ctypes binding of librx.so (include/rx.h).
+
+torch is imported first on purpose: torch ships its own libamdhip64.so.7 and
+librx.so links against the same SONAME, so loading librx after torch makes
+both share ONE HIP runtime (streams and device pointers are then
+interchangeable).  There is no CPU fallback: if the library is missing or the
+device is absent, calls fail loudly.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
+
+from . import _build
+
+RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
+RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
+RX_EF_PENDING_RESET = 1
+RX_AUTORESET_NEXT_STEP, RX_AUTORESET_SAME_STEP, RX_AUTORESET_DISABLED = 0, 1, 2
+RX_INFO_W = 4
+RX_INFO_SPEED, RX_INFO_PROGRESS, RX_INFO_PROGRESS_DELTA, RX_INFO_PLACEMENT = 0, 1, 2, 3
+
+_P = ctypes.c_void_p
+
+EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sensor_angles", "rx_upload_tracks",
+           "rx_assign", "rx_bind_state", "rx_set_speed_weight", "rx_reset", "rx_step", "rx_step_phases", "rx_gae",
+           "rx_gae_scan")
+RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
+
+
+class RxConfig(ctypes.Structure):
+    _fields_ = [("n_envs", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_sensors", ctypes.c_int32),
+                ("max_steps", ctypes.c_int32), ("autoreset", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double)]
+
+
+STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
+                "steps", "track", "env_flags", "ep_return", "ep_length", "speed_weight")
+
+
+class RxState(ctypes.Structure):
+    _fields_ = [(k, _P) for k in STATE_FIELDS]
+
+
+IO_FIELDS = ("actions", "obs", "reward", "reward64", "terminated", "truncated", "done_f32", "info", "ep_done",
+             "ep_stats")
+
+
+class RxIO(ctypes.Structure):
+    _fields_ = [(k, _P) for k in IO_FIELDS]
+
+
+class RxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path():
+    return _build.LIB
+
+
+def load(build_if_missing=True):
+    """Load librx.so (building it with hipcc if it is missing and allowed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RxError(f"librx.so not built at {path} (run python -m rx._build)")
+        _build.build()
+    L = ctypes.CDLL(path)
+    L.rx_last_error.restype = ctypes.c_char_p
+    L.rx_abi_version.restype = ctypes.c_int
+    L.rx_create.argtypes = [ctypes.POINTER(RxConfig), ctypes.POINTER(_P)]
+    L.rx_destroy.argtypes = [_P]
+    L.rx_sensor_angles.argtypes = [_P, _P]
+    L.rx_upload_tracks.argtypes = [_P, ctypes.c_int32, _P, _P, _P, _P, _P]
+    L.rx_assign.argtypes = [_P, _P]
+    L.rx_bind_state.argtypes = [_P, ctypes.POINTER(RxState)]
+    L.rx_set_speed_weight.argtypes = [_P, ctypes.c_double]
+    L.rx_reset.argtypes = [_P, _P, ctypes.POINTER(RxIO), _P]
+    L.rx_step.argtypes = [_P, ctypes.POINTER(RxIO), _P]
+    L.rx_step_phases.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, _P]
+    gae_args = [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _P, _P]
+    L.rx_gae.argtypes = gae_args
+    L.rx_gae_scan.argtypes = gae_args
+    for name in EXPORTS:
+        if name not in ("rx_last_error", "rx_abi_version"):
+            getattr(L, name).restype = ctypes.c_int
+    if L.rx_abi_version() != 1:
+        raise RxError(f"librx ABI {L.rx_abi_version()} != 1")
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != RX_OK:
+        msg = _lib.rx_last_error().decode() if _lib is not None else "?"
+        raise RxError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device (or host) pointer of a tensor / ndarray, None for None."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        assert t.is_contiguous(), "tensors handed to librx must be contiguous"
+        return _P(t.data_ptr())
+    return _P(t.ctypes.data)
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return _P(s.cuda_stream)

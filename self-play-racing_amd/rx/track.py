@@ -1,0 +1,192 @@
+"""Host-side track generation and the device track table.
+
+Restates environment/track.py's generation and geometry (SURVEY.md §8(a) rows
+A1, A2, A7) with the same numpy/scipy calls in the same order, so waypoints,
+normals and boundary segments are bit-identical to the reference's
+(tests/test_track_host.py checks them against the golden vectors).  What is
+new is what happens around them:
+
+* ``gen_tracks(..., seed=s)`` reseeds the global RNG inside every track
+  (track.py:5-6), so the per-track draws cycle through at most five states;
+  the generator memoises that cycle instead of re-drawing 65,536 times, and
+  leaves the global RNG exactly where the reference would.
+* ``TrackSet`` deduplicates (control points, width) pairs into slots -- seed 1
+  gives 7 slots for any number of envs -- and packs them into the flat
+  struct-of-arrays table the kernels read (include/rx.h rx_upload_tracks).
+"""
+import numpy as np
+from scipy.interpolate import CubicSpline
+
+TWO_PI = 2 * np.pi
+
+DEFAULT_CONTROL_POINTS = np.array([
+    [0, 0], [50, 0], [70, 20], [60, 40],
+    [70, 50], [50, 70], [20, 70], [10, 50],
+    [10, 20], [0, 10],
+])  # environment/track.py:70-74 (integer array, as in the reference)
+DEFAULT_WIDTH = 6.0  # environment/track.py:77-80
+
+
+def gen_random_track(num_points=15, base_radius=50, radius_variation=15, angle_jitter=0.2, smoothness=0.5,
+                     seed=None):
+    """Random closed control polygon -- environment/track.py:4-45.
+
+    Same global-RNG draws in the same order: n jitter offsets, then n radius
+    variations (drawn one per point, as the reference's loop does)."""
+    rs = np.random
+    if seed is not None:
+        rs.seed(seed)
+    ang = np.linspace(0, TWO_PI, num_points, endpoint=False)
+    if angle_jitter > 0:
+        half = angle_jitter * (TWO_PI / num_points) / 2
+        ang = np.sort((ang + rs.uniform(-half, half, num_points)) % TWO_PI)
+    r = np.zeros(num_points)
+    for i in range(num_points):
+        v = base_radius + rs.uniform(-radius_variation, radius_variation)
+        r[i] = v if (smoothness <= 0 or i == 0) else (1 - smoothness) * v + (smoothness * r[i - 1])
+    if smoothness > 0:
+        r[0] = (r[0] + r[-1]) / 2
+    return np.column_stack([r * np.cos(ang), r * np.sin(ang)])
+
+
+def _draw_params():
+    # environment/track.py:50-54, global RNG
+    n = np.random.randint(10, 15)
+    base = np.random.randint(50, 80)
+    var = np.random.randint(10, base // 2 - 10)
+    jit = np.random.uniform(0.2, 0.7)
+    smooth = np.random.uniform(0.2, 0.7)
+    return n, base, var, jit, smooth
+
+
+def gen_tracks(num_tracks=10, seed=None):
+    """environment/track.py:47-56, with the reseed cycle memoised.
+
+    With ``seed`` set, every track's draws start from the RNG state that
+    ``np.random.seed(seed)`` plus the previous track's 2*n uniform draws left
+    behind, i.e. a function of the previous track's point count only.  The
+    loop therefore caches (prev point count) -> (control points, point count,
+    RNG state after) and replays it; the returned arrays for equal tracks are
+    the same read-only object.  The global RNG ends in the reference's state.
+    """
+    out = []
+    if seed is None or num_tracks <= 0:
+        for _ in range(num_tracks):
+            out.append(gen_random_track(*_draw_params(), seed))
+        return out
+    p = _draw_params()
+    cp = gen_random_track(*p, seed)
+    cp.setflags(write=False)
+    out.append(cp)
+    prev_n = p[0]
+    state_after = None
+    memo = {}
+    for _ in range(1, num_tracks):
+        hit = memo.get(prev_n)
+        if hit is None:
+            if state_after is not None:  # resync the real RNG before drawing anew
+                np.random.set_state(state_after)
+            q = _draw_params()
+            c = gen_random_track(*q, seed)
+            c.setflags(write=False)
+            hit = (c, q[0], np.random.get_state())
+            memo[prev_n] = hit
+        cp, prev_n, state_after = hit
+        out.append(cp)
+    if state_after is not None:
+        np.random.set_state(state_after)
+    return out
+
+
+class TrackGeometry:
+    """Track.__init__ geometry -- environment/track.py:61-148, 154-157.
+
+    Attributes mirror the reference's: waypoints [W,2], normals [W,2],
+    left_boundary/right_boundary, segment_cache {'starts','ends','v2'} [2W,2],
+    track_bounds, max_track_distance, track_width, start pose."""
+
+    def __init__(self, control_points=None, track_width=None, factor=30):
+        cp = DEFAULT_CONTROL_POINTS if control_points is None else control_points
+        self.control_points = cp
+        self.track_width = DEFAULT_WIDTH if track_width is None else track_width
+        # gen_waypoints, track.py:100-115 (chord-length periodic cubic spline)
+        closed = np.vstack((cp, cp[0]))
+        chord = np.sqrt(np.sum(np.diff(closed, axis=0) ** 2, axis=1))
+        t = np.concatenate(([0], np.cumsum(chord)))
+        sx = CubicSpline(t, closed[:, 0], bc_type="periodic")
+        sy = CubicSpline(t, closed[:, 1], bc_type="periodic")
+        tw = np.linspace(0, t[-1], len(cp) * factor, endpoint=False)
+        self.waypoints = np.column_stack((sx(tw), sy(tw)))
+        wp = self.waypoints
+        # track_bounds / max_track_distance, track.py:82-91 (np.float64 ** 2 is pow())
+        lo_x, hi_x = wp[:, 0].min(), wp[:, 0].max()
+        lo_y, hi_y = wp[:, 1].min(), wp[:, 1].max()
+        self.track_bounds = {"min_x": lo_x, "max_x": hi_x, "min_y": lo_y, "max_y": hi_y}
+        self.max_track_distance = np.sqrt((hi_x - lo_x) ** 2 + (hi_y - lo_y) ** 2)
+        # calc_normals, track.py:117-124
+        tang = np.diff(wp, axis=0, append=[wp[0]])
+        tl = np.linalg.norm(tang, axis=1, keepdims=True)
+        tang = tang / np.where(tl == 0, 1, tl)
+        self.normals = np.column_stack((-tang[:, 1], tang[:, 0]))
+        # boundaries and the segment cache, track.py:93-96, 126-148
+        self.left_boundary = wp + self.normals * self.track_width
+        self.right_boundary = wp - self.normals * self.track_width
+        starts = np.vstack([self.left_boundary, self.right_boundary])
+        ends = np.vstack([np.roll(self.left_boundary, -1, axis=0), np.roll(self.right_boundary, -1, axis=0)])
+        self.segment_cache = {"starts": starts, "ends": ends, "v2": ends - starts}
+
+    def get_start_pos(self):
+        """track.py:154-157"""
+        wp = self.waypoints
+        return (wp[0, 0], wp[0, 1], np.arctan2(wp[1, 1] - wp[0, 1], wp[1, 0] - wp[0, 0]))
+
+
+class TrackSet:
+    """Deduplicated (control points, width) slots packed as the device table.
+
+    ``slot(cp, width)`` returns the slot index of a pair, adding it on first
+    sight; ``arrays()`` gives the rx_upload_tracks layout (include/rx.h)."""
+
+    def __init__(self, factor=30):
+        self.factor = factor
+        self.geoms = []
+        self._index = {}
+        self._packed = None
+
+    @staticmethod
+    def _key(cp, width):
+        a = np.asarray(cp)
+        return (a.dtype.str, a.shape, a.tobytes(), float(width))
+
+    def slot(self, control_points=None, track_width=None):
+        cp = DEFAULT_CONTROL_POINTS if control_points is None else control_points
+        w = DEFAULT_WIDTH if track_width is None else track_width
+        key = self._key(cp, w)
+        k = self._index.get(key)
+        if k is None:
+            k = len(self.geoms)
+            self.geoms.append(TrackGeometry(cp, w, self.factor))
+            self._index[key] = k
+            self._packed = None
+        return k
+
+    def __len__(self):
+        return len(self.geoms)
+
+    def arrays(self):
+        if self._packed is None:
+            g = self.geoms
+            W = [len(t.waypoints) for t in g]
+            wp_off = np.concatenate([[0], np.cumsum(W)]).astype(np.int32)
+            wp = np.ascontiguousarray(np.concatenate([t.waypoints for t in g]), dtype=np.float64)
+            nrm = np.ascontiguousarray(np.concatenate([t.normals for t in g]), dtype=np.float64)
+            seg = np.ascontiguousarray(np.concatenate(
+                [np.concatenate([t.segment_cache["starts"], t.segment_cache["v2"]], axis=1) for t in g]),
+                dtype=np.float64)
+            meta = np.zeros((len(g), 8), dtype=np.float64)
+            for k, t in enumerate(g):
+                sx, sy, sa = t.get_start_pos()
+                meta[k] = (sx, sy, sa, float(t.track_width), float(t.max_track_distance),
+                           t.normals[0, 0], t.normals[0, 1], 0.0)
+            self._packed = dict(wp_off=wp_off, wp=wp, nrm=nrm, seg=seg, meta=meta)
+        return self._packed

@@ -1,0 +1,315 @@
+"""Device-resident vectorised racing envs (the host side of include/rx.h).
+
+``RacingVectorEnv`` replaces ``gym.vector.SyncVectorEnv([RacingEnv ...])`` +
+``RecordEpisodeStatistics`` (agent/ppo.py:70,85-95): every env lives as one
+row of struct-of-arrays device state, and one ``rx_step`` advances all of them
+(SURVEY.md §8(b)).  Two surfaces:
+
+* device fast path -- ``reset_device`` / ``step_device`` take and return torch
+  tensors on the GPU, write straight into caller buffers (e.g. the PPO rollout
+  rows), and never synchronise with the host;
+* SyncVectorEnv-compatible numpy surface -- ``reset`` / ``step`` return numpy
+  arrays and gymnasium-style ``infos`` (``episode``/``_episode`` ...), for
+  unmodified callers.
+
+Autoreset follows gymnasium 1.x SyncVectorEnv's default NEXT_STEP mode: the
+step after a terminal one ignores the action, resets the env and reports
+reward 0, terminated = truncated = False (unpinned, gymnasium
+is not installed here).
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from .spaces import Box, single_action_space, single_observation_space
+from .track import TrackSet
+
+_AUTORESET = {"next_step": _lib.RX_AUTORESET_NEXT_STEP, "same_step": _lib.RX_AUTORESET_SAME_STEP,
+              "disabled": _lib.RX_AUTORESET_DISABLED}
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise _lib.RxError("RacingVectorEnv needs a HIP device (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _EnvProxy:
+    """Stands in for ``envs.envs[i]`` (a RecordEpisodeStatistics wrapper in the
+    reference).  ``setattr(envs.envs[i], 'speed_weight', w)`` (agent/ppo.py:
+    256-258) lands on the wrapper there and never reaches RacingEnv (SURVEY.md
+    §8 Q9), so here too it is recorded on the proxy only."""
+
+    def __init__(self, idx):
+        self.idx = idx
+
+
+class RacingVectorEnv:
+    """N envs (A = 1: RacingEnv, A = 2: MultiRacingEnv) on one device.
+
+    Parameters mirror the reference constructors: per env a control-point
+    array (``track_pool[track_id]``) and a track width; ``n_sensors`` (11 in
+    train.py); sensor cone pi/3 for A=1 (racing_env.py:45) and pi/2 for A=2
+    (multi_racing_env.py:50)."""
+
+    def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
+                 seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None):
+        self.L = _lib.load()
+        self.device = torch.device(device) if device is not None else _default_device()
+        if self.device.type != "cuda":
+            raise _lib.RxError(f"RacingVectorEnv runs on a HIP device, got {self.device}")
+        N = len(control_points)
+        if N <= 0 or len(widths) != N:
+            raise ValueError("need one width per env")
+        self.num_envs = N
+        self.n_agents = A = int(n_agents)
+        self.n_sensors = R = int(n_sensors)
+        self.D = R + 4 + 4 * (A - 1)
+        self.max_steps = int(max_steps)
+        self.speed_weight = float(speed_weight)
+        if half_cone is None:
+            half_cone = np.pi / 3 if A == 1 else np.pi / 2
+        self.tracks = track_set if track_set is not None else TrackSet()
+        slots = np.empty(N, dtype=np.int32)
+        cache = {}
+        for i, (cp, w) in enumerate(zip(control_points, widths)):
+            key = (id(cp), float(w) if w is not None else None)
+            k = cache.get(key)
+            if k is None:
+                k = self.tracks.slot(cp, w)
+                cache[key] = k
+            slots[i] = k
+        self.track_of_env = slots
+        dev = self.device
+        with torch.cuda.device(dev):
+            f64 = dict(dtype=torch.float64, device=dev)
+            self.state = {k: torch.zeros(N * A, **f64) for k in ("x", "y", "angle", "vx", "vy", "progress",
+                                                               "last_progress", "last_steering")}
+            self.state["finished_step"] = torch.full((N * A,), -1, dtype=torch.int32, device=dev)
+            self.state["flags"] = torch.zeros(N * A, dtype=torch.uint8, device=dev)
+            self.state["steps"] = torch.zeros(N, dtype=torch.int32, device=dev)
+            self.state["track"] = torch.from_numpy(slots).to(dev)
+            self.state["env_flags"] = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self.state["ep_return"] = torch.zeros(N, **f64)
+            self.state["ep_length"] = torch.zeros(N, dtype=torch.int32, device=dev)
+            obs_shape = (N, self.D) if A == 1 else (N, A, self.D)
+            self.buf = dict(
+                actions=torch.zeros((N, A, 2), dtype=torch.float32, device=dev),
+                obs=torch.zeros(obs_shape, dtype=torch.float32, device=dev),
+                reward=torch.zeros((N,) if A == 1 else (N, A), dtype=torch.float32, device=dev),
+                reward64=torch.zeros((N,) if A == 1 else (N, A), **f64),
+                terminated=torch.zeros(N, dtype=torch.uint8, device=dev),
+                truncated=torch.zeros(N, dtype=torch.uint8, device=dev),
+                done_f32=torch.zeros(N, dtype=torch.float32, device=dev),
+                info=torch.zeros((N, A, _lib.RX_INFO_W), **f64),
+                ep_done=torch.zeros(N, dtype=torch.uint8, device=dev),
+                ep_stats=torch.zeros(3, **f64),
+            )
+            cfg = _lib.RxConfig(N, A, R, self.max_steps, _AUTORESET[autoreset], dev.index or 0, int(seed) & (2**64 - 1),
+                                float(half_cone), self.speed_weight)
+            h = _lib._P()
+            _lib.check(self.L.rx_create(cfg, h), "rx_create")
+            self._h = h
+            self._upload_tracks()
+            self.state["speed_weight"] = None  # per-env weights: set_speed_weights()
+            st = self._state_struct()
+            _lib.check(self.L.rx_bind_state(self._h, st), "rx_bind_state")
+            _lib.check(self.L.rx_assign(self._h, _lib.ptr(np.ascontiguousarray(slots))), "rx_assign")
+        rel = np.zeros(R, dtype=np.float64)
+        _lib.check(self.L.rx_sensor_angles(self._h, _lib.ptr(rel)), "rx_sensor_angles")
+        self.sensor_angles = rel
+        self.single_observation_space = single_observation_space(R, A)
+        self.single_action_space = single_action_space(A)
+        self.observation_space = Box(-1.0, 1.0, shape=(N,) + self.single_observation_space.shape, dtype=np.float32)
+        self.action_space = Box(np.tile(self.single_action_space.low, (N, 1)),
+                                np.tile(self.single_action_space.high, (N, 1)), shape=(N, 2), dtype=np.float32)
+        self.envs = [_EnvProxy(i) for i in range(N)]
+        self._episode_start = np.full(N, time.perf_counter())
+        self._closed = False
+
+    # ------------------------------------------------------------ plumbing
+    def _upload_tracks(self):
+        t = self.tracks.arrays()
+        n = len(t["meta"])
+        _lib.check(self.L.rx_upload_tracks(self._h, n, _lib.ptr(t["wp_off"]), _lib.ptr(t["wp"]), _lib.ptr(t["nrm"]),
+                                           _lib.ptr(t["seg"]), _lib.ptr(t["meta"])), "rx_upload_tracks")
+
+    def _io(self, actions=None, obs=None, reward=None, done=None, full=False):
+        b = self.buf
+        return _lib.RxIO(
+            _lib.ptr(actions) if actions is not None else None,
+            _lib.ptr(obs if obs is not None else b["obs"]),
+            _lib.ptr(reward if reward is not None else b["reward"]),
+            _lib.ptr(b["reward64"]) if full else None,
+            _lib.ptr(b["terminated"]),
+            _lib.ptr(b["truncated"]),
+            _lib.ptr(done if done is not None else b["done_f32"]),
+            _lib.ptr(b["info"]) if full else None,
+            _lib.ptr(b["ep_done"]),
+            _lib.ptr(b["ep_stats"]),
+        )
+
+    def _state_struct(self):
+        return _lib.RxState(*[_lib.ptr(self.state[k]) for k in _lib.STATE_FIELDS])
+
+    def set_speed_weights(self, w):
+        """Per-env RacingEnv.speed_weight ([N] array), or None to use the uniform value."""
+        if w is None:
+            self.state["speed_weight"] = None
+        else:
+            self.state["speed_weight"] = torch.as_tensor(np.asarray(w, dtype=np.float64).reshape(self.num_envs)).to(
+                self.device).contiguous()
+        _lib.check(self.L.rx_bind_state(self._h, self._state_struct()), "rx_bind_state")
+
+    def set_speed_weight(self, w):
+        """RacingEnv.speed_weight for every env (racing_env.py:26,140)."""
+        self.speed_weight = float(w)
+        _lib.check(self.L.rx_set_speed_weight(self._h, self.speed_weight), "rx_set_speed_weight")
+
+    def _as_actions(self, actions):
+        A = self.n_agents
+        if isinstance(actions, torch.Tensor):
+            a = actions
+            if a.device != self.device or a.dtype != torch.float32:
+                a = a.to(self.device, torch.float32)
+        else:
+            a = torch.from_numpy(np.ascontiguousarray(actions, dtype=np.float32)).to(self.device)
+        if a.numel() != self.num_envs * A * 2:
+            raise ValueError(f"actions must have {self.num_envs}x{A}x2 elements, got shape {tuple(a.shape)}")
+        return a.contiguous()
+
+    # ------------------------------------------------------------ device path
+    def reset_device(self, mask=None, obs_out=None, stream=None):
+        """Reset all envs (or where ``mask``, a device uint8/bool [N]); returns obs."""
+        m = None
+        if mask is not None:
+            m = mask.to(self.device, torch.uint8).contiguous()
+        io = self._io(obs=obs_out, full=True)
+        _lib.check(self.L.rx_reset(self._h, _lib.ptr(m), io, _lib.stream_ptr(stream)), "rx_reset")
+        return obs_out if obs_out is not None else self.buf["obs"]
+
+    def step_device(self, actions, obs_out=None, reward_out=None, done_out=None, full_info=False, stream=None,
+                    phases=3):
+        """One step of every env from device actions; returns (obs, reward, done_f32) tensors.
+
+        ``obs_out`` / ``reward_out`` / ``done_out`` may be rows of a rollout buffer
+        (contiguous, right shape): the kernels write there directly.  ``phases``
+        (rx_step_phases) splits the step into its two kernels for timing."""
+        a = self._as_actions(actions)
+        io = self._io(actions=a, obs=obs_out, reward=reward_out, done=done_out, full=full_info)
+        if phases == 3:
+            _lib.check(self.L.rx_step(self._h, io, _lib.stream_ptr(stream)), "rx_step")
+        else:
+            _lib.check(self.L.rx_step_phases(self._h, io, int(phases), _lib.stream_ptr(stream)), "rx_step_phases")
+        return (obs_out if obs_out is not None else self.buf["obs"],
+                reward_out if reward_out is not None else self.buf["reward"],
+                done_out if done_out is not None else self.buf["done_f32"])
+
+    def episode_stats(self, reset=True):
+        """(sum of returns, sum of lengths, count) of episodes that ended since the
+        last call -- one device->host copy."""
+        s = self.buf["ep_stats"].cpu().numpy().copy()
+        if reset:
+            self.buf["ep_stats"].zero_()
+        return float(s[0]), float(s[1]), int(s[2])
+
+    def get_state(self):
+        return {k: v.cpu().numpy() for k, v in self.state.items() if v is not None}
+
+    def set_state(self, **arrays):
+        """State injection (parity tests): overwrite state arrays from host arrays."""
+        for k, v in arrays.items():
+            t = self.state[k]
+            t.copy_(torch.as_tensor(np.ascontiguousarray(v).reshape(t.shape)).to(t.device, t.dtype))
+
+    # ------------------------------------------------------------ numpy surface
+    def reset(self, seed=None, options=None):
+        """SyncVectorEnv.reset -> every env's reset (racing_env.py:86-102)."""
+        self.reset_device()
+        self._episode_start[:] = time.perf_counter()
+        obs = self.buf["obs"].cpu().numpy().copy()
+        return obs, self._infos(reset_mask=np.ones(self.num_envs, dtype=bool), stepped=np.zeros(self.num_envs, bool))
+
+    def step(self, actions):
+        """SyncVectorEnv.step -> RecordEpisodeStatistics.step -> RacingEnv.step."""
+        pending = (self.state["env_flags"] & _lib.RX_EF_PENDING_RESET).bool().cpu().numpy()
+        self.step_device(actions, full_info=True)
+        b = self.buf
+        obs = b["obs"].cpu().numpy().copy()
+        rew = b["reward64"].cpu().numpy().copy()
+        term = b["terminated"].cpu().numpy().astype(bool)
+        trunc = b["truncated"].cpu().numpy().astype(bool)
+        infos = self._infos(reset_mask=pending, stepped=~pending, terminated=term, truncated=trunc, reward=rew)
+        now = time.perf_counter()
+        self._episode_start[pending] = now
+        return obs, rew, term, trunc, infos
+
+    def _infos(self, reset_mask, stepped, terminated=None, truncated=None, reward=None):
+        N = self.num_envs
+        st = {k: self.state[k].cpu().numpy() for k in ("x", "y", "flags")}
+        inf = self.buf["info"].cpu().numpy()
+        a0 = slice(0, None, self.n_agents)  # agent 0 (the learner)
+        fl = st["flags"][a0]
+        everyone = np.ones(N, dtype=bool)
+        infos = {
+            "position": np.stack([st["x"][a0], st["y"][a0]], axis=1), "_position": everyone.copy(),
+            "speed": inf[:, 0, _lib.RX_INFO_SPEED].copy(), "_speed": everyone.copy(),
+            "progress": inf[:, 0, _lib.RX_INFO_PROGRESS].copy(), "_progress": everyone.copy(),
+            "crashed": (fl & _lib.RX_F_CRASHED) != 0, "_crashed": everyone.copy(),
+            "finished": (fl & _lib.RX_F_FINISHED) != 0, "_finished": everyone.copy(),
+        }
+        if reward is not None and stepped.any():
+            infos["reward"] = np.where(stepped, reward if reward.ndim == 1 else reward[:, 0], 0.0)
+            infos["_reward"] = stepped.copy()
+            if self.n_agents == 1:
+                infos["progress_delta"] = np.where(stepped, inf[:, 0, _lib.RX_INFO_PROGRESS_DELTA], 0.0)
+                infos["_progress_delta"] = stepped.copy()
+            else:
+                pl = inf[:, 0, _lib.RX_INFO_PLACEMENT].astype(np.int64)
+                if (pl > 0).any():
+                    infos["placement"] = pl
+                    infos["_placement"] = pl > 0
+        if terminated is not None:
+            ended = (terminated | truncated) & stepped
+            if ended.any():
+                ret = self.state["ep_return"].cpu().numpy()
+                ln = self.state["ep_length"].cpu().numpy()
+                el = np.round(time.perf_counter() - self._episode_start, 6)
+                # ep_return/ep_length were already zeroed only if reset this step;
+                # ended envs are reset on the NEXT step, so their counters are intact.
+                infos["episode"] = {"r": np.where(ended, ret, 0.0), "l": np.where(ended, ln, 0).astype(np.int64),
+                                    "t": np.where(ended, el, 0.0)}
+                infos["_episode"] = ended
+        return infos
+
+    def close(self):
+        if not self._closed and getattr(self, "_h", None) is not None:
+            self.L.rx_destroy(self._h)
+            self._h = None
+            self._closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ------------------------------------------------------------ construction helpers
+    @classmethod
+    def from_envs(cls, envs, **kw):
+        """Build from reference-style env objects (rx.envs.RacingEnv / MultiRacingEnv
+        specs returned by a train.py ``env_fn``)."""
+        envs = list(envs)
+        first = envs[0]
+        n_agents = getattr(first, "num_agents", 1)
+        n_sensors = first.num_sensors
+        for e in envs:
+            if getattr(e, "num_agents", 1) != n_agents or e.num_sensors != n_sensors:
+                raise ValueError("all envs of one vector env must share num_agents and num_sensors")
+        cps = [e.control_points for e in envs]
+        widths = [e.track_width for e in envs]
+        kw.setdefault("speed_weight", getattr(first, "speed_weight", 8.0))
+        return cls(cps, widths, n_agents=n_agents, n_sensors=n_sensors, **kw)

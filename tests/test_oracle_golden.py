@@ -176,3 +176,23 @@ def test_device_sincos_is_correctly_rounded(oracle):
     # and it agrees with glibc almost always (glibc is not CR: ~0.15% differ by 1 ulp)
     assert (s != np.sin(x)).mean() < 0.01 and (c != np.cos(x)).mean() < 0.01
     assert math.copysign(1.0, oracle.sincos_dev(np.array([-0.0]))[0][0]) == -1.0
+
+
+def test_numpy_restatement_bit_exact(golden):
+    """oracle/np_env.py (bench.py's cpu_baseline) reproduces the reference exactly."""
+    from oracle.np_env import NpRacingEnv, make_track
+    step = golden["step_single"]
+    tracks = {}
+    for i in range(0, len(step["x"]), 7):  # every 7th KAT (the full set is the C oracle's job)
+        k = int(step["track"][i])
+        if k not in tracks:
+            tracks[k] = make_track(golden.tracks[k])
+        e = NpRacingEnv(tracks[k], 11, float(step["speed_weight"][i]))
+        e.x, e.y, e.angle, e.vx, e.vy = (float(step[c][i]) for c in ("x", "y", "angle", "vx", "vy"))
+        e.progress, e.crashed, e.finished = float(step["progress"][i]), bool(step["crashed"][i]), bool(step["finished"][i])
+        e.steps, e.last_progress, e.last_steering = int(step["steps"][i]), float(step["last_progress"][i]), float(step["last_steering"][i])
+        e.cp = [bool(c) for c in step["cp"][i]]
+        obs, r, term, trunc = e.step(step["action"][i])
+        assert np.array_equal(obs, step["o_obs"][i]), i
+        assert r == step["o_reward"][i] and term == step["o_terminated"][i] and trunc == step["o_truncated"][i], i
+        assert (e.x, e.y, e.vx, e.vy) == tuple(step[c][i] for c in ("o_x", "o_y", "o_vx", "o_vy")), i
