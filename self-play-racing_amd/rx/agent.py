@@ -1,0 +1,44 @@
+"""Actor-critic policy -- agent/ppo.py:11-62, same modules, init and state_dict
+keys (actor_mu.{0,2,4}, critic.{0,2,4}, log_std buffer), so checkpoints move
+between the reference and this engine unchanged (SURVEY.md §5 checkpoint row).
+
+The MLP is ~10.5k parameters: its GEMMs are far too small for hand-written
+MFMA tiles to matter, so it stays on PyTorch-ROCm (rocBLAS/hipBLASLt), as the
+north star prescribes; the env step and GAE are the hand-written kernels.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+class Agent(nn.Module):
+    def __init__(self, obs_space, action_space):
+        super().__init__()
+        obs_dim = int(np.array(obs_space.shape).prod())
+        act_dim = action_space.shape[0]
+        lin = Agent.layer_optimization
+        # mean head bounded by tanh; the std is a fixed (annealed) buffer, not a parameter
+        self.actor_mu = nn.Sequential(lin(nn.Linear(obs_dim, 64)), nn.Tanh(), lin(nn.Linear(64, 64)), nn.Tanh(),
+                                      lin(nn.Linear(64, act_dim), std=0.01), nn.Tanh())
+        self.register_buffer("log_std", torch.zeros(act_dim))
+        self.critic = nn.Sequential(lin(nn.Linear(obs_dim, 64)), nn.Tanh(), lin(nn.Linear(64, 64)), nn.Tanh(),
+                                    lin(nn.Linear(64, 1), std=1.0))
+
+    def get_value(self, obs):
+        return self.critic(obs)
+
+    def get_action_and_value(self, obs, action=None):
+        """Sample (or score) an action: Normal(mu, exp(log_std)); samples are
+        clamped to [-1, 1] and the log-prob is of the CLAMPED action (SURVEY.md
+        §8 Q7), summed over the 2 action dims; entropy likewise."""
+        mu = self.actor_mu(obs)
+        dist = torch.distributions.Normal(mu, torch.exp(self.log_std).expand_as(mu))
+        if action is None:
+            action = torch.clamp(dist.sample(), -1.0, 1.0)
+        return action, dist.log_prob(action).sum(-1), dist.entropy().sum(-1), self.critic(obs)
+
+    @staticmethod
+    def layer_optimization(layer, std=np.sqrt(2), bias=0.0):
+        torch.nn.init.orthogonal_(layer.weight, std)
+        torch.nn.init.constant_(layer.bias, bias)
+        return layer

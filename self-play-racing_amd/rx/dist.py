@@ -1,0 +1,84 @@
+"""Data parallelism over GPUs (BASELINE.json configs[4]).
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).  Envs
+are independent, so each rank owns the contiguous env shard
+[rank*N/W, (rank+1)*N/W) with its own track table, rollout buffer and GAE;
+the only exchanges are, per optimizer step,
+
+* one all-reduce of the flat gradient bucket (10,563 floats = 42 KB for the
+  15-dim policy) -- latency-bound on xGMI, so ONE bucket, never per-parameter;
+* one 4-float all-reduce [KL sum, advantage sum, advantage square-sum, count]
+  so the KL early stop and the minibatch advantage normalisation are global
+  (every rank stops in the same minibatch);
+
+and one 3-float all-reduce of episode statistics per update.  Minibatch
+shuffles use np.random with the same seed on every rank, so all ranks walk
+the same minibatch schedule over their own shards.
+
+Everything here also runs with the gloo backend on CPU (tests/test_dist_cpu.py).
+"""
+import torch
+import torch.distributed as td
+
+
+def active():
+    return td.is_available() and td.is_initialized() and td.get_world_size() > 1
+
+
+def world():
+    return td.get_world_size() if active() else 1
+
+
+def rank():
+    return td.get_rank() if active() else 0
+
+
+def shard(n):
+    """(first env, env count) of this rank's shard of n envs."""
+    w, r = world(), rank()
+    if n % w:
+        raise ValueError(f"num_envs={n} is not divisible by world size {w}")
+    k = n // w
+    return r * k, k
+
+
+def sum_stats(s, device):
+    """Sum (sum_return, sum_length, count) over ranks."""
+    if not active():
+        return s
+    t = torch.tensor([float(s[0]), float(s[1]), float(s[2])], dtype=torch.float64, device=device)
+    td.all_reduce(t)
+    return float(t[0]), float(t[1]), int(round(float(t[2])))
+
+
+def minibatch_stats(kl_sum, adv):
+    """[KL sum, sum(adv), sum(adv^2), count] over all ranks' minibatch shards."""
+    a = adv.detach().to(torch.float64)
+    t = torch.stack([kl_sum.detach().to(torch.float64), a.sum(), (a * a).sum(),
+                     torch.tensor(float(adv.numel()), dtype=torch.float64, device=adv.device)])
+    if active():
+        td.all_reduce(t)
+    return t
+
+
+def average_gradients(params):
+    """Mean of every gradient over ranks: ONE flat bucket, one all-reduce."""
+    if not active():
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    td.all_reduce(flat)
+    flat.div_(td.get_world_size())
+    o = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[o:o + n].view_as(g))
+        o += n
+
+
+def broadcast_parameters(module, src=0):
+    """Make every rank start from rank ``src``'s weights."""
+    if not active():
+        return
+    for t in list(module.parameters()) + list(module.buffers()):
+        td.broadcast(t.data, src)

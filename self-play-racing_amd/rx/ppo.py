@@ -1,0 +1,254 @@
+"""PPO with the reference's API (agent/ppo.py:65-293) on a device-resident rollout.
+
+``PPO(env_fn, config, device)`` / ``.train()`` / ``.save()`` / ``.load()`` and
+the per-phase methods keep their reference signatures, so train.py drops in.
+What changes underneath:
+
+* the N ``env_fn(i)`` envs become ONE ``RacingVectorEnv`` (rx.envs specs) and
+  every rollout step is one batched HIP step, written straight into the
+  rollout buffers (obs[t+1], rewards[t], dones[t+1]) -- no host round trip
+  per step (the reference does 1 D2H + 3 H2D copies per step, agent/ppo.py:
+  114-120);
+* GAE is one HIP kernel (rx.gae), bit-exact with compute_advantages;
+* episode statistics are summed on the device and read once per update;
+* with torch.distributed initialised, each rank owns its env shard and the
+  update averages gradients with one all-reduce per optimizer step
+  (rx.dist), plus a 4-float all-reduce for the global advantage
+  normalisation and the synchronised KL early stop.
+
+Semantics kept on purpose: next-step autoreset, the KL early stop that ends
+the WHOLE update (agent/ppo.py:178-182), per-minibatch advantage
+normalisation with the unbiased std, np.random.shuffle of b_inds, the linear
+lr / log_std anneals, and the speed-weight anneal that the reference applies
+to its RecordEpisodeStatistics wrappers only (set
+config["apply_speed_weight_anneal"] = True to really apply it).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+from . import dist as rdist
+from .agent import Agent
+from .gae import compute_gae
+
+
+class EpisodeSummary:
+    """Device-summed episode statistics of one rollout (replaces the list of
+    per-episode dicts agent/ppo.py:121-130 builds on the host)."""
+
+    def __init__(self, sum_return, sum_length, count):
+        self.sum_return, self.sum_length, self.count = sum_return, sum_length, int(count)
+
+    def __len__(self):
+        return self.count
+
+    def __bool__(self):
+        return self.count > 0
+
+    @property
+    def mean_reward(self):
+        return self.sum_return / self.count if self.count else float("nan")
+
+    @property
+    def mean_length(self):
+        return self.sum_length / self.count if self.count else float("nan")
+
+
+def build_vector_env(env_fn, num_envs, seed, device, **kw):
+    """Call env_fn(i) for every env (train.py factories) and gather the specs
+    into one device vector env, reset (agent/ppo.py:70,85-95)."""
+    from .vector_env import RacingVectorEnv
+    specs = [env_fn(i) for i in range(num_envs)]
+    venv = RacingVectorEnv.from_envs(specs, device=device, seed=seed, **kw)
+    venv.reset_device()
+    return venv
+
+
+class PPO:
+    log_std_schedule = (-0.5, -1.6)  # agent/ppo.py:250-251
+    info_path = "data/training_info_single_3.json"
+
+    def __init__(self, env_fn, config, device="cuda"):
+        self.config = config
+        want = device if torch.cuda.is_available() and config.get("cuda", True) else "cpu"
+        self.device = torch.device(want)
+        if self.device.type != "cuda":
+            raise RuntimeError("rx.ppo.PPO steps its envs on a HIP device; no CPU env path exists "
+                               "(torch.cuda.is_available() is False or config['cuda'] is False)")
+        self.env_fn = env_fn
+        self.envs = self._make_envs(env_fn)
+        random.seed(config["seed"])
+        np.random.seed(config["seed"])
+        torch.manual_seed(config["seed"])
+        self.agent = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
+        self.optimizer = optim.Adam(self.agent.parameters(), lr=config["learning_rate"], eps=1e-5)
+        self._fresh_obs = True
+
+    def _make_envs(self, env_fn):
+        c = self.config
+        lo, n = rdist.shard(c["num_envs"])
+        fn = env_fn if lo == 0 else (lambda i: env_fn(lo + i))
+        return build_vector_env(fn, n, c["seed"] + rdist.rank(), self.device)
+
+    @property
+    def num_local_envs(self):
+        return self.envs.num_envs
+
+    # ------------------------------------------------------------ rollout
+    def collect_rollout(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
+        """agent/ppo.py:97-132 on the device.  Buffers are [T, N_local, ...]."""
+        T = obs.shape[0]
+        with torch.no_grad():
+            obs[0].copy_(next_obs)
+            dones[0].copy_(next_done)
+            for step in range(T):
+                action, logprob, _, value = self.agent.get_action_and_value(obs[step])
+                actions[step].copy_(action)
+                logprobs[step].copy_(logprob)
+                values[step].copy_(value.flatten())
+                last = step + 1 == T
+                self.envs.step_device(action,
+                                      obs_out=next_obs if last else obs[step + 1],
+                                      reward_out=rewards[step],
+                                      done_out=next_done if last else dones[step + 1])
+        s = self.envs.episode_stats(reset=True)
+        s = rdist.sum_stats(s, self.device)
+        return obs, actions, logprobs, dones, rewards, values, next_obs, next_done, EpisodeSummary(*s)
+
+    def compute_advantages(self, rewards, dones, values, next_value, next_done):
+        """agent/ppo.py:134-154 as one HIP kernel (bit-exact)."""
+        c = self.config
+        return compute_gae(rewards, dones, values, next_value, next_done, c["gamma"], c["gae_lambda"])
+
+    # ------------------------------------------------------------ update
+    def ppo_update(self, advantages, returns, values, logprobs, actions, obs):
+        """agent/ppo.py:156-209; distributed-aware (rx.dist)."""
+        c = self.config
+        b_obs = obs.reshape((-1,) + obs.shape[2:])
+        b_actions = actions.reshape((-1,) + actions.shape[2:])
+        b_logprobs = logprobs.reshape(-1)
+        b_advantages = advantages.reshape(-1)
+        b_returns = returns.reshape(-1)
+        b_values = values.reshape(-1)
+        B = b_obs.shape[0]
+        world = rdist.world()
+        mb = c["minibatch_size"] // world if world > 1 else c["minibatch_size"]
+        b_inds = np.arange(B)
+        params = [p for p in self.agent.parameters()]
+        for epoch in range(c["update_epochs"]):
+            np.random.shuffle(b_inds)
+            perm = torch.from_numpy(b_inds).to(self.device)
+            for start in range(0, B, mb):
+                mb_inds = perm[start:start + mb]
+                _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+                ratio = (newlogprob - b_logprobs[mb_inds]).exp()
+                mb_adv = b_advantages[mb_inds]
+                with torch.no_grad():
+                    if world > 1:  # one 4-float all-reduce: global KL and advantage moments
+                        stats = rdist.minibatch_stats((b_logprobs[mb_inds] - newlogprob).sum(), mb_adv)
+                        count = stats[3]
+                        approx_kl = stats[0] / count
+                    else:
+                        approx_kl = (b_logprobs[mb_inds] - newlogprob).mean()
+                    if approx_kl > c["kl_target"]:
+                        if rdist.rank() == 0:
+                            print(f"  Early stopping at epoch {epoch + 1} due to KL divergence: {approx_kl:.4f}")
+                        return
+                if world > 1:
+                    mean = stats[1] / count
+                    var = (stats[2] - count * mean * mean) / (count - 1)
+                    mb_adv = (mb_adv - mean) / (var.clamp_min(0).sqrt() + 1e-8)
+                else:
+                    mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+                pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - c["clip_coef"],
+                                                                           1 + c["clip_coef"])).mean()
+                newvalue = newvalue.flatten()
+                v_clip = b_values[mb_inds] + torch.clamp(newvalue - b_values[mb_inds], -c["clip_coef"],
+                                                         c["clip_coef"])
+                v_loss = 0.5 * torch.max((newvalue - b_returns[mb_inds]) ** 2,
+                                         (v_clip - b_returns[mb_inds]) ** 2).mean()
+                loss = pg_loss + c["ent_coef"] * (-entropy.mean()) + c["vf_coef"] * v_loss
+                self.optimizer.zero_grad()
+                loss.backward()
+                rdist.average_gradients(params)
+                nn.utils.clip_grad_norm_(params, c["max_grad_norm"])
+                self.optimizer.step()
+
+    # ------------------------------------------------------------ driver
+    def _anneal(self, update, num_updates):
+        c = self.config
+        frac = max(0.0, 1.0 - update / num_updates)
+        self.optimizer.param_groups[0]["lr"] = frac * c["learning_rate"]
+        lo, hi = self.log_std_schedule
+        self.agent.log_std.data.fill_(frac * lo + (1 - frac) * hi)
+        return frac
+
+    def _speed_weight_anneal(self, frac):
+        w = 8.0 + (1 - frac) * 6.0  # agent/ppo.py:256
+        if self.config.get("apply_speed_weight_anneal", False):
+            self.envs.set_speed_weight(w)
+        return w
+
+    def _buffers(self):
+        c = self.config
+        T, N = c["num_steps"], self.num_local_envs
+        obs_shape = tuple(self.envs.single_observation_space.shape)
+        act_shape = tuple(self.envs.single_action_space.shape)
+        z = lambda *s: torch.zeros(s, device=self.device)  # noqa: E731
+        return (z(T, N, *obs_shape), z(T, N, *act_shape), z(T, N), z(T, N), z(T, N), z(T, N))
+
+    def train(self):
+        c = self.config
+        obs, actions, logprobs, dones, rewards, values = self._buffers()
+        next_obs = self.envs.buf["obs"].clone()  # obs of the reset done at construction
+        next_done = torch.zeros(self.num_local_envs, device=self.device)
+        num_updates = c["total_timesteps"] // c["batch_size"]
+        global_step = 0
+        training_info = {"steps": [], "rewards": []}
+        for update in range(num_updates):
+            frac = self._anneal(update, num_updates)
+            self._speed_weight_anneal(frac)
+            obs, actions, logprobs, dones, rewards, values, next_obs, next_done, ep = self.collect_rollout(
+                obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
+            with torch.no_grad():
+                next_value = self.agent.get_value(next_obs).flatten()
+            advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
+            self.ppo_update(advantages, returns, values, logprobs, actions, obs)
+            global_step += c["batch_size"]
+            self._log(update, num_updates, global_step, ep, training_info)
+        self._save_info(training_info)
+        return training_info
+
+    def _log(self, update, num_updates, global_step, ep, info, extra=""):
+        if ep:
+            info["steps"].append(global_step)
+            info["rewards"].append(float(ep.mean_reward))
+            if rdist.rank() == 0:
+                print(f"Update {update + 1}/{num_updates} | Step {global_step} | Episodes: {len(ep)} | "
+                      f"Mean Reward: {ep.mean_reward:.2f} | Mean Length: {ep.mean_length:.2f}{extra}")
+        elif rdist.rank() == 0:
+            print(f"Update {update + 1}/{num_updates} | Step {global_step} | No episodes completed this rollout")
+
+    def _save_info(self, info):
+        if rdist.rank() != 0:
+            return
+        try:
+            with open(self.info_path, "w") as f:
+                json.dump(info, f)
+            print(f"\nTraining data saved to {self.info_path}")
+        except Exception as e:  # noqa: BLE001 -- agent/ppo.py:282-287 behaviour
+            print(f"Warning: Could not save data: {e}")
+
+    def save(self, path):
+        d = os.path.dirname(path)
+        if d and not os.path.isdir(d):
+            os.makedirs(d, exist_ok=True)
+        torch.save(self.agent.state_dict(), path)
+
+    def load(self, path):
+        self.agent.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))

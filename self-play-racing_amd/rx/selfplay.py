@@ -1,0 +1,195 @@
+"""Two-car self-play (BASELINE.json configs[3]) -- environment/wrappers.py:5-63
+and agent/self_play_ppo.py:8-187 on the device.
+
+``SelfPlayVectorEnv`` exposes agent 0 of N two-car envs as N single-agent
+envs, like N ``SelfPlayWrapper``s inside a SyncVectorEnv, but the opponent
+(agent 1) is driven by ONE batched forward of the frozen policy over all N
+envs per step (the reference runs a batch-1 forward with a host round trip
+per env per step, wrappers.py:36-39), or by uniform random actions drawn on
+the device when the pool is empty (wrappers.py:32-33; Box([-1, 0], [1, 1]),
+so throttle in [0, 1] maps to (a+1)/2 in [0.5, 1] inside the env).
+
+``SelfPlayPPO`` keeps the reference's pool mechanics: snapshot every
+``snapshot_freq`` updates into a FIFO pool of ``pool_size``, an opponent drawn
+with np.random.choice per update (None while the pool is empty), envs rebuilt
+(= reset) every update while next_obs is left stale (SURVEY.md §8 Q10;
+config["refresh_obs_on_rebuild"] = True fixes it), a full checkpoint every 10
+updates, and ``train(resume_from=...)``.
+"""
+import copy
+import json
+
+import numpy as np
+import torch
+
+from . import dist as rdist
+from .agent import Agent
+from .ppo import PPO, EpisodeSummary
+
+
+class SelfPlayVectorEnv:
+    def __init__(self, venv, agent_idx=0, seed=0):
+        if venv.n_agents != 2:
+            raise ValueError("self-play needs a 2-car vector env")
+        self.venv = venv
+        self.agent_idx = agent_idx
+        self.opp_idx = 1 - agent_idx
+        self.num_envs = venv.num_envs
+        self.device = venv.device
+        self.single_observation_space = venv.single_observation_space
+        self.single_action_space = venv.single_action_space
+        self.envs = venv.envs
+        self.opponent_policy = None
+        self._act = torch.zeros((self.num_envs, 2, 2), dtype=torch.float32, device=self.device)
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(int(seed) + 7919)
+        self.buf = {"obs": self.venv.buf["obs"][:, agent_idx]}
+
+    def set_opponent(self, policy):
+        self.opponent_policy = policy
+
+    def _opponent_actions(self):
+        o = self._act[:, self.opp_idx]
+        if self.opponent_policy is None:
+            u = torch.rand((self.num_envs, 2), generator=self._gen, device=self.device)
+            u[:, 0].mul_(2.0).sub_(1.0)  # steer ~ U(-1, 1); throttle ~ U(0, 1)
+            o.copy_(u)
+        else:
+            with torch.no_grad():
+                a = self.opponent_policy.get_action_and_value(self.venv.buf["obs"][:, self.opp_idx])[0]
+            o.copy_(a)
+
+    def reset_device(self):
+        self.venv.reset_device()
+        return self.venv.buf["obs"][:, self.agent_idx]
+
+    def step_device(self, actions, obs_out=None, reward_out=None, done_out=None, **kw):
+        self._opponent_actions()
+        self._act[:, self.agent_idx].copy_(actions)
+        obs, rew, done = self.venv.step_device(self._act, done_out=done_out, **kw)
+        o = obs[:, self.agent_idx]
+        r = rew[:, self.agent_idx]
+        if obs_out is not None:
+            obs_out.copy_(o)
+            o = obs_out
+        if reward_out is not None:
+            reward_out.copy_(r)
+            r = reward_out
+        return o, r, done  # done = dones['__all__'] (wrappers.py:51) = terminated | truncated
+
+    def episode_stats(self, reset=True):
+        return self.venv.episode_stats(reset)
+
+    def close(self):
+        self.venv.close()
+
+
+class SelfPlayPPO(PPO):
+    log_std_schedule = (-0.3, -1.2)  # agent/self_play_ppo.py:128-129
+    info_path = "data/training_info_self_play_3.json"
+    checkpoint_fmt = "models/checkpoint_update_{}.pth"
+
+    def __init__(self, env_fn, config, device="cuda"):
+        self.opponent_pool = []
+        self.curr_opponent = None
+        self.snapshot_freq = config["snapshot_freq"]
+        self.pool_size = config["pool_size"]
+        super().__init__(env_fn, config, device)
+
+    def _make_envs(self, env_fn):
+        from .ppo import build_vector_env
+        c = self.config
+        lo, n = rdist.shard(c["num_envs"])
+        fn = env_fn if lo == 0 else (lambda i: env_fn(lo + i))
+        venv = build_vector_env(fn, n, c["seed"] + rdist.rank(), self.device)
+        return SelfPlayVectorEnv(venv, 0, seed=c["seed"] + rdist.rank())
+
+    def snapshot_agent(self):
+        snap = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
+        snap.load_state_dict(copy.deepcopy(self.agent.state_dict()))
+        snap.eval()
+        for p in snap.parameters():
+            p.requires_grad = False
+        return snap
+
+    def select_opponent(self):
+        if not self.opponent_pool:
+            return None
+        return self.opponent_pool[np.random.choice(len(self.opponent_pool))]
+
+    def update_opponent(self):
+        """agent/self_play_ppo.py:46-50: pick an opponent and rebuild (= reset) the envs."""
+        self.curr_opponent = self.select_opponent()
+        self.envs.set_opponent(self.curr_opponent)
+        self.envs.reset_device()
+
+    def load_checkpoint(self, path):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.agent.load_state_dict(ck["agent_state_dict"])
+        self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+        self.opponent_pool = []
+        for sd in ck["opponent_pool"]:
+            o = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
+            o.load_state_dict(sd)
+            o.eval()
+            for p in o.parameters():
+                p.requires_grad = False
+            self.opponent_pool.append(o)
+        info = ck.get("training_info", {"steps": [], "rewards": [], "opponent_pool_size": []})
+        return ck["update"], ck["global_step"], info
+
+    def train(self, resume_from=None):
+        c = self.config
+        obs, actions, logprobs, dones, rewards, values = self._buffers()
+        next_obs = self.envs.buf["obs"].clone()
+        next_done = torch.zeros(self.num_local_envs, device=self.device)
+        num_updates = c["total_timesteps"] // c["batch_size"]
+        if resume_from:
+            start, global_step, info = self.load_checkpoint(resume_from)
+            start += 1
+        else:
+            start, global_step = 0, 0
+            info = {"steps": [], "rewards": [], "opponent_pool_size": []}
+        for update in range(start, num_updates):
+            if update > 0 and update % self.snapshot_freq == 0:
+                self.opponent_pool.append(self.snapshot_agent())
+                if len(self.opponent_pool) > self.pool_size:
+                    self.opponent_pool.pop(0)
+            self.update_opponent()
+            if c.get("refresh_obs_on_rebuild", False):
+                next_obs.copy_(self.envs.buf["obs"])
+                next_done.zero_()
+            self._anneal(update, num_updates)
+            obs, actions, logprobs, dones, rewards, values, next_obs, next_done, ep = self.collect_rollout(
+                obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
+            with torch.no_grad():
+                next_value = self.agent.get_value(next_obs).flatten()
+            advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
+            self.ppo_update(advantages, returns, values, logprobs, actions, obs)
+            global_step += c["batch_size"]
+            if update > 0 and update % 10 == 0 and rdist.rank() == 0:
+                self.save_checkpoint(update, global_step, info)
+            if ep:
+                info["opponent_pool_size"].append(len(self.opponent_pool))
+            self._log(update, num_updates, global_step, ep, info, extra=f" | Pool Size: {len(self.opponent_pool)}")
+        self._save_info(info)
+        return info
+
+    def save_checkpoint(self, update, global_step, info, path=None):
+        """agent/self_play_ppo.py:146-159 checkpoint dict."""
+        import os
+        path = path or self.checkpoint_fmt.format(update)
+        d = os.path.dirname(path)
+        try:
+            if d:
+                os.makedirs(d, exist_ok=True)
+            torch.save({"update": update, "global_step": global_step, "agent_state_dict": self.agent.state_dict(),
+                        "optimizer_state_dict": self.optimizer.state_dict(),
+                        "opponent_pool": [o.state_dict() for o in self.opponent_pool],
+                        "config": json.loads(json.dumps(self.config)), "training_info": info}, path)
+        except OSError as e:
+            print(f"Warning: could not save checkpoint: {e}")
+        return path
+
+
+__all__ = ["SelfPlayVectorEnv", "SelfPlayPPO", "EpisodeSummary"]

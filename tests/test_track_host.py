@@ -1,0 +1,65 @@
+"""Host track generation/geometry (rx.track) vs the reference's golden geometry.
+
+gen_tracks (environment/track.py:4-56) and Track geometry (track.py:61-157)
+must be bit-identical, including the global-RNG state left behind (the
+reference draws track widths from it right after, train.py:79)."""
+import random
+
+import numpy as np
+
+from rx.track import DEFAULT_CONTROL_POINTS, TrackGeometry, TrackSet, gen_tracks
+
+
+def _pool(n, seed=1):
+    random.seed(seed)
+    np.random.seed(seed)
+    pool = gen_tracks(num_tracks=n, seed=seed)
+    widths = [np.random.randint(6, 10) for _ in range(n)]
+    return pool, widths
+
+
+def test_gen_tracks_seeded_matches_reference(golden):
+    g = golden.geo
+    for n, key in ((16, None), (64, "pool1x64")):
+        pool, widths = _pool(n)
+        if key is None:
+            for k in range(16):
+                assert np.array_equal(pool[k], golden.tracks[k]["cp"])
+            assert widths == list(g["pool1_widths"])
+        else:
+            off = g[key + "_cp_off"]
+            for k in range(n):
+                assert np.array_equal(pool[k], g[key + "_cp"][off[k]:off[k + 1]]), k
+            assert widths == list(g[key + "_widths"])
+
+
+def test_gen_tracks_unseeded_matches_reference(golden):
+    g = golden.geo
+    np.random.seed(7)
+    free = gen_tracks(num_tracks=8, seed=None)
+    off = g["free7x8_cp_off"]
+    for k in range(8):
+        assert np.array_equal(free[k], g["free7x8_cp"][off[k]:off[k + 1]])
+
+
+def test_geometry_bit_exact(golden):
+    for k, t in enumerate(golden.tracks):
+        cp = DEFAULT_CONTROL_POINTS if t["label"] == "default" else t["cp"]
+        geo = TrackGeometry(cp, t["width"] if t["label"] != "default" else None)
+        assert np.array_equal(geo.waypoints, t["wp"]), k
+        assert np.array_equal(geo.normals, t["nrm"]), k
+        assert np.array_equal(geo.segment_cache["starts"], t["starts"]), k
+        assert np.array_equal(geo.segment_cache["v2"], t["v2"]), k
+        assert geo.max_track_distance == t["maxd"], k
+        assert np.array_equal(np.array([float(v) for v in geo.get_start_pos()]), t["start"]), k
+
+
+def test_trackset_dedups_seed1_pool_to_7_slots():
+    pool, widths = _pool(4096)
+    ts = TrackSet()
+    slots = [ts.slot(c, w) for c, w in zip(pool, widths)]
+    assert len(ts) == 7
+    a = ts.arrays()
+    assert a["wp_off"][-1] == sum(len(t.waypoints) for t in ts.geoms)
+    assert a["seg"].shape == (2 * a["wp_off"][-1], 4)
+    assert max(slots) == 6
