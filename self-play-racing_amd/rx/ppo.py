@@ -202,14 +202,15 @@ class PPO:
         z = lambda *s: torch.zeros(s, device=self.device)  # noqa: E731
         return (z(T, N, *obs_shape), z(T, N, *act_shape), z(T, N), z(T, N), z(T, N), z(T, N))
 
-    def train(self):
+    def train_iter(self):
+        """agent/ppo.py:211-281 as a generator: yields (update, num_updates,
+        global_step, EpisodeSummary) after every update (evaluation hooks)."""
         c = self.config
         obs, actions, logprobs, dones, rewards, values = self._buffers()
         next_obs = self.envs.buf["obs"].clone()  # obs of the reset done at construction
         next_done = torch.zeros(self.num_local_envs, device=self.device)
         num_updates = c["total_timesteps"] // c["batch_size"]
         global_step = 0
-        training_info = {"steps": [], "rewards": []}
         for update in range(num_updates):
             frac = self._anneal(update, num_updates)
             self._speed_weight_anneal(frac)
@@ -220,6 +221,11 @@ class PPO:
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
             global_step += c["batch_size"]
+            yield update, num_updates, global_step, ep
+
+    def train(self):
+        training_info = {"steps": [], "rewards": []}
+        for update, num_updates, global_step, ep in self.train_iter():
             self._log(update, num_updates, global_step, ep, training_info)
         self._save_info(training_info)
         return training_info

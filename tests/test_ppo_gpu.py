@@ -144,3 +144,16 @@ def test_selfplay_opponent_batched_forward():
     o, r, d = sp.step_device(a)
     assert o.shape == (8, 19) and r.shape == (8,) and d.shape == (8,)
     assert torch.equal(sp._act[:, 0], a) and sp._act[:, 1].abs().max() <= 1.0
+
+
+def test_evaluator_protocol_runs():
+    from rx.agent import Agent
+    from rx.evaluate import Evaluator
+    ev = Evaluator(max_steps=300, device="cuda")
+    assert ev.venv.num_envs == 200 and len(ev.venv.tracks) <= 12
+    torch.manual_seed(0)
+    ag = Agent(ev.venv.single_observation_space, ev.venv.single_action_space).cuda()
+    res = ev.run(ag)
+    assert res["num_episodes"] == 200 and 0.0 <= res["success_rate"] <= 1.0
+    assert res["crash_rate"] > 0.5  # an untrained policy crashes
+    ev.close()

@@ -63,3 +63,15 @@ def test_trackset_dedups_seed1_pool_to_7_slots():
     assert a["wp_off"][-1] == sum(len(t.waypoints) for t in ts.geoms)
     assert a["seg"].shape == (2 * a["wp_off"][-1], 4)
     assert max(slots) == 6
+
+
+def test_eval_pool_matches_reference_protocol(golden):
+    """evaluate.py:178-182 pool (the golden set drew it after np.random.seed(12345))."""
+    from rx.evaluate import eval_pool
+    cps, ws, ids = eval_pool(40, 5, 42, global_seed=12345)
+    assert len(cps) == 200 and ids[7] == (1, 2)
+    labels = [t["label"] for t in golden.tracks]
+    for t in range(4):
+        k = labels.index(f"eval42[{t}] w={int(golden.geo['eval42_widths'][t])}")
+        assert np.array_equal(cps[5 * t], golden.tracks[k]["cp"])
+    assert ws[:5] == list(golden.geo["eval42_widths"][:5])  # widths indexed by RUN (evaluate.py:30)
