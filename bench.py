@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cull-chunk", type=int, default=16, help="raycast chunk culling (0 = brute force)")
+    ap.add_argument("--sort-interval", type=int, default=0, help="spatial env re-sort period (0 = never)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,7 +105,8 @@ def main():
     n_total = E * world
     pool, widths = seed1_pool(n_total)
     lo, hi = rank * E, (rank + 1) * E
-    env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step")
+    env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step",
+                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval)
     n_slots = len(env.tracks)
     S_of_env = 2 * np.diff(env.tracks.arrays()["wp_off"])[env.track_of_env]
     ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))
@@ -177,6 +180,7 @@ def main():
             "config": {"workload": "configs[2]: 65536 single-agent racing envs per GPU (seed-1 gen_tracks pool, "
                                    "11 sensors, uniform random device actions, next-step autoreset)",
                        "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
+                       "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,

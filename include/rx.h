@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 1
+#define RX_ABI_VERSION 2
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -75,6 +75,8 @@ typedef struct {
   uint64_t seed;           /* device RNG (two-car start-slot shuffle) */
   double sensor_half_cone; /* pi/3 (racing_env.py:45) or pi/2 (multi_racing_env.py:50) */
   double speed_weight;     /* RacingEnv.speed_weight, 8.0 (racing_env.py:9,26) */
+  int32_t cull_chunk;      /* raycast culling: segments per chunk (16 recommended; 0 = test every segment) */
+  int32_t sort_interval;   /* re-sort envs by track position every k dynamics launches (0 = never) */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are

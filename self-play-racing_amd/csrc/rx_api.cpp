@@ -73,18 +73,87 @@ struct rx_env {
   std::vector<int32_t> wp_off_h;
   DevBuf<int32_t> wp_off;
   DevBuf<double> wp, nrm, seg, meta;
+  // raycast culling tables (derived from the track table)
+  DevBuf<int32_t> chunk_off;
+  DevBuf<double> chunk_box, slot_geo;
   // assignment
   bool assigned = false;
-  DevBuf<int32_t> perm;
+  DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
+  int cur = 0;
   DevBuf<rx_wave> dyn_waves, ray_waves;
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
+  // spatial sort (scheduling only)
+  DevBuf<uint32_t> keys_in, keys_out;
+  DevBuf<int32_t> vals_in;
+  DevBuf<char> sort_tmp;
+  size_t sort_tmp_bytes = 0;
+  int sort_bits = 16;
+  uint64_t dyn_calls = 0;
   // state
   bool bound = false;
   rx_state st{};
   uint64_t calls = 0;
 };
+
+namespace {
+// Culling tables for every slot: chunks of G consecutive boundary segments
+// (per side), their end-point boxes, and per slot the bounding circle of all
+// boundary points and the longest segment (kernel margins).
+int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* seg) {
+  const int G = h->cfg.cull_chunk;
+  if (G <= 0) return RX_OK;
+  std::vector<int32_t> off(n_tracks + 1, 0);
+  std::vector<double> boxes, geo(4 * (size_t)n_tracks);
+  for (int k = 0; k < n_tracks; ++k) {
+    const int W = wp_off[k + 1] - wp_off[k];
+    const int nch = (W + G - 1) / G;
+    const double* s = seg + 8 * (size_t)wp_off[k];  // 2W segments x 4
+    double xmin = 1e300, ymin = 1e300, xmax = -1e300, ymax = -1e300, L = 0.0;
+    for (int j = 0; j < 2 * W; ++j) {
+      const double* g = s + 4 * j;
+      const double ex = g[0] + g[2], ey = g[1] + g[3];
+      xmin = std::min({xmin, g[0], ex});
+      xmax = std::max({xmax, g[0], ex});
+      ymin = std::min({ymin, g[1], ey});
+      ymax = std::max({ymax, g[1], ey});
+      L = std::max(L, std::sqrt(g[2] * g[2] + g[3] * g[3]));
+    }
+    const double cx = 0.5 * (xmin + xmax), cy = 0.5 * (ymin + ymax);
+    double rad = 0.0;
+    for (int j = 0; j < 2 * W; ++j) {
+      const double* g = s + 4 * j;
+      const double ex = g[0] + g[2], ey = g[1] + g[3];
+      rad = std::max({rad, std::hypot(g[0] - cx, g[1] - cy), std::hypot(ex - cx, ey - cy)});
+    }
+    geo[4 * k + 0] = cx;
+    geo[4 * k + 1] = cy;
+    geo[4 * k + 2] = rad * (1.0 + 1e-12) + 1e-9;  // round up: the kernel needs an upper bound
+    geo[4 * k + 3] = L * (1.0 + 1e-12) + 1e-12;
+    for (int side = 0; side < 2; ++side) {
+      for (int c = 0; c < nch; ++c) {
+        double bx0 = 1e300, by0 = 1e300, bx1 = -1e300, by1 = -1e300;
+        for (int j = side * W + c * G; j < side * W + std::min(W, (c + 1) * G); ++j) {
+          const double* g = s + 4 * j;
+          const double ex = g[0] + g[2], ey = g[1] + g[3];
+          bx0 = std::min({bx0, g[0], ex});
+          bx1 = std::max({bx1, g[0], ex});
+          by0 = std::min({by0, g[1], ey});
+          by1 = std::max({by1, g[1], ey});
+        }
+        boxes.insert(boxes.end(), {bx0, by0, bx1, by1});
+      }
+    }
+    off[k + 1] = off[k] + 2 * nch;
+  }
+  int rc;
+  if ((rc = upload(h->chunk_off, off.data(), off.size()))) return rc;
+  if ((rc = upload(h->chunk_box, boxes.data(), boxes.size()))) return rc;
+  if ((rc = upload(h->slot_geo, geo.data(), geo.size()))) return rc;
+  return RX_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -146,15 +215,13 @@ int rx_sensor_angles(const rx_env* h, double* out) {
 int rx_destroy(rx_env* h) {
   if (!h) return RX_OK;
   (void)hipSetDevice(h->cfg.device);
-  h->wp_off.release();
-  h->wp.release();
-  h->nrm.release();
-  h->seg.release();
-  h->meta.release();
-  h->perm.release();
+  for (auto* b : {&h->wp, &h->nrm, &h->seg, &h->meta, &h->chunk_box, &h->slot_geo, &h->rel_angles}) b->release();
+  for (auto* b : {&h->wp_off, &h->chunk_off, &h->perm[0], &h->perm[1], &h->vals_in}) b->release();
   h->dyn_waves.release();
   h->ray_waves.release();
-  h->rel_angles.release();
+  h->keys_in.release();
+  h->keys_out.release();
+  h->sort_tmp.release();
   delete h;
   return RX_OK;
 }
@@ -178,6 +245,7 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
   if ((rc = upload(h->nrm, nrm, 2 * Wt))) return rc;
   if ((rc = upload(h->seg, seg, 8 * Wt))) return rc;
   if ((rc = upload(h->meta, meta, 8 * (size_t)n_tracks))) return rc;
+  if ((rc = build_chunks(h, n_tracks, wp_off, seg))) return rc;
   h->wp_off_h.assign(wp_off, wp_off + n_tracks + 1);
   h->n_tracks = n_tracks;
   h->assigned = false;  // slots may have changed meaning: require rx_assign again
@@ -211,7 +279,25 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   }
   RX_HIP(hipSetDevice(h->cfg.device));
   int rc;
-  if ((rc = upload(h->perm, perm.data(), perm.size()))) return rc;
+  if ((rc = upload(h->perm[0], perm.data(), perm.size()))) return rc;
+  if ((rc = upload(h->perm[1], perm.data(), perm.size()))) return rc;
+  h->cur = 0;
+  if (h->cfg.sort_interval > 0) {  // spatial sort buffers (keys: slot << 16 | waypoint)
+    if ((rc = upload(h->vals_in, perm.data(), perm.size()))) return rc;
+    std::vector<uint32_t> zk(N, 0u);
+    if ((rc = upload(h->keys_in, zk.data(), zk.size()))) return rc;
+    if ((rc = upload(h->keys_out, zk.data(), zk.size()))) return rc;
+    int bits = 16;
+    while ((1 << (bits - 16)) < h->n_tracks) ++bits;
+    h->sort_bits = bits;
+    size_t tmp = 0;
+    RX_HIP((hipError_t)rx_sort_pairs(nullptr, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[1].p, N,
+                                     bits, nullptr));
+    h->sort_tmp.release();
+    if (hipMalloc(&h->sort_tmp.p, std::max<size_t>(tmp, 16)) != hipSuccess) return fail(RX_ENOMEM, "sort temp alloc");
+    h->sort_tmp.n = std::max<size_t>(tmp, 16);
+    h->sort_tmp_bytes = tmp;
+  }
   if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
   if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
   h->n_dyn_waves = (int32_t)dyn.size();
@@ -250,12 +336,13 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (!io->obs) return fail(RX_EINVAL, "io->obs is required");
   if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
   rx_kargs a{};
-  a.tr = rx_track_view{h->wp_off.p, h->wp.p, h->nrm.p, h->seg.p, h->meta.p};
+  a.tr = rx_track_view{h->wp_off.p, h->wp.p, h->nrm.p, h->seg.p, h->meta.p,
+                       h->chunk_off.p, h->chunk_box.p, h->slot_geo.p};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;
   a.ray_waves = h->ray_waves.p;
-  a.perm = h->perm.p;
+  a.perm = h->perm[h->cur].p;
   a.rel_angles = h->rel_angles.p;
   a.reset_mask = mask;
   a.n_dyn_waves = h->n_dyn_waves;
@@ -265,13 +352,37 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.max_steps = h->cfg.max_steps;
   a.autoreset = h->cfg.autoreset;
   a.mode = mode;
+  a.cull_chunk = h->chunk_box.p ? h->cfg.cull_chunk : 0;
   a.speed_weight = h->cfg.speed_weight;
   a.seed = h->cfg.seed;
   a.call = ++h->calls;
-  if (!(phases & RX_PHASE_DYNAMICS)) a.n_dyn_waves = 0;
-  if (!(phases & RX_PHASE_RAYS)) a.n_ray_waves = 0;
-  const int rc = rx_launch_step(&a, h->cfg.n_agents, (hipStream_t)stream);
-  if (rc != 0) return fail(RX_EHIP, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if (phases & RX_PHASE_DYNAMICS) {
+    // re-sort the env order every sort_interval dynamics launches (scheduling only)
+    const bool sort = h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
+    if (sort) {
+      a.sort_keys = h->keys_in.p;
+      a.sort_vals = h->vals_in.p;
+    }
+    if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_DYNAMICS, s)) != 0)
+      return fail(RX_EHIP, "k_dyn launch failed: %s", hipGetErrorString((hipError_t)rc));
+    if (sort) {
+      size_t tmp = h->sort_tmp_bytes;
+      const int nxt = 1 - h->cur;
+      if ((rc = rx_sort_pairs(h->sort_tmp.p, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[nxt].p,
+                              h->cfg.n_envs, h->sort_bits, s)) != 0)
+        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
+      h->cur = nxt;
+      a.perm = h->perm[nxt].p;
+    }
+  }
+  if (phases & RX_PHASE_RAYS) {
+    a.sort_keys = nullptr;
+    a.sort_vals = nullptr;
+    if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_RAYS, s)) != 0)
+      return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
+  }
   return RX_OK;
 }
 

@@ -21,11 +21,15 @@ struct rx_wave {
 };
 
 struct rx_track_view {
-  const int32_t* wp_off;  // [n+1]
-  const double* wp;       // [Wtot][2]
-  const double* nrm;      // [Wtot][2]
-  const double* seg;      // [2*Wtot][4]
-  const double* meta;     // [n][8]
+  const int32_t* wp_off;     // [n+1]
+  const double* wp;          // [Wtot][2]
+  const double* nrm;         // [Wtot][2]
+  const double* seg;         // [2*Wtot][4]
+  const double* meta;        // [n][8]
+  // raycast culling (derived by rx_upload_tracks)
+  const int32_t* chunk_off;  // [n+1] first chunk of each slot (2*ceil(W/G) chunks per slot: left side, right side)
+  const double* chunk_box;   // [n_chunks][4] xmin, ymin, xmax, ymax of the chunk's segment end points
+  const double* slot_geo;    // [n][4] bounding-circle centre x, y, radius of all boundary points; max |v2|
 };
 
 struct rx_kargs {
@@ -34,9 +38,11 @@ struct rx_kargs {
   rx_io io;
   const rx_wave* dyn_waves;
   const rx_wave* ray_waves;
-  const int32_t* perm;
+  const int32_t* perm;        // env order the kernels read (sorted by slot, then position)
   const double* rel_angles;   // [n_sensors]
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
+  uint32_t* sort_keys;        // [N] k_dyn writes (slot << 16 | waypoint) at its perm position, or nullptr
+  int32_t* sort_vals;         // [N] k_dyn writes the env id at its perm position
   int32_t n_dyn_waves;
   int32_t n_ray_waves;
   int32_t n_sensors;
@@ -44,12 +50,14 @@ struct rx_kargs {
   int32_t max_steps;
   int32_t autoreset;
   int32_t mode;
-  int32_t pad_;
+  int32_t cull_chunk;         // segments per culling chunk G (0 = brute force over all segments)
   double speed_weight;
   uint64_t seed;
   uint64_t call;
 };
 
-extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, hipStream_t s);
+extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
+extern "C" int rx_sort_pairs(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                             int32_t* vout, int n, int end_bit, hipStream_t s);

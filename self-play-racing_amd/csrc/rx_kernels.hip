@@ -129,6 +129,19 @@ __device__ __forceinline__ bool corner_out(const double2* __restrict__ wp, const
 
 __device__ __forceinline__ double speed_of(double vx, double vy) { return __builtin_sqrt(rx_sq(vx) + rx_sq(vy)); }
 
+// Spatial-coherence key for the next wave assignment: (slot, waypoint of the
+// car).  Sorting by it (rx_sort_pairs) keeps slot groups in place and puts
+// cars that are near each other on the track into the same wavefronts, which
+// is what makes k_rays' per-wave chunk culling effective.  Pure scheduling:
+// results never depend on the order.
+__device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k, int e, double progress, int W) {
+  if (!a.sort_keys) return;
+  int w = (int)(progress * (double)W + 0.5);
+  w = w < 0 ? 0 : (w > 0xffff ? 0xffff : w);
+  a.sort_keys[pos] = ((uint32_t)k << 16) | (uint32_t)w;
+  a.sort_vals[pos] = e;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -302,6 +315,7 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
     o[2] = (float)rx_clip(0.0 / 3.0, -1.0, 1.0);  // angular_velocity is always 0
     o[3] = (float)last_steering;
   }
+  write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
 }
 
 // ============================================================ k_dyn, A == 2
@@ -586,6 +600,7 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     ob[6] = (float)rx_clip(lvx / RX_MAX_SPEED, -1.0, 1.0);
     ob[7] = (float)rx_clip(lvy / RX_MAX_SPEED, -1.0, 1.0);
   }
+  write_sort_key(a, we.perm_start + lane, k, e, c[0].progress, W);
 }
 
 // ============================================================ k_rays
@@ -602,6 +617,67 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
 //   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
 // (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
 // range its rounding cannot cross the threshold).  Only hit segments divide.
+__device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
+                                             double v3x, double v3y, double& best) {
+#pragma unroll 4
+  for (int j = j0; j < j1; ++j) {
+    const double4 g = seg[j];  // wave-uniform -> s_load_dwordx8
+    const double v1x = ox - g.x, v1y = oy - g.y;
+    const double dotp = g.z * v3x + g.w * v3y;
+    const double cross = g.z * v1y - g.w * v1x;
+    const double dot = v1x * v3x + v1y * v3y;
+    const double D = __builtin_fabs(dotp);
+    const bool neg = dotp < 0.0;
+    const double C = neg ? -cross : cross;
+    const double N = neg ? -dot : dot;
+    const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
+    if (hit) {
+      const double t = C / D;
+      best = t < best ? t : best;
+    }
+  }
+}
+
+// Chunk culling (exact; derivation in DESIGN.md §3).  The 2W boundary
+// segments of a slot are cut into chunks of G consecutive segments with
+// axis-aligned boxes of their end points.  A computed hit on segment j means
+// the exact line intersection P = o + t*.d lies within eps_s|v2| of the
+// segment and the computed t_j >= t* - eps_t, where (|D| > 1e-10, |v1| <= R,
+// t* <= T, |v2| <= L, u = 2^-53)
+//   eps_t  <= u*L*(4R + 2T)/1e-10 + u*T,    eps_s|v2| <= u*(3R + 2L)*L/1e-10.
+// So with the box grown by mb >= eps_s|v2| and the slab entry distance
+// t_in <= t*, every hit of a chunk has t_j >= t_in - mt; if that is >= the
+// lane's best t found so far, no segment of the chunk can lower the minimum
+// and the chunk is skipped.  A wave skips a chunk only if all its lanes may.
+// Chunks are visited outward from the wave's first car, so best tightens
+// early; envs are kept spatially sorted (write_sort_key) so a wave's cars
+// are neighbours.
+__device__ __forceinline__ bool chunk_needed(const double* __restrict__ box, double mb, double mt, double ox,
+                                             double oy, double dx, double dy, double idx_, double idy_, double best) {
+  const double x0 = box[0] - mb, y0 = box[1] - mb, x1 = box[2] + mb, y1 = box[3] + mb;
+  double lo = -mt, hi = __builtin_inf();
+  bool miss = false;
+  if (dx != 0.0) {
+    const double t1 = (x0 - ox) * idx_, t2 = (x1 - ox) * idx_;
+    lo = __builtin_fmax(lo, __builtin_fmin(t1, t2));
+    hi = __builtin_fmin(hi, __builtin_fmax(t1, t2));
+  } else {
+    miss = miss || ox < x0 || ox > x1;
+  }
+  if (dy != 0.0) {
+    const double t1 = (y0 - oy) * idy_, t2 = (y1 - oy) * idy_;
+    lo = __builtin_fmax(lo, __builtin_fmin(t1, t2));
+    hi = __builtin_fmin(hi, __builtin_fmax(t1, t2));
+  } else {
+    miss = miss || oy < y0 || oy > y1;
+  }
+  // slack for the rounding of the slab arithmetic itself
+  const double lo_s = lo - (__builtin_fabs(lo) * 0x1p-40 + 1e-9);
+  const double hi_s = hi + (__builtin_fabs(hi) * 0x1p-40 + 1e-9);
+  miss = miss || (lo_s > hi_s);
+  return !miss && (lo_s - mt < best);
+}
+
 template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -610,7 +686,8 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int lane = threadIdx.x & 63;
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
-  const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
+  const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
+  const int S_ = 2 * W;
   const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
   if (lane >= we.count) return;
   const int R = a.n_sensors;
@@ -627,21 +704,39 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   rx_sincos(theta, &sn, &cs);
   const double v3x = -sn, v3y = cs;
   double best = __builtin_inf();
-#pragma unroll 4
-  for (int j = 0; j < S_; ++j) {
-    const double4 g = seg[j];  // wave-uniform -> s_load_dwordx8
-    const double v1x = ox - g.x, v1y = oy - g.y;
-    const double dotp = g.z * v3x + g.w * v3y;
-    const double cross = g.z * v1y - g.w * v1x;
-    const double dot = v1x * v3x + v1y * v3y;
-    const double D = __builtin_fabs(dotp);
-    const bool neg = dotp < 0.0;
-    const double C = neg ? -cross : cross;
-    const double N = neg ? -dot : dot;
-    const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
-    if (hit) {
-      const double t = C / D;
-      best = t < best ? t : best;
+  const int G = a.cull_chunk;
+  if (G <= 0) {
+    ray_segments(seg, 0, S_, ox, oy, v3x, v3y, best);
+  } else {
+    const int nch = (W + G - 1) / G;  // chunks per side
+    const double* __restrict__ boxes = a.tr.chunk_box + 4 * (size_t)uniform(a.tr.chunk_off[k]);
+    const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
+    const double cx = sg[0], cy = sg[1], rad = sg[2], L = sg[3];
+    const double ddx = ox - cx, ddy = oy - cy;
+    const double Rr = __builtin_sqrt(ddx * ddx + ddy * ddy) + rad;  // >= |o - p| for every boundary point p
+    const double T = Rr + L;
+    const double u2 = 0x1p-52;  // 2u: factor-2 safety on both bounds
+    const double mt = u2 * L * (4.0 * Rr + 2.0 * T) * 1e10 + u2 * T + 1e-9;
+    const double mb = u2 * (3.0 * Rr + 2.0 * L) * L * 1e10 + 1e-9;
+    const double idx_ = cs != 0.0 ? 1.0 / cs : 0.0;  // ray direction d = (cos, sin)
+    const double idy_ = sn != 0.0 ? 1.0 / sn : 0.0;
+    // visit chunks outward from the wave's first car
+    int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
+    w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
+    const int c0 = uniform(w0 / G);
+    for (int s = 0; s < nch; ++s) {
+      const int off = (s + 1) >> 1;
+      int c = (s & 1) ? c0 - off : c0 + off;
+      c = c < 0 ? c + nch : (c >= nch ? c - nch : c);
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const bool need = chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best);
+        if (__any(need)) {
+          const int j0 = side * W + c * G;
+          const int j1 = side * W + min(W, (c + 1) * G);
+          ray_segments(seg, j0, j1, ox, oy, v3x, v3y, best);
+        }
+      }
     }
   }
   double dist = (best == __builtin_inf()) ? RX_MAX_RANGE : best;
@@ -751,16 +846,16 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 }  // namespace
 
 // ------------------------------------------------------------ launchers
-extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, hipStream_t s) {
+extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s) {
   const dim3 blk(256);
-  if (a->n_dyn_waves > 0) {
+  if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
     if (n_agents == 1)
       hipLaunchKernelGGL(k_dyn1, grd, blk, 0, s, *a);
     else
       hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
   }
-  if (a->n_ray_waves > 0) {
+  if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
     const dim3 grd((a->n_ray_waves + 3) / 4);
     if (n_agents == 1)
       hipLaunchKernelGGL(k_rays<1>, grd, blk, 0, s, *a);

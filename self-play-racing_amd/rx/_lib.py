@@ -13,6 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
+ABI_VERSION = 2
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -31,7 +32,8 @@ RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
 class RxConfig(ctypes.Structure):
     _fields_ = [("n_envs", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_sensors", ctypes.c_int32),
                 ("max_steps", ctypes.c_int32), ("autoreset", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double)]
+                ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double),
+                ("cull_chunk", ctypes.c_int32), ("sort_interval", ctypes.c_int32)]
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
@@ -90,8 +92,8 @@ def load(build_if_missing=True):
     for name in EXPORTS:
         if name not in ("rx_last_error", "rx_abi_version"):
             getattr(L, name).restype = ctypes.c_int
-    if L.rx_abi_version() != 1:
-        raise RxError(f"librx ABI {L.rx_abi_version()} != 1")
+    if L.rx_abi_version() != ABI_VERSION:
+        raise RxError(f"librx ABI {L.rx_abi_version()} != {ABI_VERSION} (rebuild: python -m rx._build)")
     _lib = L
     return L
 
