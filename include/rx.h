@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 2
+#define RX_ABI_VERSION 3
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -115,6 +115,8 @@ typedef struct {
   double* info;          /* [N][A][RX_INFO_W] */
   uint8_t* ep_done;      /* [N] an episode ended this step (infos['_episode']) */
   double* ep_stats;      /* [3] += (sum return, sum length, count) of episodes ended */
+  unsigned long long* counters; /* [4] profiling, NULL = off: += per wave (raycast chunk tests,
+                                   raycast chunks scanned, waypoint chunk tests, waypoint chunks scanned) */
 } rx_io;
 
 const char* rx_last_error(void);

@@ -75,7 +75,8 @@ struct rx_env {
   DevBuf<double> wp, nrm, seg, meta;
   // raycast culling tables (derived from the track table)
   DevBuf<int32_t> chunk_off;
-  DevBuf<double> chunk_box, slot_geo;
+  DevBuf<double> chunk_box, slot_geo, wchunk_box;
+  DevBuf<int32_t> wchunk_off;
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
@@ -101,11 +102,11 @@ namespace {
 // Culling tables for every slot: chunks of G consecutive boundary segments
 // (per side), their end-point boxes, and per slot the bounding circle of all
 // boundary points and the longest segment (kernel margins).
-int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* seg) {
+int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* seg) {
   const int G = h->cfg.cull_chunk;
   if (G <= 0) return RX_OK;
-  std::vector<int32_t> off(n_tracks + 1, 0);
-  std::vector<double> boxes, geo(4 * (size_t)n_tracks);
+  std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0);
+  std::vector<double> boxes, wboxes, geo(4 * (size_t)n_tracks);
   for (int k = 0; k < n_tracks; ++k) {
     const int W = wp_off[k + 1] - wp_off[k];
     const int nch = (W + G - 1) / G;
@@ -146,11 +147,27 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
       }
     }
     off[k + 1] = off[k] + 2 * nch;
+    // waypoint chunks (argmin culling): RX_WP_CHUNK consecutive waypoints each
+    const double* w = wp + 2 * (size_t)wp_off[k];
+    const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
+    for (int c = 0; c < nwc; ++c) {
+      double bx0 = 1e300, by0 = 1e300, bx1 = -1e300, by1 = -1e300;
+      for (int i = c * RX_WP_CHUNK; i < std::min(W, (c + 1) * RX_WP_CHUNK); ++i) {
+        bx0 = std::min(bx0, w[2 * i]);
+        bx1 = std::max(bx1, w[2 * i]);
+        by0 = std::min(by0, w[2 * i + 1]);
+        by1 = std::max(by1, w[2 * i + 1]);
+      }
+      wboxes.insert(wboxes.end(), {bx0, by0, bx1, by1});
+    }
+    woff[k + 1] = woff[k] + nwc;
   }
   int rc;
   if ((rc = upload(h->chunk_off, off.data(), off.size()))) return rc;
   if ((rc = upload(h->chunk_box, boxes.data(), boxes.size()))) return rc;
   if ((rc = upload(h->slot_geo, geo.data(), geo.size()))) return rc;
+  if ((rc = upload(h->wchunk_off, woff.data(), woff.size()))) return rc;
+  if ((rc = upload(h->wchunk_box, wboxes.data(), wboxes.size()))) return rc;
   return RX_OK;
 }
 }  // namespace
@@ -215,8 +232,9 @@ int rx_sensor_angles(const rx_env* h, double* out) {
 int rx_destroy(rx_env* h) {
   if (!h) return RX_OK;
   (void)hipSetDevice(h->cfg.device);
-  for (auto* b : {&h->wp, &h->nrm, &h->seg, &h->meta, &h->chunk_box, &h->slot_geo, &h->rel_angles}) b->release();
-  for (auto* b : {&h->wp_off, &h->chunk_off, &h->perm[0], &h->perm[1], &h->vals_in}) b->release();
+  for (auto* b : {&h->wp, &h->nrm, &h->seg, &h->meta, &h->chunk_box, &h->slot_geo, &h->wchunk_box, &h->rel_angles})
+    b->release();
+  for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->perm[0], &h->perm[1], &h->vals_in}) b->release();
   h->dyn_waves.release();
   h->ray_waves.release();
   h->keys_in.release();
@@ -245,7 +263,7 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
   if ((rc = upload(h->nrm, nrm, 2 * Wt))) return rc;
   if ((rc = upload(h->seg, seg, 8 * Wt))) return rc;
   if ((rc = upload(h->meta, meta, 8 * (size_t)n_tracks))) return rc;
-  if ((rc = build_chunks(h, n_tracks, wp_off, seg))) return rc;
+  if ((rc = build_chunks(h, n_tracks, wp_off, wp, seg))) return rc;
   h->wp_off_h.assign(wp_off, wp_off + n_tracks + 1);
   h->n_tracks = n_tracks;
   h->assigned = false;  // slots may have changed meaning: require rx_assign again
@@ -337,7 +355,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
   rx_kargs a{};
   a.tr = rx_track_view{h->wp_off.p, h->wp.p, h->nrm.p, h->seg.p, h->meta.p,
-                       h->chunk_off.p, h->chunk_box.p, h->slot_geo.p};
+                       h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;

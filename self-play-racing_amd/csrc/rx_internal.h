@@ -30,7 +30,12 @@ struct rx_track_view {
   const int32_t* chunk_off;  // [n+1] first chunk of each slot (2*ceil(W/G) chunks per slot: left side, right side)
   const double* chunk_box;   // [n_chunks][4] xmin, ymin, xmax, ymax of the chunk's segment end points
   const double* slot_geo;    // [n][4] bounding-circle centre x, y, radius of all boundary points; max |v2|
+  // closest-waypoint culling: chunks of RX_WP_CHUNK consecutive waypoints
+  const int32_t* wchunk_off; // [n+1]
+  const double* wchunk_box;  // [n_wchunks][4]
 };
+
+#define RX_WP_CHUNK 32
 
 struct rx_kargs {
   rx_track_view tr;

@@ -84,6 +84,91 @@ __device__ __forceinline__ void argmin_pts(const double2* __restrict__ wp, int W
   }
 }
 
+// Closest waypoint of the car's previous position (progress = idx / W exactly).
+__device__ __forceinline__ int prev_waypoint(double progress, int W) {
+  int i = (int)(progress * (double)W + 0.5);
+  return i < 0 ? 0 : (i >= W ? W - 1 : i);
+}
+
+// Order-independent argmin update: smaller distance, or equal distance and a
+// smaller index -- the same result as the reference's first-index argmin
+// whatever order the waypoints are visited in.
+__device__ __forceinline__ void argmin_take(double d, int i, double& best, int& idx) {
+  const bool take = (d < best) | ((d == best) & (i < idx));
+  best = take ? d : best;
+  idx = take ? i : idx;
+}
+
+// The same argmin with culling (exact).  Phase 1: every lane scans a window
+// of 2H+1 waypoints around ITS car's previous closest waypoint (per-lane
+// gathers; the car moved <= 1.5 units, so the window nearly always holds the
+// answer).  Phase 2: the slot's waypoint chunks are visited wave-uniformly;
+// a chunk is scanned (scalar loads) only if for some lane and point the
+// box's squared distance lower bound does not exceed that point's best.
+// The bound is shrunk by 2^-46 relative, far beyond the few-ulp rounding of
+// both the bound and the per-waypoint distances, so a skipped chunk can
+// neither beat nor tie the best (ties are broken by index, argmin_take).
+template <int NP, int NC>
+__device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, const double* __restrict__ wbox, int W,
+                                              const double px[NP], const double py[NP], const int prev[NC],
+                                              int idx[NP], unsigned long long* counters) {
+  constexpr int PPC = NP / NC;  // points per car
+  constexpr int H = 6;
+  double best[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    best[p] = __builtin_inf();
+    idx[p] = 0x7fffffff;
+  }
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    for (int j = -H; j <= H; ++j) {
+      int i = prev[q] + j;
+      i = i < 0 ? i + W : (i >= W ? i - W : i);
+      const double2 w = wp[i];  // per-lane gather (L1/L2 resident)
+#pragma unroll
+      for (int p = q * PPC; p < (q + 1) * PPC; ++p) {
+        const double dx = w.x - px[p], dy = w.y - py[p];
+        argmin_take(dx * dx + dy * dy, i, best[p], idx[p]);
+      }
+    }
+  }
+  const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
+  const int c0 = uniform(prev[0] / RX_WP_CHUNK);
+  int scanned = 0;
+  for (int s = 0; s < nwc; ++s) {
+    const int off = (s + 1) >> 1;
+    int c = (s & 1) ? c0 - off : c0 + off;
+    c = c < 0 ? c + nwc : (c >= nwc ? c - nwc : c);
+    const double* b = wbox + 4 * c;
+    const double x0 = b[0], y0 = b[1], x1 = b[2], y1 = b[3];
+    bool need = false;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const double gx = __builtin_fmax(__builtin_fmax(x0 - px[p], px[p] - x1), 0.0);
+      const double gy = __builtin_fmax(__builtin_fmax(y0 - py[p], py[p] - y1), 0.0);
+      const double lb = (gx * gx + gy * gy) * (1.0 - 0x1p-46);
+      need = need | !(lb > best[p]);
+    }
+    if (__any(need)) {
+      ++scanned;
+      const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
+      for (int i = c * RX_WP_CHUNK; i < i1; ++i) {
+        const double2 w = wp[i];  // uniform -> s_load
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const double dx = w.x - px[p], dy = w.y - py[p];
+          argmin_take(dx * dx + dy * dy, i, best[p], idx[p]);
+        }
+      }
+    }
+  }
+  if (counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
+    atomicAdd(&counters[2], (unsigned long long)nwc);
+    atomicAdd(&counters[3], (unsigned long long)scanned);
+  }
+}
+
 // Car.update -- environment/car.py:45-80, minus the argmins (done by the
 // caller for all cars of the lane in one pass).  Returns cos/sin of the new
 // angle and the 4 corners.
@@ -198,7 +283,13 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
     double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
     double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
     int idx[5];
-    argmin_pts<5>(wp, W, px, py, idx);
+    if (a.cull_chunk > 0) {
+      const int prev[1] = {prev_waypoint(c.progress, W)};
+      argmin_culled<5, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, px, py, prev, idx,
+                          a.io.counters);
+    } else {
+      argmin_pts<5>(wp, W, px, py, idx);
+    }
     c.progress = (double)idx[0] / (double)W;  // track.py:159-161
     bool out = false;
 #pragma unroll
@@ -444,7 +535,13 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
         }
       }
       int idx[10];
-      argmin_pts<10>(wp, W, px, py, idx);
+      if (a.cull_chunk > 0) {
+        const int prev[2] = {prev_waypoint(c[0].progress, W), prev_waypoint(c[1].progress, W)};
+        argmin_culled<10, 2>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, px, py, prev, idx,
+                             a.io.counters);
+      } else {
+        argmin_pts<10>(wp, W, px, py, idx);
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (!mv[q]) continue;
@@ -724,6 +821,7 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
     int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
     const int c0 = uniform(w0 / G);
+    int scanned = 0;
     for (int s = 0; s < nch; ++s) {
       const int off = (s + 1) >> 1;
       int c = (s & 1) ? c0 - off : c0 + off;
@@ -732,11 +830,16 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
       for (int side = 0; side < 2; ++side) {
         const bool need = chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best);
         if (__any(need)) {
+          ++scanned;
           const int j0 = side * W + c * G;
           const int j1 = side * W + min(W, (c + 1) * G);
           ray_segments(seg, j0, j1, ox, oy, v3x, v3y, best);
         }
       }
+    }
+    if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
+      atomicAdd(&a.io.counters[0], (unsigned long long)(2 * nch));
+      atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
   }
   double dist = (best == __builtin_inf()) ? RX_MAX_RANGE : best;

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -45,7 +45,7 @@ class RxState(ctypes.Structure):
 
 
 IO_FIELDS = ("actions", "obs", "reward", "reward64", "terminated", "truncated", "done_f32", "info", "ep_done",
-             "ep_stats")
+             "ep_stats", "counters")
 
 
 class RxIO(ctypes.Structure):

@@ -128,6 +128,7 @@ class RacingVectorEnv:
         self.action_space = Box(np.tile(self.single_action_space.low, (N, 1)),
                                 np.tile(self.single_action_space.high, (N, 1)), shape=(N, 2), dtype=np.float32)
         self.envs = [_EnvProxy(i) for i in range(N)]
+        self.counters = None
         self._episode_start = np.full(N, time.perf_counter())
         self._closed = False
 
@@ -151,7 +152,19 @@ class RacingVectorEnv:
             _lib.ptr(b["info"]) if full else None,
             _lib.ptr(b["ep_done"]),
             _lib.ptr(b["ep_stats"]),
+            _lib.ptr(self.counters) if self.counters is not None else None,
         )
+
+    def enable_counters(self, on=True):
+        """Per-wave culling counters (rx_io.counters): chunk tests / scans."""
+        self.counters = torch.zeros(4, dtype=torch.int64, device=self.device) if on else None
+
+    def read_counters(self, reset=True):
+        c = self.counters.cpu().numpy().copy()
+        if reset:
+            self.counters.zero_()
+        return {"ray_chunk_tests": int(c[0]), "ray_chunks_scanned": int(c[1]), "wp_chunk_tests": int(c[2]),
+                "wp_chunks_scanned": int(c[3])}
 
     def _state_struct(self):
         return _lib.RxState(*[_lib.ptr(self.state[k]) for k in _lib.STATE_FIELDS])
