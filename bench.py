@@ -47,6 +47,31 @@ def seed1_pool(n_total):
     return pool, widths
 
 
+def gae_roofline(n_envs, dev, T=128, reps=20):
+    """k_gae (agent/ppo.py:134-154) on a [T, N] rollout: HBM-bound, 20 B per
+    (t, env) element (read r, v, d; write A, R; f32) -- SURVEY.md §8(d)."""
+    from rx.gae import compute_gae
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = torch.randn((T, n_envs), generator=g, device=dev)
+    v = torch.randn((T, n_envs), generator=g, device=dev)
+    d = (torch.rand((T, n_envs), generator=g, device=dev) < 0.02).float()
+    nv = torch.randn(n_envs, generator=g, device=dev)
+    nd = torch.zeros(n_envs, device=dev)
+    out = (torch.empty_like(r), torch.empty_like(r))
+    for _ in range(3):
+        compute_gae(r, d, v, nv, nd, 0.99, 0.95, out=out)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        compute_gae(r, d, v, nv, nd, 0.99, 0.95, out=out)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    gbs = 20.0 * T * n_envs / (ms * 1e-3) / 1e9
+    return {"kernel": "k_gae", "T": T, "N": n_envs, "avg_launch_ms": round(ms, 5), "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
+
+
 def cpu_baseline(pool, widths, budget_s=15.0, n_envs=16):
     """The reference's CPU execution model (NumPy step per env, sequential loop,
     16 envs = configs/base_config.py num_envs) on one host core, bounded in time."""
@@ -152,6 +177,7 @@ def main():
     dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
     ep = env.episode_stats()
+    gae = gae_roofline(E, dev) if rank == 0 else None
 
     if rank == 0:
         value = n_total * args.steps / elapsed
@@ -190,6 +216,7 @@ def main():
                                  "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TF,
                                  "flops_per_launch": ray_flops_per_launch},
             "kernels_ms": {"k_dyn1": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
+            "gae": gae,
             "episodes_ended": ep[2],
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -82,6 +82,7 @@ struct rx_env {
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
   int cur = 0;
   DevBuf<rx_wave> dyn_waves, ray_waves;
+  DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -95,7 +96,6 @@ struct rx_env {
   // state
   bool bound = false;
   rx_state st{};
-  uint64_t calls = 0;
 };
 
 namespace {
@@ -300,6 +300,10 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if ((rc = upload(h->perm[0], perm.data(), perm.size()))) return rc;
   if ((rc = upload(h->perm[1], perm.data(), perm.size()))) return rc;
   h->cur = 0;
+  if (A == 2) {
+    std::vector<uint32_t> z(N, 0u);
+    if ((rc = upload(h->resets, z.data(), z.size()))) return rc;
+  }
   if (h->cfg.sort_interval > 0) {  // spatial sort buffers (keys: slot << 16 | waypoint)
     if ((rc = upload(h->vals_in, perm.data(), perm.size()))) return rc;
     std::vector<uint32_t> zk(N, 0u);
@@ -373,7 +377,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.cull_chunk = h->chunk_box.p ? h->cfg.cull_chunk : 0;
   a.speed_weight = h->cfg.speed_weight;
   a.seed = h->cfg.seed;
-  a.call = ++h->calls;
+  a.reset_count = h->resets.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;
   if (phases & RX_PHASE_DYNAMICS) {

@@ -58,7 +58,7 @@ struct rx_kargs {
   int32_t cull_chunk;         // segments per culling chunk G (0 = brute force over all segments)
   double speed_weight;
   uint64_t seed;
-  uint64_t call;
+  uint32_t* reset_count;  // [N] (2-car envs), advanced by k_dyn2 at every reset
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

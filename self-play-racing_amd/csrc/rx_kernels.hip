@@ -625,7 +625,7 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     }
   }
   if (do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
-    const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.call << 32) ^ (uint64_t)e));
+    const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.reset_count[e]++ << 32) ^ (uint64_t)e));
     const int first = (int)(h & 1ull);  // agent_order[0] after np.random.shuffle([0, 1])
 #pragma unroll
     for (int q = 0; q < 2; ++q) {

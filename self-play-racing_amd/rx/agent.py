@@ -31,11 +31,20 @@ class Agent(nn.Module):
         """Sample (or score) an action: Normal(mu, exp(log_std)); samples are
         clamped to [-1, 1] and the log-prob is of the CLAMPED action (SURVEY.md
         §8 Q7), summed over the 2 action dims; entropy likewise."""
-        mu = self.actor_mu(obs)
-        dist = torch.distributions.Normal(mu, torch.exp(self.log_std).expand_as(mu))
+        mu = self.actor_mu(obs).float()  # no-op in fp32; under bf16 autocast only the GEMMs are bf16
+        # validate_args=False: the default check is a host sync (illegal inside a
+        # captured rollout); scale = exp(log_std) > 0 always, so only NaN inputs
+        # would behave differently (no ValueError)
+        std = torch.exp(self.log_std).expand_as(mu)
+        dist = torch.distributions.Normal(mu, std, validate_args=False)
         if action is None:
-            action = torch.clamp(dist.sample(), -1.0, 1.0)
-        return action, dist.log_prob(action).sum(-1), dist.entropy().sum(-1), self.critic(obs)
+            with torch.no_grad():
+                # = dist.sample() = torch.normal(mu, std) bit for bit (ATen normal_out_impl
+                # draws N(0, 1) into the output, then mul_(std).add_(mean)) without its
+                # std.min() >= 0 host check, which cannot run inside a captured graph
+                eps = torch.empty_like(mu).normal_()
+                action = torch.clamp(eps.mul_(std).add_(mu), -1.0, 1.0)
+        return action, dist.log_prob(action).sum(-1), dist.entropy().sum(-1), self.critic(obs).float()
 
     @staticmethod
     def layer_optimization(layer, std=np.sqrt(2), bias=0.0):

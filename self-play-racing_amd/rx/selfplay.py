@@ -41,8 +41,6 @@ class SelfPlayVectorEnv:
         self.envs = venv.envs
         self.opponent_policy = None
         self._act = torch.zeros((self.num_envs, 2, 2), dtype=torch.float32, device=self.device)
-        self._gen = torch.Generator(device=self.device)
-        self._gen.manual_seed(int(seed) + 7919)
         self.buf = {"obs": self.venv.buf["obs"][:, agent_idx]}
 
     def set_opponent(self, policy):
@@ -51,7 +49,7 @@ class SelfPlayVectorEnv:
     def _opponent_actions(self):
         o = self._act[:, self.opp_idx]
         if self.opponent_policy is None:
-            u = torch.rand((self.num_envs, 2), generator=self._gen, device=self.device)
+            u = torch.rand((self.num_envs, 2), device=self.device)  # default generator: graph-capturable
             u[:, 0].mul_(2.0).sub_(1.0)  # steer ~ U(-1, 1); throttle ~ U(0, 1)
             o.copy_(u)
         else:
@@ -118,10 +116,30 @@ class SelfPlayPPO(PPO):
         return self.opponent_pool[np.random.choice(len(self.opponent_pool))]
 
     def update_opponent(self):
-        """agent/self_play_ppo.py:46-50: pick an opponent and rebuild (= reset) the envs."""
+        """agent/self_play_ppo.py:46-50: pick an opponent and rebuild (= reset) the envs.
+
+        The chosen pool member's weights are copied into one static opponent
+        module, so a graph-captured rollout keeps valid parameter addresses."""
         self.curr_opponent = self.select_opponent()
-        self.envs.set_opponent(self.curr_opponent)
+        if self.curr_opponent is None:
+            self.envs.set_opponent(None)
+        else:
+            if getattr(self, "_opp_static", None) is None:
+                self._opp_static = self.snapshot_agent()
+            with torch.no_grad():
+                for dst, src in zip(self._opp_static.state_dict().values(), self.curr_opponent.state_dict().values()):
+                    dst.copy_(src)
+            self.envs.set_opponent(self._opp_static)
         self.envs.reset_device()
+
+    def collect_rollout(self, *bufs):
+        # one captured graph per opponent kind (random vs frozen policy): the kind
+        # changes control flow inside the step, the weights do not (static module)
+        graphs = getattr(self, "_graphs_by_kind", {})
+        kind = self.envs.opponent_policy is not None
+        self._graphs = graphs.setdefault(kind, {})
+        self._graphs_by_kind = graphs
+        return super().collect_rollout(*bufs)
 
     def load_checkpoint(self, path):
         ck = torch.load(path, map_location=self.device, weights_only=True)

@@ -73,6 +73,50 @@ def test_collect_rollout_equals_reference_loop():
         assert torch.equal(x, y)
 
 
+def test_agent_sampling_is_torch_normal():
+    """Agent's capture-safe sampling == Normal(mu, std).sample() (agent/ppo.py:56) bit for bit."""
+    from rx.agent import Agent
+    from rx.spaces import Box
+    torch.manual_seed(3)
+    ag = Agent(Box(-1, 1, (11,)), Box(-1, 1, (2,))).cuda()
+    ag.log_std.fill_(-0.7)
+    obs = torch.randn(1000, 11, device="cuda")
+    torch.manual_seed(5)
+    a, lp, ent, v = ag.get_action_and_value(obs)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        mu = ag.actor_mu(obs)
+        d = torch.distributions.Normal(mu, torch.exp(ag.log_std).expand_as(mu))
+        ref = torch.clamp(d.sample(), -1.0, 1.0)
+    assert torch.equal(a, ref)
+    assert torch.equal(lp, d.log_prob(ref).sum(-1)) and torch.equal(ent, d.entropy().sum(-1))
+
+
+def test_graph_rollout_equals_eager_across_updates():
+    """The captured rollout replays with the CURRENT weights, log_std and RNG
+    state: two updates with graph_rollout on == the same two updates eager."""
+    outs = []
+    for graph in (True, False):
+        t, c = _train_single_style(num_envs=64, num_steps=16, graph_rollout=graph)
+        bufs = t._buffers()
+        nobs = t.envs.buf["obs"].clone()
+        nd = torch.zeros(64, device="cuda")
+        seq = []
+        for u in range(2):
+            t._anneal(u, 4)
+            out = t.collect_rollout(*bufs, nobs, nd)
+            obs, actions, logprobs, dones, rewards, values, nobs, nd, ep = out
+            seq.append([x.clone() for x in out[:8]])
+            with torch.no_grad():
+                nv = t.agent.get_value(nobs).flatten()
+            adv, ret = t.compute_advantages(rewards, dones, values, nv, nd)
+            t.ppo_update(adv, ret, values, logprobs, actions, obs)
+        outs.append(seq)
+    for ua, ub in zip(*outs):
+        for x, y in zip(ua, ub):
+            assert torch.equal(x, y)
+
+
 def test_gae_in_ppo_is_reference_formula():
     trainer, c = _train_single_style(num_envs=16, num_steps=8)
     g = torch.Generator(device="cuda").manual_seed(0)
