@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 3
+#define RX_ABI_VERSION 4
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -187,6 +187,68 @@ int rx_gae(int32_t T, int32_t N, const float* rewards, const float* values, cons
 int rx_gae_scan(int32_t T, int32_t N, const float* rewards, const float* values, const float* dones,
                 const float* next_value, const float* next_done, double gamma, double gae_lambda, float* advantages,
                 float* returns, void* stream);
+
+/* Fused optimizer step of PPO.ppo_update (agent/ppo.py:204-207):
+ * nn.utils.clip_grad_norm_(params, max_grad_norm) then torch.optim.Adam.step()
+ * (the default eps=1e-5 Adam of agent/ppo.py:83, no weight decay/amsgrad),
+ * over parameters stored back to back in ONE float32 buffer: tensor k owns
+ * elements [offsets[k], offsets[k+1]).  One workgroup: per-tensor gradient
+ * norms -> global norm -> clip coefficient -> Adam update, one launch.
+ *
+ *   step    device f32 scalar, the Adam step count (incremented here);
+ *   lr      device f64 scalar (read at run time, so a captured graph follows
+ *           the host-side lr anneal);
+ *   stop    device bool or NULL: when *stop != 0 the launch changes nothing
+ *           (the KL early stop of agent/ppo.py:178-182 without a host sync).
+ * max_grad_norm <= 0 disables clipping.  Grads are scaled in place, as
+ * clip_grad_norm_ does.  Equal to torch's clip + Adam within float rounding
+ * (tests/test_optim_gpu.py), not bit for bit (reduction order). */
+#define RX_ADAM_MAX_TENSORS 32
+typedef struct rx_adam_config {
+  int32_t n_tensors;
+  int64_t offsets[RX_ADAM_MAX_TENSORS + 1];
+  double beta1, beta2, eps, max_grad_norm;
+} rx_adam_config;
+int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                      float* step, const double* lr, const uint8_t* stop, void* stream);
+
+/* Fused PPO minibatch gradient (agent/ppo.py:170-203) for the reference's
+ * actor-critic (agent/ppo.py:11-62: Linear(D,64)-tanh-Linear(64,64)-tanh-
+ * Linear(64,2)-tanh actor, same trunk with a 1-wide linear head for the
+ * critic, fixed log_std buffer), parameters flat in module.parameters() order
+ * (rx_adam_clip_step layout).  For minibatch m of an epoch (rows
+ * perm[m*mb .. (m+1)*mb)) it computes the gradient of
+ *   pg_loss - ent_coef * entropy + vf_coef * v_loss
+ * (the entropy term has no parameter gradient: it depends on log_std only)
+ * into grad [P], and approx_kl = mean(old_logp - new_logp); if approx_kl >
+ * kl_target it sets *stop (and *kl_at_stop) so the rx_adam_clip_step that
+ * follows is skipped.  With *stop already set the call does nothing.
+ * fp32; equal to torch autograd within float rounding (tests/test_ppo_fused_gpu.py). */
+typedef struct rx_ppo_batch {
+  int32_t obs_dim;          /* D: 15 (single-agent) or 19 (two-car) */
+  int32_t mb;               /* minibatch rows */
+  int64_t n_rows;           /* B = rows of the flattened rollout; perm entries must be < B */
+  const float* obs;         /* [B][D] */
+  const float* actions;     /* [B][2] */
+  const float* logprobs;    /* [B] */
+  const float* advantages;  /* [B] */
+  const float* returns;     /* [B] */
+  const float* values;      /* [B] */
+  const int64_t* perm;      /* [n_mb*mb] this epoch's shuffled row indices (b_inds) */
+  const float* params;      /* [P] flat parameters */
+  const float* log_std;     /* [2] Agent.log_std buffer */
+  const float* adv_stats;   /* [n_mb][2] (mean, unbiased std) from rx_ppo_adv_stats */
+  float clip_coef, vf_coef, kl_target;
+} rx_ppo_batch;
+/* P for obs_dim (10,563 for 15, 11,075 for 19; 0 = unsupported). */
+int rx_ppo_n_params(int32_t obs_dim);
+/* float / double workspace sizes rx_ppo_minibatch_grad needs for minibatch size mb. */
+size_t rx_ppo_workspace_floats(int32_t obs_dim, int32_t mb);
+size_t rx_ppo_workspace_doubles(int32_t mb);
+/* (mean, unbiased std) of advantages[perm[m*mb ..]] for every minibatch m < n_mb. */
+int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* stream);
+int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, double* ws_f64, float* grad,
+                          uint8_t* stop, float* kl_at_stop, void* stream);
 
 #ifdef __cplusplus
 }

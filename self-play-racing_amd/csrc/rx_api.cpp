@@ -442,4 +442,61 @@ int rx_gae_scan(int32_t T, int32_t N, const float* r, const float* v, const floa
   return gae(T, N, r, v, d, nv, nd, gamma, lam, adv, ret, 1, stream);
 }
 
+int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                      float* step, const double* lr, const uint8_t* stop, void* stream) {
+  if (!cfg) return fail(RX_EINVAL, "rx_adam_clip_step: cfg is null");
+  if (cfg->n_tensors <= 0 || cfg->n_tensors > RX_ADAM_MAX_TENSORS)
+    return fail(RX_EINVAL, "rx_adam_clip_step: n_tensors=%d not in [1, %d]", cfg->n_tensors, RX_ADAM_MAX_TENSORS);
+  if (cfg->offsets[0] != 0) return fail(RX_EINVAL, "rx_adam_clip_step: offsets[0] must be 0");
+  for (int k = 0; k < cfg->n_tensors; ++k)
+    if (cfg->offsets[k + 1] < cfg->offsets[k]) return fail(RX_EINVAL, "rx_adam_clip_step: offsets not ascending");
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !lr)
+    return fail(RX_EINVAL, "rx_adam_clip_step: null buffer");
+  if (!(cfg->beta1 >= 0.0 && cfg->beta1 < 1.0 && cfg->beta2 >= 0.0 && cfg->beta2 < 1.0 && cfg->eps >= 0.0))
+    return fail(RX_EINVAL, "rx_adam_clip_step: bad betas/eps");
+  const int rc = rx_launch_adam(cfg, params, grads, exp_avg, exp_avg_sq, step, lr, stop, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "adam launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_n_params(int32_t obs_dim);  // rx_ppo.hip
+
+size_t rx_ppo_workspace_floats(int32_t obs_dim, int32_t mb) {
+  return (obs_dim == 15 || obs_dim == 19) && mb > 0 ? rx_ppo_partial_floats(obs_dim, mb) : 0;
+}
+
+size_t rx_ppo_workspace_doubles(int32_t mb) { return mb > 0 ? (size_t)(mb + 255) / 256 : 0; }
+
+static int check_ppo_batch(const rx_ppo_batch* b) {
+  if (!b) return fail(RX_EINVAL, "rx_ppo: batch is null");
+  if (b->obs_dim != 15 && b->obs_dim != 19) return fail(RX_EINVAL, "rx_ppo: obs_dim=%d (15 or 19)", b->obs_dim);
+  if (b->mb <= 0 || b->n_rows <= 0) return fail(RX_EINVAL, "rx_ppo: mb=%d n_rows=%lld", b->mb, (long long)b->n_rows);
+  if (!b->obs || !b->actions || !b->logprobs || !b->advantages || !b->returns || !b->values || !b->perm ||
+      !b->params || !b->log_std)
+    return fail(RX_EINVAL, "rx_ppo: null buffer");
+  return RX_OK;
+}
+
+int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if (n_mb <= 0 || !stats) return fail(RX_EINVAL, "rx_ppo_adv_stats: n_mb=%d stats=%p", n_mb, (void*)stats);
+  if ((int64_t)n_mb * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_adv_stats: n_mb*mb > n_rows");
+  if ((rc = rx_launch_adv_stats(b, n_mb, stats, (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "adv stats launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, double* ws_f64, float* grad,
+                          uint8_t* stop, float* kl_at_stop, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if (!b->adv_stats) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: adv_stats is null");
+  if (m < 0 || (int64_t)(m + 1) * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: m=%d out of range", m);
+  if (!ws_f32 || !ws_f64 || !grad || !stop || !kl_at_stop) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: null buffer");
+  if ((rc = rx_launch_ppo_grad(b, m, stop, kl_at_stop, ws_f32, ws_f64, grad, (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
 }  // extern "C"

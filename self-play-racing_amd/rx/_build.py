@@ -17,7 +17,7 @@ CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librx.so")
-SOURCES = ["rx_kernels.hip", "rx_sort.hip", "rx_api.cpp"]
+SOURCES = ["rx_kernels.hip", "rx_sort.hip", "rx_optim.hip", "rx_ppo.hip", "rx_api.cpp"]
 HEADERS = ["rx_internal.h", "rx_math.h", "rx_sincos_table.h"]
 
 ARCH = os.environ.get("RX_OFFLOAD_ARCH", "gfx950")

@@ -76,6 +76,14 @@ def average_gradients(params):
         o += n
 
 
+def average_flat(flat):
+    """Mean over ranks of the flat gradient buffer (rx.optim.FlatAdam): one all-reduce, no copies."""
+    if not active():
+        return
+    td.all_reduce(flat)
+    flat.div_(td.get_world_size())
+
+
 def broadcast_parameters(module, src=0):
     """Make every rank start from rank ``src``'s weights."""
     if not active():

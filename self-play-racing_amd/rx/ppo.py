@@ -27,6 +27,7 @@ import contextlib
 import json
 import os
 import random
+import types
 
 import numpy as np
 import torch
@@ -36,6 +37,7 @@ import torch.optim as optim
 from . import dist as rdist
 from .agent import Agent
 from .gae import compute_gae
+from .optim import FlatAdam
 
 
 class EpisodeSummary:
@@ -88,6 +90,8 @@ class PPO:
         torch.manual_seed(config["seed"])
         self.agent = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
         self.optimizer = optim.Adam(self.agent.parameters(), lr=config["learning_rate"], eps=1e-5)
+        # parameters move into one flat buffer here, BEFORE any graph captures their addresses
+        self._flat = FlatAdam(self.agent, self.optimizer, config["max_grad_norm"])
         self._fresh_obs = True
 
     def _make_envs(self, env_fn):
@@ -103,7 +107,8 @@ class PPO:
     # ------------------------------------------------------------ rollout
     def _policy_ctx(self):
         if self.config.get("policy_dtype", "fp32") == "bf16":
-            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+            # no weight-cast cache: the casts must be re-recorded inside captured graphs
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False)
         return contextlib.nullcontext()
 
     def _rollout_body(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
@@ -167,63 +172,193 @@ class PPO:
     def compute_advantages(self, rewards, dones, values, next_value, next_done):
         """agent/ppo.py:134-154 as one HIP kernel (bit-exact)."""
         c = self.config
-        return compute_gae(rewards, dones, values, next_value, next_done, c["gamma"], c["gae_lambda"])
+        # persistent outputs: the captured update graph keeps their addresses
+        out = self.__dict__.get("_gae_out")
+        if out is None or out[0].shape != rewards.shape or out[0].device != rewards.device:
+            out = self._gae_out = (torch.empty_like(rewards), torch.empty_like(rewards))
+        return compute_gae(rewards, dones, values, next_value, next_done, c["gamma"], c["gae_lambda"], out=out)
 
     # ------------------------------------------------------------ update
-    def ppo_update(self, advantages, returns, values, logprobs, actions, obs):
-        """agent/ppo.py:156-209; distributed-aware (rx.dist)."""
+    def _flat_batch(self, advantages, returns, values, logprobs, actions, obs):
+        return (obs.reshape((-1,) + obs.shape[2:]), actions.reshape((-1,) + actions.shape[2:]), logprobs.reshape(-1),
+                advantages.reshape(-1), returns.reshape(-1), values.reshape(-1))
+
+    def _minibatch_loss(self, b, mb_inds):
+        """agent/ppo.py:170-203 for one minibatch -> (loss, approx_kl)."""
         c = self.config
-        b_obs = obs.reshape((-1,) + obs.shape[2:])
-        b_actions = actions.reshape((-1,) + actions.shape[2:])
-        b_logprobs = logprobs.reshape(-1)
-        b_advantages = advantages.reshape(-1)
-        b_returns = returns.reshape(-1)
-        b_values = values.reshape(-1)
-        B = b_obs.shape[0]
+        b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values = b
         world = rdist.world()
-        mb = c["minibatch_size"] // world if world > 1 else c["minibatch_size"]
+        with self._policy_ctx():
+            _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+        ratio = (newlogprob - b_logprobs[mb_inds]).exp()
+        mb_adv = b_advantages[mb_inds]
+        with torch.no_grad():
+            if world > 1:  # one 4-float all-reduce: global KL and advantage moments
+                stats = rdist.minibatch_stats((b_logprobs[mb_inds] - newlogprob).sum(), mb_adv)
+                count = stats[3]
+                approx_kl = stats[0] / count
+            else:
+                approx_kl = (b_logprobs[mb_inds] - newlogprob).mean()
+        if world > 1:
+            mean = stats[1] / count
+            var = (stats[2] - count * mean * mean) / (count - 1)
+            mb_adv = (mb_adv - mean) / (var.clamp_min(0).sqrt() + 1e-8)
+        else:
+            mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+        pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - c["clip_coef"], 1 + c["clip_coef"])).mean()
+        newvalue = newvalue.flatten()
+        v_clip = b_values[mb_inds] + torch.clamp(newvalue - b_values[mb_inds], -c["clip_coef"], c["clip_coef"])
+        v_loss = 0.5 * torch.max((newvalue - b_returns[mb_inds]) ** 2, (v_clip - b_returns[mb_inds]) ** 2).mean()
+        loss = pg_loss + c["ent_coef"] * (-entropy.mean()) + c["vf_coef"] * v_loss
+        return loss, approx_kl
+
+    def _early_stop_msg(self, epoch, kl):
+        if rdist.rank() == 0:
+            print(f"  Early stopping at epoch {epoch + 1} due to KL divergence: {kl:.4f}")
+
+    def _minibatch_size(self):
+        world = rdist.world()
+        mb = self.config["minibatch_size"]
+        return mb // world if world > 1 else mb
+
+    def ppo_update(self, advantages, returns, values, logprobs, actions, obs):
+        """agent/ppo.py:156-209; distributed-aware (rx.dist).
+
+        Optimizer step = rx_adam_clip_step (clip_grad_norm_ + Adam in one HIP
+        launch on flat buffers, rx.optim).  On one GPU with
+        config["graph_update"] (default on) each epoch's 16 minibatch steps --
+        gather, forward, loss, backward, KL check, clip + Adam -- are ONE
+        captured HIP graph: the KL early stop becomes a device flag that turns
+        the remaining optimizer launches into no-ops, read by the host once per
+        epoch, so parameters, Adam state and np.random consumption end exactly
+        where the reference's immediate return leaves them."""
+        b = self._flat_batch(advantages, returns, values, logprobs, actions, obs)
+        flat = getattr(self, "_flat", None)
+        if flat is None:
+            return self._update_torch(b)
+        flat.rebind()
+        flat.sync_lr()
+        if rdist.world() == 1 and self.config.get("graph_update", True):
+            return self._update_graphed(b)
+        return self._update_flat_eager(b)
+
+    def _update_torch(self, b):
+        """Reference control flow with torch.optim (no flat buffers: CPU tests)."""
+        c = self.config
+        B, mb = b[0].shape[0], self._minibatch_size()
         b_inds = np.arange(B)
         params = [p for p in self.agent.parameters()]
         for epoch in range(c["update_epochs"]):
             np.random.shuffle(b_inds)
             perm = torch.from_numpy(b_inds).to(self.device)
             for start in range(0, B, mb):
-                mb_inds = perm[start:start + mb]
-                with self._policy_ctx():
-                    _, newlogprob, entropy, newvalue = self.agent.get_action_and_value(b_obs[mb_inds],
-                                                                                       b_actions[mb_inds])
-                ratio = (newlogprob - b_logprobs[mb_inds]).exp()
-                mb_adv = b_advantages[mb_inds]
-                with torch.no_grad():
-                    if world > 1:  # one 4-float all-reduce: global KL and advantage moments
-                        stats = rdist.minibatch_stats((b_logprobs[mb_inds] - newlogprob).sum(), mb_adv)
-                        count = stats[3]
-                        approx_kl = stats[0] / count
-                    else:
-                        approx_kl = (b_logprobs[mb_inds] - newlogprob).mean()
-                    if approx_kl > c["kl_target"]:
-                        if rdist.rank() == 0:
-                            print(f"  Early stopping at epoch {epoch + 1} due to KL divergence: {approx_kl:.4f}")
-                        return
-                if world > 1:
-                    mean = stats[1] / count
-                    var = (stats[2] - count * mean * mean) / (count - 1)
-                    mb_adv = (mb_adv - mean) / (var.clamp_min(0).sqrt() + 1e-8)
-                else:
-                    mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
-                pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - c["clip_coef"],
-                                                                           1 + c["clip_coef"])).mean()
-                newvalue = newvalue.flatten()
-                v_clip = b_values[mb_inds] + torch.clamp(newvalue - b_values[mb_inds], -c["clip_coef"],
-                                                         c["clip_coef"])
-                v_loss = 0.5 * torch.max((newvalue - b_returns[mb_inds]) ** 2,
-                                         (v_clip - b_returns[mb_inds]) ** 2).mean()
-                loss = pg_loss + c["ent_coef"] * (-entropy.mean()) + c["vf_coef"] * v_loss
+                loss, approx_kl = self._minibatch_loss(b, perm[start:start + mb])
+                if approx_kl > c["kl_target"]:
+                    self._early_stop_msg(epoch, float(approx_kl))
+                    return
                 self.optimizer.zero_grad()
                 loss.backward()
                 rdist.average_gradients(params)
                 nn.utils.clip_grad_norm_(params, c["max_grad_norm"])
                 self.optimizer.step()
+
+    def _update_flat_eager(self, b):
+        """Eager minibatch loop on the flat optimizer (data parallel: ONE flat
+        gradient all-reduce per step; the KL check syncs per minibatch)."""
+        c = self.config
+        B, mb = b[0].shape[0], self._minibatch_size()
+        b_inds = np.arange(B)
+        for epoch in range(c["update_epochs"]):
+            np.random.shuffle(b_inds)
+            perm = torch.from_numpy(b_inds).to(self.device)
+            for start in range(0, B, mb):
+                loss, approx_kl = self._minibatch_loss(b, perm[start:start + mb])
+                if approx_kl > c["kl_target"]:
+                    self._early_stop_msg(epoch, float(approx_kl))
+                    return
+                self._flat.zero_grad()
+                loss.backward()
+                rdist.average_flat(self._flat.flat_grad)
+                self._flat.step()
+
+    def _graph_minibatch(self, b, mb_inds):
+        loss, approx_kl = self._minibatch_loss(b, mb_inds)
+        hit = (approx_kl > self.config["kl_target"]).reshape(1)
+        self._kl_at_stop.copy_(torch.where(hit & ~self._stop, approx_kl.reshape(1).float(), self._kl_at_stop))
+        self._stop.logical_or_(hit)
+        self._flat.zero_grad()
+        loss.backward()
+        self._flat.step(stop=self._stop)
+
+    def _epoch_graph(self, b, B, mb):
+        """One captured graph per (buffers, batch, minibatch, dtype, kernel): all
+        minibatch steps of an epoch over the static index tensor ``perm``.
+
+        With config["fused_update"] (default on) and the reference policy
+        layout, a minibatch step is rx_ppo_minibatch_grad + rx_adam_clip_step
+        (rx.ppo_fused: 3 launches); otherwise it is torch autograd + the flat
+        Adam launch."""
+        from . import ppo_fused
+        fused = self.config.get("fused_update", True) and ppo_fused.supported(self.agent, b, mb)
+        key = tuple(t.data_ptr() for t in b) + (B, mb, self.config.get("policy_dtype", "fp32"), fused)
+        graphs = self.__dict__.setdefault("_upd_graphs", {})
+        if key in graphs:
+            return graphs[key]
+        dev = self.device
+        ent = types.SimpleNamespace(
+            perm=torch.arange(B, device=dev), perm_host=torch.empty(B, dtype=torch.int64).pin_memory(),
+            stop=torch.ones(1, dtype=torch.bool, device=dev),  # a warm-up must not move anything
+            kl=torch.zeros(1, dtype=torch.float32, device=dev), graph=torch.cuda.CUDAGraph(), fused=None)
+        if fused:
+            ent.fused = ppo_fused.FusedMinibatchGrad(self.agent, self._flat, b, mb, ent.perm, self.config)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.graph(ent.graph):
+                ent.fused.epoch(ent.stop, ent.kl)
+        else:
+            self._stop, self._kl_at_stop = ent.stop, ent.kl
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self._graph_minibatch(b, ent.perm[:mb])
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.graph(ent.graph):
+                for start in range(0, B, mb):
+                    self._graph_minibatch(b, ent.perm[start:start + mb])
+        graphs[key] = ent
+        return ent
+
+    def _update_graphed(self, b):
+        c = self.config
+        B, mb = b[0].shape[0], self._minibatch_size()
+        ent = self._epoch_graph(b, B, mb)
+        device_shuffle = c.get("shuffle", "numpy") == "device"
+        b_inds = np.arange(B)
+        nxt = None
+        ent.stop.zero_()
+        for epoch in range(c["update_epochs"]):
+            if device_shuffle:  # torch.randperm on the device: no host shuffle / H2D copy
+                torch.randperm(B, device=self.device, out=ent.perm)
+            else:
+                if nxt is None:
+                    np.random.shuffle(b_inds)
+                else:
+                    b_inds = nxt
+                ent.perm_host.numpy()[:] = b_inds
+                ent.perm.copy_(ent.perm_host, non_blocking=True)
+            ent.graph.replay()
+            rng = None
+            if not device_shuffle and epoch + 1 < c["update_epochs"]:
+                # shuffle the next epoch while this one runs; undone if it stopped
+                rng = np.random.get_state()
+                nxt = b_inds.copy()
+                np.random.shuffle(nxt)
+            if bool(ent.stop.item()):
+                if rng is not None:
+                    np.random.set_state(rng)
+                self._early_stop_msg(epoch, float(ent.kl.item()))
+                return
 
     # ------------------------------------------------------------ driver
     def _anneal(self, update, num_updates):

@@ -1,0 +1,64 @@
+"""Driver of the fused PPO minibatch gradient (include/rx.h rx_ppo_*).
+
+``FusedMinibatchGrad`` binds one flattened rollout (obs, actions, logprobs,
+advantages, returns, values -- persistent buffers), the flat policy
+parameters of rx.optim.FlatAdam and the epoch's index tensor, and issues per
+epoch: one rx_ppo_adv_stats launch (every minibatch's advantage mean/std),
+then per minibatch rx_ppo_minibatch_grad (forward + loss + backward + split-K
+reduce + KL check) followed by rx_adam_clip_step.  Everything is enqueued on
+the current stream with no host sync, so PPO captures an epoch as one graph.
+"""
+import torch
+
+from . import _lib
+
+
+def supported(agent, b, mb):
+    """True when the fused kernel covers this policy / batch: the reference
+    Agent layout (64-wide tanh trunks, 2 actions, D in {15, 19}), float32,
+    and a batch that splits into whole minibatches."""
+    obs = b[0]
+    if obs.dim() != 2 or obs.shape[1] not in (15, 19) or b[1].shape[-1] != 2:
+        return False
+    B = obs.shape[0]
+    if mb <= 0 or B % mb or any(t.dtype != torch.float32 or not t.is_contiguous() for t in b):
+        return False
+    L = _lib.load()
+    n = sum(p.numel() for p in agent.parameters())
+    return n == L.rx_ppo_n_params(obs.shape[1])
+
+
+class FusedMinibatchGrad:
+    def __init__(self, agent, flat, b, mb, perm, config):
+        L = _lib.load()
+        self.L = L
+        obs, actions, logprobs, advantages, returns, values = b
+        B, D = obs.shape
+        self.n_mb = B // mb
+        self.mb = mb
+        dev = obs.device
+        self.stats = torch.zeros(2 * self.n_mb, dtype=torch.float32, device=dev)
+        self.ws_f = torch.empty(L.rx_ppo_workspace_floats(D, mb), dtype=torch.float32, device=dev)
+        self.ws_d = torch.empty(L.rx_ppo_workspace_doubles(mb), dtype=torch.float64, device=dev)
+        self.flat = flat
+        self._keep = (b, perm, agent.log_std)  # the struct holds raw pointers into these
+        self.batch = _lib.RxPPOBatch(D, mb, B, _lib.ptr(obs), _lib.ptr(actions), _lib.ptr(logprobs),
+                                     _lib.ptr(advantages), _lib.ptr(returns), _lib.ptr(values), _lib.ptr(perm),
+                                     _lib.ptr(flat.flat_param), _lib.ptr(agent.log_std), _lib.ptr(self.stats),
+                                     float(config["clip_coef"]), float(config["vf_coef"]), float(config["kl_target"]))
+
+    def adv_stats(self, stream=None):
+        _lib.check(self.L.rx_ppo_adv_stats(self.batch, self.n_mb, _lib.ptr(self.stats), _lib.stream_ptr(stream)),
+                   "rx_ppo_adv_stats")
+
+    def grad(self, m, stop, kl_at_stop, stream=None):
+        _lib.check(self.L.rx_ppo_minibatch_grad(self.batch, int(m), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
+                                                _lib.ptr(self.flat.flat_grad), _lib.ptr(stop), _lib.ptr(kl_at_stop),
+                                                _lib.stream_ptr(stream)), "rx_ppo_minibatch_grad")
+
+    def epoch(self, stop, kl_at_stop):
+        """All minibatch steps of one epoch over the current perm."""
+        self.adv_stats()
+        for m in range(self.n_mb):
+            self.grad(m, stop, kl_at_stop)
+            self.flat.step(stop=stop)

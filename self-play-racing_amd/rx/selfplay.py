@@ -145,6 +145,7 @@ class SelfPlayPPO(PPO):
         ck = torch.load(path, map_location=self.device, weights_only=True)
         self.agent.load_state_dict(ck["agent_state_dict"])
         self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+        self._flat.import_state()
         self.opponent_pool = []
         for sd in ck["opponent_pool"]:
             o = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
@@ -198,6 +199,7 @@ class SelfPlayPPO(PPO):
         import os
         path = path or self.checkpoint_fmt.format(update)
         d = os.path.dirname(path)
+        self._flat.export_state()
         try:
             if d:
                 os.makedirs(d, exist_ok=True)

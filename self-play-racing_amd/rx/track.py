@@ -12,7 +12,11 @@ new is what happens around them:
   leaves the global RNG exactly where the reference would.
 * ``TrackSet`` deduplicates (control points, width) pairs into slots -- seed 1
   gives 7 slots for any number of envs -- and packs them into the flat
-  struct-of-arrays table the kernels read (include/rx.h rx_upload_tracks).
+  struct-of-arrays table the kernels read (include/rx.h rx_upload_tracks);
+  ``TrackSet.save`` / ``TrackSet.load`` keep that table (plus the control
+  points and, optionally, the env -> slot assignment) in one ``.npz`` file, so
+  a 65,536-env pool is rebuilt without regenerating or re-splining anything
+  (format in DESIGN.md).
 """
 import numpy as np
 from scipy.interpolate import CubicSpline
@@ -135,6 +139,26 @@ class TrackGeometry:
         ends = np.vstack([np.roll(self.left_boundary, -1, axis=0), np.roll(self.right_boundary, -1, axis=0)])
         self.segment_cache = {"starts": starts, "ends": ends, "v2": ends - starts}
 
+    @classmethod
+    def from_arrays(cls, control_points, track_width, waypoints, normals, seg, max_track_distance):
+        """Rebuild from a stored table slot (no spline): every attribute is an
+        exact function of the stored arrays."""
+        self = cls.__new__(cls)
+        self.control_points = control_points
+        self.track_width = track_width
+        self.waypoints = waypoints
+        wp = waypoints
+        self.track_bounds = {"min_x": wp[:, 0].min(), "max_x": wp[:, 0].max(), "min_y": wp[:, 1].min(),
+                             "max_y": wp[:, 1].max()}
+        self.max_track_distance = np.float64(max_track_distance)
+        self.normals = normals
+        W = len(wp)
+        starts, v2 = seg[:, :2].copy(), seg[:, 2:].copy()
+        self.left_boundary, self.right_boundary = starts[:W], starts[W:]
+        ends = np.vstack([np.roll(self.left_boundary, -1, axis=0), np.roll(self.right_boundary, -1, axis=0)])
+        self.segment_cache = {"starts": starts, "ends": ends, "v2": v2}
+        return self
+
     def get_start_pos(self):
         """track.py:154-157"""
         wp = self.waypoints
@@ -190,3 +214,61 @@ class TrackSet:
                            t.normals[0, 0], t.normals[0, 1], 0.0)
             self._packed = dict(wp_off=wp_off, wp=wp, nrm=nrm, seg=seg, meta=meta)
         return self._packed
+
+    # ------------------------------------------------------------ on-disk table
+    TABLE_VERSION = 1
+
+    def save(self, path, track_of_env=None):
+        """Write the table as an uncompressed .npz (loads with allow_pickle=False).
+
+        Keys: version, factor, n_slots; per slot: widths [n], cp_off [n+1] int64,
+        cp_is_int [n] bool, control_points [sum P, 2] f64; the device table
+        wp_off / wp / nrm / seg / meta exactly as rx_upload_tracks takes it;
+        optional track_of_env [N] int32 (the env -> slot assignment)."""
+        a = self.arrays()
+        cps = [np.asarray(g.control_points) for g in self.geoms]
+        cp_off = np.concatenate([[0], np.cumsum([len(c) for c in cps])]).astype(np.int64)
+        extra = {}
+        if track_of_env is not None:
+            toe = np.asarray(track_of_env, dtype=np.int32)
+            if toe.size and (toe.min() < 0 or toe.max() >= len(self)):
+                raise ValueError("track_of_env refers to a slot outside the table")
+            extra["track_of_env"] = toe
+        np.savez(path, version=np.int64(self.TABLE_VERSION), factor=np.int64(self.factor),
+                 n_slots=np.int64(len(self)), widths=np.array([float(g.track_width) for g in self.geoms]),
+                 cp_off=cp_off, cp_is_int=np.array([np.issubdtype(c.dtype, np.integer) for c in cps]),
+                 control_points=np.concatenate(cps).astype(np.float64) if cps else np.zeros((0, 2)),
+                 **a, **extra)
+
+    @classmethod
+    def load(cls, path, verify=False):
+        """-> (TrackSet, track_of_env or None).  ``verify`` re-splines every slot
+        from its control points and requires the stored geometry bit for bit."""
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["version"]) != cls.TABLE_VERSION:
+                raise ValueError(f"track table version {int(z['version'])} != {cls.TABLE_VERSION}")
+            d = {k: z[k] for k in z.files}
+        ts = cls(factor=int(d["factor"]))
+        n = int(d["n_slots"])
+        wp_off, cp_off = d["wp_off"], d["cp_off"]
+        if wp_off.shape != (n + 1,) or cp_off.shape != (n + 1,) or d["meta"].shape != (n, 8):
+            raise ValueError("inconsistent track table")
+        for k in range(n):
+            cp = d["control_points"][cp_off[k]:cp_off[k + 1]]
+            if d["cp_is_int"][k]:
+                cp = cp.astype(np.int64)
+            w = float(d["widths"][k])
+            a, b = wp_off[k], wp_off[k + 1]
+            g = TrackGeometry.from_arrays(cp, w, d["wp"][a:b], d["nrm"][a:b], d["seg"][2 * a:2 * b],
+                                          d["meta"][k, 4])
+            if verify:
+                ref = TrackGeometry(cp, w, ts.factor)
+                for x, y in ((ref.waypoints, g.waypoints), (ref.normals, g.normals),
+                             (ref.segment_cache["starts"], g.segment_cache["starts"]),
+                             (ref.segment_cache["v2"], g.segment_cache["v2"])):
+                    if x.shape != y.shape or x.tobytes() != y.tobytes():
+                        raise ValueError(f"track table slot {k} does not match its control points")
+            ts._index[cls._key(cp, w)] = len(ts.geoms)
+            ts.geoms.append(g)
+        ts._packed = {k: np.ascontiguousarray(d[k]) for k in ("wp_off", "wp", "nrm", "seg", "meta")}
+        return ts, (d["track_of_env"] if "track_of_env" in d else None)

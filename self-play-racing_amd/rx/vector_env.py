@@ -313,6 +313,21 @@ class RacingVectorEnv:
 
     # ------------------------------------------------------------ construction helpers
     @classmethod
+    def from_table(cls, path, track_of_env=None, **kw):
+        """Build from an on-disk track table (rx.track.TrackSet.save): env i
+        runs slot track_of_env[i] (default: the assignment stored in the file)."""
+        ts, stored = TrackSet.load(path)
+        toe = stored if track_of_env is None else np.asarray(track_of_env, dtype=np.int32)
+        if toe is None:
+            raise ValueError(f"{path} holds no env assignment: pass track_of_env")
+        g = ts.geoms
+        return cls([g[k].control_points for k in toe], [g[k].track_width for k in toe], track_set=ts, **kw)
+
+    def save_table(self, path):
+        """Write this env's track table and env -> slot assignment (TrackSet.save)."""
+        self.tracks.save(path, self.track_of_env)
+
+    @classmethod
     def from_envs(cls, envs, **kw):
         """Build from reference-style env objects (rx.envs.RacingEnv / MultiRacingEnv
         specs returned by a train.py ``env_fn``)."""

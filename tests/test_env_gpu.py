@@ -304,3 +304,30 @@ def test_culled_raycast_on_golden_kats(rx, golden):
         # compare against the oracle (device libm) exactly, against the reference to 1e-5
         np.testing.assert_allclose(obs[:, 5], want, rtol=0, atol=1e-5)
         assert (obs[:, 5] == want).mean() > 0.99
+
+
+def test_vector_env_from_table_file(tmp_path):
+    """RacingVectorEnv.from_table (on-disk track table) == the env built from the pool."""
+    import random
+    from rx.track import gen_tracks
+    from rx.vector_env import RacingVectorEnv
+    random.seed(1)
+    np.random.seed(1)
+    pool = gen_tracks(64, seed=1)
+    widths = [np.random.randint(6, 10) for _ in range(64)]
+    a = RacingVectorEnv(pool, widths, device="cuda")
+    p = tmp_path / "tbl.npz"
+    a.save_table(p)
+    b = RacingVectorEnv.from_table(p, device="cuda")
+    assert np.array_equal(a.track_of_env, b.track_of_env)
+    a.reset_device()
+    b.reset_device()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for _ in range(200):
+        act = torch.rand((64, 2), generator=g, device="cuda") * torch.tensor([2.0, 1.0], device="cuda") \
+            - torch.tensor([1.0, 0.0], device="cuda")
+        oa, ra, da = a.step_device(act)
+        ob, rb, db = b.step_device(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+    a.close()
+    b.close()

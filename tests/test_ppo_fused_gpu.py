@@ -1,0 +1,124 @@
+"""Fused PPO minibatch gradient (rx_ppo_minibatch_grad) vs torch autograd of
+the reference loss (agent/ppo.py:170-203), and the fused update's control flow."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bare_ppo(agent, **over):
+    from rx.configs import base_config
+    from rx.ppo import PPO
+    p = PPO.__new__(PPO)
+    p.config = base_config(**over)
+    p.device = torch.device("cuda")
+    p.agent = agent
+    return p
+
+
+def _batch(B, D, seed=0, adv_scale=5.0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    obs = torch.rand(B, D, generator=g, device="cuda") * 2 - 1
+    act = torch.rand(B, 2, generator=g, device="cuda") * 2 - 1
+    logp = torch.randn(B, generator=g, device="cuda") * 0.3 - 1.0
+    adv = torch.randn(B, generator=g, device="cuda") * adv_scale + 0.3
+    ret = torch.randn(B, generator=g, device="cuda") * 10
+    val = ret + torch.randn(B, generator=g, device="cuda") * 0.3  # some value-clip ties / both branches
+    return obs, act, logp, adv, ret, val
+
+
+@pytest.mark.parametrize("D", [15, 19])
+def test_fused_grad_matches_autograd(D):
+    from rx.agent import Agent
+    from rx.optim import FlatAdam
+    from rx.ppo_fused import FusedMinibatchGrad, supported
+    from rx.spaces import Box
+    torch.manual_seed(7)
+    ag = Agent(Box(-1, 1, (D,)), Box(-1, 1, (2,))).cuda()
+    ag.log_std.fill_(-0.8)
+    with torch.no_grad():  # non-trivial outputs (the head init is 0.01 / 1.0)
+        ag.actor_mu[4].weight.mul_(60.0)
+    ref = copy.deepcopy(ag)
+    fl = FlatAdam(ag, torch.optim.Adam(ag.parameters(), lr=1e-3, eps=1e-5), 0.5)
+    B, mb = 2048, 512
+    b = _batch(B, D)
+    b_ppo = (b[0], b[1], b[2], b[3], b[4], b[5])
+    perm = torch.randperm(B, device="cuda")
+    assert supported(ag, b_ppo, mb)
+    cfg = _bare_ppo(ref).config
+    fg = FusedMinibatchGrad(ag, fl, b_ppo, mb, perm, cfg)
+    fg.adv_stats()
+    stop = torch.zeros(1, dtype=torch.bool, device="cuda")
+    kl = torch.zeros(1, device="cuda")
+    p = _bare_ppo(ref)
+    # the PPO loss on (obs, act, logp, adv, ret, val) in _minibatch_loss order
+    bt = (b[0], b[1], b[2], b[3], b[4], b[5])
+    for m in range(B // mb):
+        stop.zero_()
+        fg.grad(m, stop, kl)
+        ref.zero_grad()
+        loss, akl = p._minibatch_loss(bt, perm[m * mb:(m + 1) * mb])
+        loss.backward()
+        want = torch.cat([q.grad.reshape(-1) for q in ref.parameters()])
+        got = fl.flat_grad
+        scale = want.abs().max()
+        torch.testing.assert_close(got, want, rtol=2e-4, atol=2e-5 * float(scale))
+        assert bool(stop) == (float(akl) > cfg["kl_target"])  # random old log-probs: KL is large
+        # kl: the fused kernel accumulates in double; compare to torch's mean
+        s = float(fg.ws_d[:mb // 256].sum()) / mb
+        assert abs(s - float(akl)) <= 1e-5 + 1e-4 * abs(float(akl))
+
+
+def _trainer(**over):
+    from tests.test_ppo_gpu import _train_single_style
+    return _train_single_style(num_envs=32, num_steps=32, **over)[0]
+
+
+def _rollout(t):
+    from tests.test_optim_gpu import _rollout as r
+    return r(t)
+
+
+def test_fused_update_step_close_to_torch():
+    """One fused optimizer step == one torch autograd + flat Adam step within float rounding."""
+    over = dict(kl_target=1e9, update_epochs=1, num_minibatches=1)
+    ta = _trainer(**over)                      # graph + fused
+    tb = _trainer(graph_update=False, **over)  # eager autograd, flat Adam
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    data = _rollout(ta)
+    np.random.seed(5)
+    ta.ppo_update(*data)
+    np.random.seed(5)
+    tb.ppo_update(*data)
+    assert next(iter(ta._upd_graphs.values())).fused is not None
+    torch.testing.assert_close(ta._flat.flat_grad, tb._flat.flat_grad, rtol=2e-4,
+                               atol=2e-5 * float(tb._flat.flat_grad.abs().max()))
+    for x, y in zip(ta.agent.parameters(), tb.agent.parameters()):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=2e-6)
+
+
+def test_fused_update_early_stop_and_full_run(capsys):
+    t = _trainer(kl_target=-1.0)  # every KL exceeds it: stop at the first minibatch
+    data = _rollout(t)
+    before = t._flat.flat_param.clone()
+    np.random.seed(9)
+    st = np.random.get_state()
+    t._anneal(0, 4)
+    t.ppo_update(*data)
+    after = np.random.get_state()
+    assert torch.equal(before, t._flat.flat_param) and float(t._flat.step_t) == 0.0
+    assert "Early stopping at epoch 1" in capsys.readouterr().out
+    np.random.set_state(st)
+    np.random.shuffle(np.arange(32 * 32))  # exactly one shuffle consumed, as the reference's return
+    now = np.random.get_state()
+    assert np.array_equal(now[1], after[1]) and now[2] == after[2]
+    t2 = _trainer(kl_target=1e9)
+    data2 = _rollout(t2)
+    t2._anneal(0, 4)
+    t2.ppo_update(*data2)
+    c = t2.config
+    assert float(t2._flat.step_t) == c["update_epochs"] * (c["batch_size"] // c["minibatch_size"])
+    assert not torch.equal(t2._flat.flat_param, before)

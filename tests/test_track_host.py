@@ -75,3 +75,50 @@ def test_eval_pool_matches_reference_protocol(golden):
         k = labels.index(f"eval42[{t}] w={int(golden.geo['eval42_widths'][t])}")
         assert np.array_equal(cps[5 * t], golden.tracks[k]["cp"])
     assert ws[:5] == list(golden.geo["eval42_widths"][:5])  # widths indexed by RUN (evaluate.py:30)
+
+
+def test_track_table_file_roundtrip(golden, tmp_path):
+    """On-disk table (TrackSet.save/load): the loaded table
+    is the saved one byte for byte, its slots are the golden geometry, and the
+    stored env assignment comes back."""
+    ts = TrackSet()
+    want = {}
+    for t in golden.tracks:
+        cp = DEFAULT_CONTROL_POINTS if t["label"] == "default" else t["cp"]
+        w = None if t["label"] == "default" else t["width"]
+        want[ts.slot(cp, w)] = t
+    pool, widths = _pool(256)
+    toe = np.array([ts.slot(c, w) for c, w in zip(pool, widths)], dtype=np.int32)
+    p = tmp_path / "tracks.npz"
+    ts.save(p, toe)
+    ld, toe2 = TrackSet.load(p, verify=True)
+    assert np.array_equal(toe, toe2) and len(ld) == len(ts)
+    for k in ts.arrays():
+        assert ts.arrays()[k].tobytes() == ld.arrays()[k].tobytes(), k
+    for k, t in want.items():
+        g = ld.geoms[k]
+        assert np.array_equal(g.waypoints, t["wp"]) and np.array_equal(g.normals, t["nrm"])
+        assert np.array_equal(g.segment_cache["starts"], t["starts"]) and np.array_equal(g.segment_cache["v2"], t["v2"])
+        assert g.max_track_distance == t["maxd"]
+        assert np.array_equal(np.array([float(v) for v in g.get_start_pos()]), t["start"])
+        ref = ts.geoms[k]
+        assert np.array_equal(g.segment_cache["ends"], ref.segment_cache["ends"])
+        assert g.track_bounds == ref.track_bounds
+    # slot lookup by (control points, width) still dedups against loaded slots
+    assert ld.slot(pool[0], widths[0]) == toe[0] and len(ld) == len(ts)
+    assert ld.slot(DEFAULT_CONTROL_POINTS, None) == ts.slot(DEFAULT_CONTROL_POINTS, None)
+
+
+def test_track_table_rejects_tampering(tmp_path):
+    import pytest
+    ts = TrackSet()
+    ts.slot(DEFAULT_CONTROL_POINTS, 7)
+    p = tmp_path / "t.npz"
+    ts.save(p)
+    d = dict(np.load(p))
+    d["wp"] = d["wp"].copy()
+    d["wp"][3, 0] += 1e-9
+    np.savez(tmp_path / "bad.npz", **d)
+    with pytest.raises(ValueError):
+        TrackSet.load(tmp_path / "bad.npz", verify=True)
+    assert TrackSet.load(p)[1] is None
