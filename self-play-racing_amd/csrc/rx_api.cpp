@@ -465,7 +465,7 @@ size_t rx_ppo_workspace_floats(int32_t obs_dim, int32_t mb) {
   return (obs_dim == 15 || obs_dim == 19) && mb > 0 ? rx_ppo_partial_floats(obs_dim, mb) : 0;
 }
 
-size_t rx_ppo_workspace_doubles(int32_t mb) { return mb > 0 ? (size_t)(mb + 255) / 256 : 0; }
+size_t rx_ppo_workspace_doubles(int32_t mb) { return mb > 0 ? (size_t)rx_ppo_n_wg(mb) : 0; }
 
 static int check_ppo_batch(const rx_ppo_batch* b) {
   if (!b) return fail(RX_EINVAL, "rx_ppo: batch is null");

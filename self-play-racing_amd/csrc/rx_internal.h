@@ -67,6 +67,7 @@ extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                               const double* lr, const uint8_t* stop, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
+extern "C" int rx_ppo_n_wg(int mb);
 extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, hipStream_t s);
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, float* kl_at_stop, float* partial,
                                   double* klp, float* grad, hipStream_t s);

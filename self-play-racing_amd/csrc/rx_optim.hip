@@ -26,37 +26,37 @@ struct adam_args {
   const uint8_t* stop;
 };
 
-__device__ double block_sum(double x, double* red) {
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();  // red[] may still be read by the previous call
-  if ((threadIdx.x & 63) == 0) red[w] = x;
-  __syncthreads();
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < kWaves; ++i) s += red[i];  // same order in every thread
-  return s;
-}
-
 __global__ __launch_bounds__(kThreads) void k_adam_clip(adam_args a) {
   if (a.stop && *a.stop) return;  // uniform: KL early stop already hit
-  __shared__ double red[kWaves];
+  __shared__ float sq[RX_ADAM_MAX_TENSORS][kThreads];  // per-thread partial sums of squares, per tensor
+  __shared__ float norms[RX_ADAM_MAX_TENSORS];
   const int n_t = a.cfg.n_tensors;
   const int64_t n = a.cfg.offsets[n_t];
   float coef = 1.0f;
   if (a.cfg.max_grad_norm > 0.0) {
     // torch.nn.utils.clip_grad_norm_: total = ||(||g_0||, ..., ||g_k||)||_2,
-    // coef = clamp(max_norm / (total + 1e-6), max=1), grads *= coef
-    float tot2 = 0.0f;
-    for (int t = 0; t < n_t; ++t) {
-      double s = 0.0;
-      for (int64_t i = a.cfg.offsets[t] + threadIdx.x; i < a.cfg.offsets[t + 1]; i += kThreads) {
-        const double x = a.g[i];
-        s += x * x;
-      }
-      const float nt = (float)sqrt(block_sum(s, red));
-      tot2 += nt * nt;
+    // coef = clamp(max_norm / (total + 1e-6), max=1), grads *= coef.
+    // Pass 1: coalesced, independent loads; each thread adds g^2 into its own
+    // slot of its element's tensor.  Pass 2: wave t reduces tensor t's slots.
+    for (int t = 0; t < n_t; ++t) sq[t][threadIdx.x] = 0.0f;
+    int t = 0;
+#pragma unroll 4
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+      while (i >= a.cfg.offsets[t + 1]) ++t;
+      const float x = a.g[i];
+      sq[t][threadIdx.x] = fmaf(x, x, sq[t][threadIdx.x]);
     }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int u = wave; u < n_t; u += kWaves) {
+      float s = 0.0f;
+      for (int k = lane; k < kThreads; k += 64) s += sq[u][k];
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0) norms[u] = sqrtf(s);
+    }
+    __syncthreads();
+    float tot2 = 0.0f;
+    for (int u = 0; u < n_t; ++u) tot2 += norms[u] * norms[u];
     const float total = sqrtf(tot2);
     coef = fminf((float)a.cfg.max_grad_norm / (total + 1e-6f), 1.0f);
   }
@@ -70,6 +70,7 @@ __global__ __launch_bounds__(kThreads) void k_adam_clip(adam_args a) {
   const float step_size = (float)(-(*a.lr / (1.0 - pow(b1, s))));
   const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, s));
   const float eps = (float)a.cfg.eps;
+#pragma unroll 4
   for (int64_t i = threadIdx.x; i < n; i += kThreads) {
     const float g = a.g[i] * coef;
     a.g[i] = g;

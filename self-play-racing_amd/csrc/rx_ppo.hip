@@ -5,293 +5,305 @@
 // whose weight-gradient GEMMs (M=N<=64, K=minibatch) hipBLASLt runs on a
 // handful of workgroups (profiles/r01/ppo_update_kernel_stats.csv).
 //
-// Layout: one thread = one minibatch row.  Weights are wave-uniform and are
-// read through scalar loads (SGPR operands of the FMAs); per-row activations
-// live in VGPRs.  Weight gradients dW = sum_r dZ[r] (x) H[r] are formed per
-// workgroup (kRows rows) by staging dZ and H in LDS and accumulating register
-// tiles, written as one partial per workgroup; k_ppo_reduce sums partials in
-// a fixed order (run-to-run deterministic, no float atomics).
+// Layout: lane = minibatch row, the 4 waves of a workgroup split the hidden
+// columns; weights are wave-uniform and read through scalar loads (SGPR
+// operands of the FMAs); activations are staged in LDS (row stride 65, so
+// lane-per-row reads are bank-conflict free).  Weight gradients
+// dW = sum_r dZ[r] (x) H[r] are register tiles over the LDS-staged rows, added
+// into one partial per workgroup (<= 512 per minibatch); k_ppo_reduce sums the
+// partials in a fixed order (run-to-run deterministic, no float atomics).
 #include <hip/hip_runtime.h>
 
 #include "rx.h"
 
 namespace {
 
-constexpr int kH = 64;       // hidden width (agent/ppo.py:20-29)
-constexpr int kNA = 2;       // action dims
-constexpr int kRows = 256;   // rows per workgroup = threads per workgroup
+constexpr int kH = 64;   // hidden width (agent/ppo.py:20-29)
+constexpr int kNA = 2;   // action dims
+constexpr int kT = 256;  // threads per workgroup (4 waves)
+constexpr int kRP = 64;  // rows per pass (lane = row)
+constexpr int kS = 65;   // LDS row stride of the [64][64] tiles (lane-per-row reads hit distinct banks)
+constexpr int kMaxWG = 512;  // partials per minibatch (rows per workgroup grow beyond that)
 
 template <int D>
-struct Lay {  // flat parameter offsets, module.parameters() order
+struct Lay {  // flat parameter offsets, module.parameters() order; Pp = partial row stride
   static constexpr int aW1 = 0, ab1 = aW1 + kH * D, aW2 = ab1 + kH, ab2 = aW2 + kH * kH, aW3 = ab2 + kH,
                        ab3 = aW3 + kNA * kH, cW1 = ab3 + kNA, cb1 = cW1 + kH * D, cW2 = cb1 + kH,
-                       cb2 = cW2 + kH * kH, cW3 = cb2 + kH, cb3 = cW3 + kH, P = cb3 + 1;
+                       cb2 = cW2 + kH * kH, cW3 = cb2 + kH, cb3 = cW3 + kH, P = cb3 + 1, Pp = (P + 63) / 64 * 64;
 };
 
 struct ppo_args {
   rx_ppo_batch b;
-  int32_t m;          // minibatch index within the epoch
+  int32_t m;            // minibatch index within the epoch
+  int32_t rows_per_wg;  // multiple of kRP
   const uint8_t* stop;
-  float* partial;     // [n_wg][P]
-  double* kl_partial; // [n_wg]
+  double* kl_partial;   // [n_wg]
 };
 
-// h = tanh(W x + b) for a 64-wide layer; W row-major [64][K] (scalar loads)
-template <int K>
-__device__ __forceinline__ void dense_tanh(const float* __restrict__ W, const float* __restrict__ bias,
-                                           const float* in, float* out) {
-#pragma unroll
-  for (int i = 0; i < kH; ++i) {
-    float z = 0.0f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) z = fmaf(W[i * K + k], in[k], z);
-    out[i] = tanhf(z + bias[i]);
-  }
-}
+__device__ __forceinline__ void put(float* p, float v, bool first) { *p = first ? v : *p + v; }
 
-// Phase helper: dW[I][J] (+)= sum_r dZ[r][i] * H[r][j] with dZ, H staged in LDS
-// ([kRows][I] and [kRows][J]); 4x4 register tiles over (i, j).
-template <int I, int J>
-__device__ __forceinline__ void acc_tile(const float* __restrict__ dZ, const float* __restrict__ Hs, float* dst,
-                                         float* dbias) {
-  static_assert(I % 4 == 0 && J % 4 == 0, "tile");
-  constexpr int TI = I / 4, TJ = J / 4, NT = TI * TJ;
-  for (int t = threadIdx.x; t < NT; t += kRows) {
-    const int i0 = (t / TJ) * 4, j0 = (t % TJ) * 4;
-    float acc[4][4] = {};
-    float bacc[4] = {};
-    for (int r = 0; r < kRows; ++r) {
-      const float4 z = *reinterpret_cast<const float4*>(dZ + r * I + i0);
-      const float4 h = *reinterpret_cast<const float4*>(Hs + r * J + j0);
-      const float zz[4] = {z.x, z.y, z.z, z.w}, hh[4] = {h.x, h.y, h.z, h.w};
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[a][c] = fmaf(zz[a], hh[c], acc[a][c]);
-        bacc[a] += zz[a];
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) dst[(i0 + a) * J + j0 + c] = acc[a][c];
-      if (j0 == 0 && dbias) dbias[i0 + a] = bacc[a];
-    }
-  }
-}
-
-// dW1[64][D] with D not a multiple of 4: thread -> (i, d) pairs.
+// One workgroup = rows_per_wg minibatch rows, processed kRP at a time.  Per
+// pass and per network (actor, then critic):
+//   forward  : wave w computes hidden columns [16w, 16w+16) for the 64 rows
+//              (lane = row), weights as SGPR operands, outputs to LDS;
+//   head     : wave 0 computes mu / value and the loss gradient per row;
+//   backward : dZ2 / dZ1 likewise column-split over waves;
+//   dW       : LDS-staged register tiles over the pass's rows, added into the
+//              workgroup's partial (each entry owned by one thread).
 template <int D>
-__device__ __forceinline__ void acc_first(const float* __restrict__ dZ, const float* __restrict__ X, float* dst,
-                                          float* dbias) {
-  for (int e = threadIdx.x; e < kH * D + kH; e += kRows) {
-    float s = 0.0f;
-    if (e < kH * D) {
-      const int i = e / D, d = e % D;
-      for (int r = 0; r < kRows; ++r) s = fmaf(dZ[r * kH + i], X[r * D + d], s);
-      dst[e] = s;
-    } else {
-      const int i = e - kH * D;
-      for (int r = 0; r < kRows; ++r) s += dZ[r * kH + i];
-      dbias[i] = s;
-    }
-  }
-}
-
-// W and partial are separate __restrict__ kernel arguments: the weights are then
-// provably never written by this kernel, so the compiler reads them with
-// scalar loads (SGPR operands) instead of per-lane vector loads.
-template <int D>
-__global__ __launch_bounds__(kRows) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
+__global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
                                                     float* __restrict__ partial) {
   using L = Lay<D>;
+  constexpr int XS = D + 1;
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
-  __shared__ float sA[kRows * kH];
-  __shared__ float sB[kRows * kH];
-  __shared__ float sX[kRows * D];
-  __shared__ double sKL[kRows / 64];
+  __shared__ float sX[kRP * XS];
+  __shared__ float sH1[kRP * kS];
+  __shared__ float sH2[kRP * kS];
+  __shared__ float sDZ[kRP * kS];
+  __shared__ float sHead[kRP * kNA];
+  __shared__ int64_t sSrc[kRP];
   const rx_ppo_batch& b = a.b;
-  float* __restrict__ out = partial + (size_t)blockIdx.x * L::P;
-  const int r = threadIdx.x;
-  const int row = blockIdx.x * kRows + r;
-  int64_t src = row < b.mb ? b.perm[(int64_t)a.m * b.mb + row] : -1;
-  const bool live = src >= 0 && src < b.n_rows;  // out-of-range indices contribute nothing
-  if (!live) src = 0;
-
-  float x[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) x[d] = live ? b.obs[src * D + d] : 0.0f;
-  // advantage normalisation with this minibatch's (mean, std), agent/ppo.py:187
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave index, provably uniform
+  float* __restrict__ out = partial + (size_t)blockIdx.x * L::Pp;
+  const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
   const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
-  const float An = live ? (b.advantages[src] - mean) / (sd + 1e-8f) : 0.0f;
   const float invM = 1.0f / (float)b.mb;
-  const float lo = 1.0f - b.clip_coef, hi = 1.0f + b.clip_coef;
-
-  // ------------------------------------------------ actor
-  float h1[kH], h2[kH];
-  dense_tanh<D>(W + L::aW1, W + L::ab1, x, h1);
-  dense_tanh<kH>(W + L::aW2, W + L::ab2, h1, h2);
-  float mu[kNA];
+  const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
+  double kl = 0.0;
+  bool first = true;
+  for (int64_t base = row0; base < row_end; base += kRP, first = false) {
+    if (t < kRP) {
+      int64_t src = base + t < row_end ? b.perm[(int64_t)a.m * b.mb + base + t] : -1;
+      sSrc[t] = (src >= 0 && src < b.n_rows) ? src : -1;  // out-of-range indices contribute nothing
+    }
+    __syncthreads();
+    for (int e = t; e < kRP * D; e += kT) {
+      const int r = e / D, d = e - r * D;
+      const int64_t src = sSrc[r];
+      sX[r * XS + d] = src >= 0 ? b.obs[src * D + d] : 0.0f;
+    }
+    const int64_t src = sSrc[lane];
+    const bool live = src >= 0;
+    __syncthreads();
+    for (int net = 0; net < 2; ++net) {
+      const int oW1 = net ? L::cW1 : L::aW1, ob1 = net ? L::cb1 : L::ab1;
+      const int oW2 = net ? L::cW2 : L::aW2, ob2 = net ? L::cb2 : L::ab2;
+      const int oW3 = net ? L::cW3 : L::aW3, ob3 = net ? L::cb3 : L::ab3;
+      const int n_out = net ? 1 : kNA;
+      // ---- layer 1: h1 = tanh(W1 x + b1), columns [16w, 16w+16)
+      {
+        float x[D];
 #pragma unroll
-  for (int j = 0; j < kNA; ++j) {
-    float z = 0.0f;
+        for (int d = 0; d < D; ++d) x[d] = sX[lane * XS + d];
+        for (int cg = 0; cg < 4; ++cg) {
+          const int c0 = w * 16 + cg * 4;
+          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < kH; ++k) z = fmaf(W[L::aW3 + j * kH + k], h2[k], z);
-    mu[j] = tanhf(z + W[L::ab3 + j]);
+          for (int d = 0; d < D; ++d) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
+        }
+      }
+      __syncthreads();
+      // ---- layer 2: h2 = tanh(W2 h1 + b2)
+      {
+        float h[kH];
+#pragma unroll
+        for (int k = 0; k < kH; ++k) h[k] = sH1[lane * kS + k];
+        for (int cg = 0; cg < 4; ++cg) {
+          const int c0 = w * 16 + cg * 4;
+          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int k = 0; k < kH; ++k) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
+        }
+      }
+      __syncthreads();
+      // ---- head and loss gradient (wave 0, lane = row)
+      if (w == 0) {
+        float h[kH];
+#pragma unroll
+        for (int k = 0; k < kH; ++k) h[k] = sH2[lane * kS + k];
+        if (net == 0) {
+          // Normal(mu, exp(log_std)).log_prob(action).sum(-1); clipped surrogate
+          float mu[kNA], diff[kNA], var[kNA], logp = 0.0f;
+#pragma unroll
+          for (int j = 0; j < kNA; ++j) {
+            float z = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kH; ++k) z = fmaf(W[oW3 + j * kH + k], h[k], z);
+            mu[j] = tanhf(z + W[ob3 + j]);
+            const float scale = expf(b.log_std[j]);
+            var[j] = scale * scale;
+            diff[j] = (live ? b.actions[src * kNA + j] : 0.0f) - mu[j];
+            logp += -(diff[j] * diff[j]) / (2.0f * var[j]) - logf(scale) - 0.91893853320467274178f;
+          }
+          const float oldlp = live ? b.logprobs[src] : 0.0f;
+          const float An = live ? (b.advantages[src] - mean) / (sd + 1e-8f) : 0.0f;
+          const float ratio = expf(logp - oldlp);
+          const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
+          const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;  // torch.max splits ties
+          const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+          const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
+#pragma unroll
+          for (int j = 0; j < kNA; ++j) sHead[lane * kNA + j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
+          if (live) kl += (double)(oldlp - logp);
+        } else {
+          float v = 0.0f;
+#pragma unroll
+          for (int k = 0; k < kH; ++k) v = fmaf(W[oW3 + k], h[k], v);
+          v += W[ob3];
+          // 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
+          const float R = live ? b.returns[src] : 0.0f, ov = live ? b.values[src] : 0.0f;
+          const float vd = v - ov;
+          const float vc = ov + fminf(fmaxf(vd, -clip), clip);
+          const float e1 = v - R, e2 = vc - R;
+          const float q1 = e1 * e1, q2 = e2 * e2;
+          const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
+          const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
+          sHead[lane] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
+        }
+      }
+      __syncthreads();
+      // ---- dW3 / db3 = sum_r head[r] (x) h2[r]
+      if (t < n_out * kH) {
+        const int j = t / kH, k = t - j * kH;
+        float s = 0.0f;
+        for (int r = 0; r < kRP; ++r) s = fmaf(sHead[r * n_out + j], sH2[r * kS + k], s);
+        put(out + oW3 + t, s, first);
+      } else if (t < n_out * kH + n_out) {
+        const int j = t - n_out * kH;
+        float s = 0.0f;
+        for (int r = 0; r < kRP; ++r) s += sHead[r * n_out + j];
+        put(out + ob3 + j, s, first);
+      }
+      // ---- dz2 = (W3^T head) * (1 - h2^2), columns [16w, 16w+16)
+      for (int q = 0; q < 16; ++q) {
+        const int k = w * 16 + q;
+        float dh = 0.0f;
+        for (int j = 0; j < n_out; ++j) dh = fmaf(sHead[lane * n_out + j], W[oW3 + j * kH + k], dh);
+        const float h2 = sH2[lane * kS + k];
+        sDZ[lane * kS + k] = dh * (1.0f - h2 * h2);
+      }
+      __syncthreads();
+      // ---- dW2 / db2 = sum_r dz2[r] (x) h1[r]: 4x4 tile per thread
+      {
+        const int c0 = (t >> 4) * 4, k0 = (t & 15) * 4;
+        float acc[4][4] = {}, bacc[4] = {};
+        for (int r = 0; r < kRP; ++r) {
+          float dz[4], hh[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            dz[q] = sDZ[r * kS + c0 + q];
+            hh[q] = sH1[r * kS + k0 + q];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(dz[i], hh[q], acc[i][q]);
+            bacc[i] += dz[i];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) put(out + oW2 + (c0 + i) * kH + k0 + q, acc[i][q], first);
+          if (k0 == 0) put(out + ob2 + c0 + i, bacc[i], first);
+        }
+      }
+      // ---- dz1 = (W2^T dz2) * (1 - h1^2), columns [16w, 16w+16) -> sH2 (h2 is dead)
+      {
+        float dz[kH];
+#pragma unroll
+        for (int c = 0; c < kH; ++c) dz[c] = sDZ[lane * kS + c];
+        for (int kg = 0; kg < 4; ++kg) {
+          const int k0 = w * 16 + kg * 4;
+          float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int c = 0; c < kH; ++c) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaf(W[oW2 + c * kH + k0 + q], dz[c], acc[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float h1 = sH1[lane * kS + k0 + q];
+            sH2[lane * kS + k0 + q] = acc[q] * (1.0f - h1 * h1);
+          }
+        }
+      }
+      __syncthreads();
+      // ---- dW1 / db1 = sum_r dz1[r] (x) x[r]
+      for (int e = t; e < kH * D + kH; e += kT) {
+        float s = 0.0f;
+        if (e < kH * D) {
+          const int c = e / D, d = e - c * D;
+          for (int r = 0; r < kRP; ++r) s = fmaf(sH2[r * kS + c], sX[r * XS + d], s);
+          put(out + oW1 + e, s, first);
+        } else {
+          const int c = e - kH * D;
+          for (int r = 0; r < kRP; ++r) s += sH2[r * kS + c];
+          put(out + ob1 + c, s, first);
+        }
+      }
+      __syncthreads();
+    }
   }
-  // Normal(mu, exp(log_std)).log_prob(action).sum(-1)  (torch.distributions.Normal)
-  float logp = 0.0f, diff[kNA], var[kNA];
-#pragma unroll
-  for (int j = 0; j < kNA; ++j) {
-    const float scale = expf(b.log_std[j]);
-    var[j] = scale * scale;
-    const float act = live ? b.actions[src * kNA + j] : 0.0f;
-    diff[j] = act - mu[j];
-    logp += -(diff[j] * diff[j]) / (2.0f * var[j]) - logf(scale) - 0.91893853320467274178f;
-  }
-  const float oldlp = live ? b.logprobs[src] : 0.0f;
-  const float ratio = expf(logp - oldlp);
-  // clipped surrogate: max(-A*ratio, -A*clamp(ratio)), torch.max splits ties
-  const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
-  const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;
-  const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-  const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
-  float dz3[kNA];
-#pragma unroll
-  for (int j = 0; j < kNA; ++j) dz3[j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
-
-  // KL partial: sum(old_logp - new_logp) over live rows
-  {
-    double kl = live ? (double)(oldlp - logp) : 0.0;
+  if (w == 0) {
     for (int o = 32; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
-    if ((r & 63) == 0) sKL[r >> 6] = kl;
+    if (lane == 0) a.kl_partial[blockIdx.x] = kl;
   }
-  // layer 3: dW3 = dz3 (x) h2
-#pragma unroll
-  for (int k = 0; k < kH; ++k) sA[r * kH + k] = live ? h2[k] : 0.0f;
-#pragma unroll
-  for (int j = 0; j < kNA; ++j) sB[r * kNA + j] = dz3[j];
-#pragma unroll
-  for (int d = 0; d < D; ++d) sX[r * D + d] = x[d];
-  __syncthreads();
-  if (r == 0) {
-    double s = 0.0;
-    for (int w = 0; w < kRows / 64; ++w) s += sKL[w];
-    a.kl_partial[blockIdx.x] = s;
-  }
-  if (r < kNA * kH) {
-    const int j = r / kH, k = r % kH;
-    float s = 0.0f;
-    for (int q = 0; q < kRows; ++q) s = fmaf(sB[q * kNA + j], sA[q * kH + k], s);
-    out[L::aW3 + j * kH + k] = s;
-  } else if (r < kNA * kH + kNA) {
-    const int j = r - kNA * kH;
-    float s = 0.0f;
-    for (int q = 0; q < kRows; ++q) s += sB[q * kNA + j];
-    out[L::ab3 + j] = s;
-  }
-  // dz2 = (W3^T dz3) * (1 - h2^2)
-#pragma unroll
-  for (int k = 0; k < kH; ++k) {
-    float s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kNA; ++j) s = fmaf(W[L::aW3 + j * kH + k], dz3[j], s);
-    h2[k] = live ? s * (1.0f - h2[k] * h2[k]) : 0.0f;  // h2 now holds dz2
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kH; ++k) {
-    sA[r * kH + k] = h2[k];                  // dz2
-    sB[r * kH + k] = live ? h1[k] : 0.0f;    // h1
-  }
-  __syncthreads();
-  acc_tile<kH, kH>(sA, sB, out + L::aW2, out + L::ab2);
-  // dz1 = (W2^T dz2) * (1 - h1^2)
-  float dz1[kH];
-#pragma unroll
-  for (int k = 0; k < kH; ++k) dz1[k] = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kH; ++i) {
-#pragma unroll
-    for (int k = 0; k < kH; ++k) dz1[k] = fmaf(W[L::aW2 + i * kH + k], h2[i], dz1[k]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kH; ++k) sA[r * kH + k] = live ? dz1[k] * (1.0f - h1[k] * h1[k]) : 0.0f;
-  __syncthreads();
-  acc_first<D>(sA, sX, out + L::aW1, out + L::ab1);
-
-  // ------------------------------------------------ critic
-  dense_tanh<D>(W + L::cW1, W + L::cb1, x, h1);
-  dense_tanh<kH>(W + L::cW2, W + L::cb2, h1, h2);
-  float v = 0.0f;
-#pragma unroll
-  for (int k = 0; k < kH; ++k) v = fmaf(W[L::cW3 + k], h2[k], v);
-  v += W[L::cb3];
-  // clipped value loss 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
-  const float R = live ? b.returns[src] : 0.0f, ov = live ? b.values[src] : 0.0f;
-  const float vd = v - ov;
-  const float vc = ov + fminf(fmaxf(vd, -b.clip_coef), b.clip_coef);
-  const float e1 = v - R, e2 = vc - R;
-  const float q1 = e1 * e1, q2 = e2 * e2;
-  const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
-  const float vin = (vd >= -b.clip_coef && vd <= b.clip_coef) ? 1.0f : 0.0f;
-  const float dv = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kH; ++k) sA[r * kH + k] = live ? h2[k] : 0.0f;
-  sB[r] = dv;
-  __syncthreads();
-  if (r < kH) {
-    float s = 0.0f;
-    for (int q = 0; q < kRows; ++q) s = fmaf(sB[q], sA[q * kH + r], s);
-    out[L::cW3 + r] = s;
-  } else if (r == kH) {
-    float s = 0.0f;
-    for (int q = 0; q < kRows; ++q) s += sB[q];
-    out[L::cb3] = s;
-  }
-#pragma unroll
-  for (int k = 0; k < kH; ++k) h2[k] = live ? W[L::cW3 + k] * dv * (1.0f - h2[k] * h2[k]) : 0.0f;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kH; ++k) {
-    sA[r * kH + k] = h2[k];
-    sB[r * kH + k] = live ? h1[k] : 0.0f;
-  }
-  __syncthreads();
-  acc_tile<kH, kH>(sA, sB, out + L::cW2, out + L::cb2);
-#pragma unroll
-  for (int k = 0; k < kH; ++k) dz1[k] = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kH; ++i) {
-#pragma unroll
-    for (int k = 0; k < kH; ++k) dz1[k] = fmaf(W[L::cW2 + i * kH + k], h2[i], dz1[k]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kH; ++k) sA[r * kH + k] = live ? dz1[k] * (1.0f - h1[k] * h1[k]) : 0.0f;
-  __syncthreads();
-  acc_first<D>(sA, sX, out + L::cW1, out + L::cb1);
 }
 
-// grad[p] = sum_w partial[w][p] (fixed order); block 0 also folds the KL
-// partials into approx_kl and raises the early-stop flag (agent/ppo.py:178-182).
-__global__ __launch_bounds__(256) void k_ppo_reduce(const float* __restrict__ partial, const double* __restrict__ klp,
-                                                    int n_wg, int P, int mb, float kl_target, float* grad,
-                                                    uint8_t* stop, float* kl_at_stop) {
+// grad[p] = sum_w partial[w][p] in a fixed order: 16 interleaved slices of
+// the workgroups per 256-parameter block (float4 lanes), combined in slice
+// order.  Block 0's wave 0 also folds the KL partials into approx_kl and raises
+// the early-stop flag (agent/ppo.py:178-182).  Partials have row stride Pp
+// (P rounded up to 64) so every row is float4-aligned.
+__global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
+                                                     const double* __restrict__ klp, int n_wg, int P, int Pp, int mb,
+                                                     float kl_target, float* grad, uint8_t* stop, float* kl_at_stop) {
   if (*stop) return;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p < P) {
-    float s = 0.0f;
-    for (int w = 0; w < n_wg; ++w) s += partial[(size_t)w * P + p];
-    grad[p] = s;
+  __shared__ float4 red[16][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int p4 = blockIdx.x * 256 + lane * 4;  // first of this lane's 4 parameters
+  float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (p4 < Pp)
+    for (int w = sl; w < n_wg; w += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + (size_t)w * Pp + p4);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  red[sl][lane] = s;
+  __syncthreads();
+  if (sl == 0 && p4 < P) {
+    float4 t = red[0][lane];
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][lane];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+    const float o[4] = {t.x, t.y, t.z, t.w};
+    for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o[q];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    double s = 0.0;
-    for (int w = 0; w < n_wg; ++w) s += klp[w];
-    const float kl = (float)(s / (double)mb);
-    if (kl > kl_target) {
+  if (blockIdx.x == 0 && sl == 1) {
+    double k = 0.0;
+    for (int w = lane; w < n_wg; w += 64) k += klp[w];
+    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
+    const float kl = (float)(k / (double)mb);
+    if (lane == 0 && kl > kl_target) {
       *kl_at_stop = kl;
       *stop = 1;  // read by the optimizer launch that follows on the stream
     }
@@ -334,9 +346,20 @@ __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ ad
 
 }  // namespace
 
+static int rows_per_wg(int mb) {
+  const int passes = (mb + kRP * kMaxWG - 1) / (kRP * kMaxWG);
+  return kRP * (passes < 1 ? 1 : passes);
+}
+
+extern "C" int rx_ppo_n_wg(int mb) {
+  const int rp = rows_per_wg(mb);
+  return (mb + rp - 1) / rp;
+}
+
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb) {
-  const int P = obs_dim == 15 ? Lay<15>::P : Lay<19>::P;
-  return (size_t)((mb + kRows - 1) / kRows) * P;
+  const int P = obs_dim == 15 ? Lay<15>::Pp : Lay<19>::Pp;
+  const int rp = rows_per_wg(mb);
+  return (size_t)((mb + rp - 1) / rp) * P;
 }
 
 extern "C" int rx_ppo_n_params(int32_t obs_dim) {
@@ -350,17 +373,18 @@ extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats
 
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, float* kl_at_stop, float* partial,
                                   double* klp, float* grad, hipStream_t s) {
-  const int n_wg = (b->mb + kRows - 1) / kRows;
-  ppo_args a{*b, m, stop, partial, klp};
-  int P;
+  const int rp = rows_per_wg(b->mb);
+  const int n_wg = (b->mb + rp - 1) / rp;
+  ppo_args a{*b, m, rp, stop, klp};
+  int P, Pp;
   if (b->obs_dim == 15) {
-    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg), dim3(kRows), 0, s, a, b->params, partial);
-    P = Lay<15>::P;
+    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg), dim3(kT), 0, s, a, b->params, partial);
+    P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
-    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg), dim3(kRows), 0, s, a, b->params, partial);
-    P = Lay<19>::P;
+    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg), dim3(kT), 0, s, a, b->params, partial);
+    P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
-  hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 255) / 256), dim3(256), 0, s, partial, klp, n_wg, P, b->mb,
+  hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 255) / 256), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
                      b->kl_target, grad, stop, kl_at_stop);
   return (int)hipGetLastError();
 }

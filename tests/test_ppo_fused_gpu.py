@@ -68,7 +68,7 @@ def test_fused_grad_matches_autograd(D):
         torch.testing.assert_close(got, want, rtol=2e-4, atol=2e-5 * float(scale))
         assert bool(stop) == (float(akl) > cfg["kl_target"])  # random old log-probs: KL is large
         # kl: the fused kernel accumulates in double; compare to torch's mean
-        s = float(fg.ws_d[:mb // 256].sum()) / mb
+        s = float(fg.ws_d.sum()) / mb  # one KL partial per workgroup
         assert abs(s - float(akl)) <= 1e-5 + 1e-4 * abs(float(akl))
 
 

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--max-minutes", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--device-shuffle", action="store_true", help="config shuffle='device' (torch.randperm)")
     args = ap.parse_args()
 
     from rx.configs import base_config
@@ -43,7 +44,7 @@ def main():
     from rx.track import gen_tracks
 
     config = base_config(num_envs=args.num_envs, num_steps=args.num_steps, total_timesteps=args.total_timesteps,
-                         seed=args.seed)
+                         seed=args.seed, shuffle="device" if args.device_shuffle else "numpy")
     random.seed(config["seed"])
     np.random.seed(config["seed"])
     torch.manual_seed(config["seed"])
@@ -85,6 +86,7 @@ def main():
            "value_s": reached["train_s"] if reached else None,
            "reached_at_step": reached["global_step"] if reached else None,
            "config": {"num_envs": args.num_envs, "num_steps": args.num_steps, "total_timesteps": args.total_timesteps,
+                      "shuffle": config.get("shuffle", "numpy"),
                       "eval": "evaluate.py protocol: 40 tracks (seed 42) x 5 runs, widths by run, max 2000 steps, "
                               "stochastic policy", "eval_every_updates": args.eval_every},
            "build_s": round(build_s, 3), "curve": curve}
