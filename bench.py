@@ -110,7 +110,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cull-chunk", type=int, default=16, help="raycast chunk culling (0 = brute force)")
-    ap.add_argument("--sort-interval", type=int, default=0, help="spatial env re-sort period (0 = never)")
+    ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
+    ap.add_argument("--ray-order", type=int, default=1, help="raycast lane order (0 env-major, 1 ray-major)")
+    ap.add_argument("--sample-every", type=int, default=8,
+                    help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,12 +123,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs visible")
+    local_dev = local % max(ndev, 1)  # gloo rehearsal: several ranks may share one GPU
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from rx.vector_env import RacingVectorEnv
     E = args.envs_per_gpu
@@ -131,51 +143,57 @@ def main():
     pool, widths = seed1_pool(n_total)
     lo, hi = rank * E, (rank + 1) * E
     env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step",
-                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval)
+                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval, ray_order=args.ray_order)
     n_slots = len(env.tracks)
     S_of_env = 2 * np.diff(env.tracks.arrays()["wp_off"])[env.track_of_env]
     ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))
 
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
+    torch.manual_seed(1234 + rank)  # default CUDA generator: graph-capturable
     scale = torch.tensor([2.0, 1.0], device=dev)
     shift = torch.tensor([-1.0, 0.0], device=dev)
     actions = torch.empty((E, 2), device=dev)
 
-    def one_step(ev=None):
-        torch.rand((E, 2), generator=gen, device=dev, out=actions)
+    def draw_actions():
+        torch.rand((E, 2), device=dev, out=actions)
         actions.mul_(scale).add_(shift)
-        if ev is None:
+
+    env.reset_device()
+
+    def one_step(ev=None):
+        draw_actions()
+        if ev is None:  # the production call: one rx_step, both kernels back to back
             env.step_device(actions)
-        else:
+        else:           # instrumented step: split into the two phases around HIP events
             ev[0].record()
             env.step_device(actions, phases=1)
             ev[1].record()
             env.step_device(actions, phases=2)
             ev[2].record()
 
-    env.reset_device()
     for _ in range(args.warmup):
         one_step()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # every --sample-every'th timed step is instrumented (event records between the
+    # kernels cost ~10 us of GPU idle per step, so not every step carries them)
+    timed = [k for k in range(args.steps) if k % args.sample_every == 0]
+    events = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for k in timed}
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(events[k])
+        one_step(events.get(k))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events.values()]))
+    ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events.values()]))
     ep = env.episode_stats()
     gae = gae_roofline(E, dev) if rank == 0 else None
 
@@ -207,6 +225,8 @@ def main():
                                    "11 sensors, uniform random device actions, next-step autoreset)",
                        "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
+                       "ray_order": args.ray_order,
+                       "kernel_timing": f"HIP events around k_dyn1 / k_rays on every {args.sample_every}th timed step",
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,

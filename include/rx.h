@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 4
+#define RX_ABI_VERSION 5
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -77,6 +77,10 @@ typedef struct {
   double speed_weight;     /* RacingEnv.speed_weight, 8.0 (racing_env.py:9,26) */
   int32_t cull_chunk;      /* raycast culling: segments per chunk (16 recommended; 0 = test every segment) */
   int32_t sort_interval;   /* re-sort envs by track position every k dynamics launches (0 = never) */
+  int32_t ray_order;       /* raycast lane order: 0 = (env, agent, ray), 11 rays of ~6 envs per wave;
+                              1 = ray-major: one (agent, ray) of 64 consecutive envs per wave -- with
+                              sort_interval > 0 those envs are track neighbours, so a wave's rays are
+                              nearly parallel and share culling chunks.  Scheduling only: same results. */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -249,6 +253,27 @@ size_t rx_ppo_workspace_doubles(int32_t mb);
 int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* stream);
 int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, double* ws_f64, float* grad,
                           uint8_t* stop, float* kl_at_stop, void* stream);
+
+/* Rollout policy step (agent/ppo.py:105-110: agent.get_action_and_value(obs)
+ * under no_grad) for the same policy layout: per row, actor + critic forward,
+ *   action = clamp(eps * exp(log_std) + mu, -1, 1)   (Normal.sample(), then
+ *            the reference's clamp; eps = N(0,1) noise drawn by the caller,
+ *            e.g. torch normal_(), so the sampling stream stays torch's)
+ *   logprob = sum_j Normal(mu, std).log_prob(action_j);  value = critic(obs).
+ * fp32; equal to the torch forward within float rounding
+ * (tests/test_ppo_fused_gpu.py). */
+typedef struct rx_policy_io {
+  int32_t obs_dim;        /* 15 or 19 */
+  int64_t n;              /* rows */
+  const float* obs;       /* [n][D] */
+  const float* eps;       /* [n][2] */
+  const float* params;    /* flat parameters */
+  const float* log_std;   /* [2] */
+  float* actions;         /* [n][2] out */
+  float* logprobs;        /* [n] out */
+  float* values;          /* [n] out */
+} rx_policy_io;
+int rx_policy_act(const rx_policy_io* io, void* stream);
 
 #ifdef __cplusplus
 }

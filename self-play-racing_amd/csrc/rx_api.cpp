@@ -82,6 +82,7 @@ struct rx_env {
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
   int cur = 0;
   DevBuf<rx_wave> dyn_waves, ray_waves;
+  DevBuf<int32_t> slot_n;   // envs per slot (ray-major decode)
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   DevBuf<double> rel_angles;
@@ -184,6 +185,7 @@ int rx_create(const rx_config* cfg, rx_env** out) {
   if (cfg->n_agents != 1 && cfg->n_agents != 2) return fail(RX_EINVAL, "n_agents must be 1 or 2 (got %d)", cfg->n_agents);
   if (cfg->n_sensors <= 0 || cfg->n_sensors > 256) return fail(RX_EINVAL, "n_sensors out of range (%d)", cfg->n_sensors);
   if (cfg->max_steps <= 0) return fail(RX_EINVAL, "max_steps must be > 0");
+  if (cfg->ray_order != 0 && cfg->ray_order != 1) return fail(RX_EINVAL, "ray_order must be 0 or 1 (got %d)", cfg->ray_order);
   if (cfg->autoreset < RX_AUTORESET_NEXT_STEP || cfg->autoreset > RX_AUTORESET_DISABLED)
     return fail(RX_EINVAL, "bad autoreset mode %d", cfg->autoreset);
   if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
@@ -283,6 +285,8 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   std::iota(perm.begin(), perm.end(), 0);
   std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return track_of_env[a] < track_of_env[b]; });
   std::vector<rx_wave> dyn, ray;
+  std::vector<int32_t> slot_n(h->n_tracks, 0);
+  for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
   int g0 = 0;
   while (g0 < N) {
     const int k = track_of_env[perm[g0]];
@@ -297,6 +301,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   }
   RX_HIP(hipSetDevice(h->cfg.device));
   int rc;
+  if ((rc = upload(h->slot_n, slot_n.data(), slot_n.size()))) return rc;
   if ((rc = upload(h->perm[0], perm.data(), perm.size()))) return rc;
   if ((rc = upload(h->perm[1], perm.data(), perm.size()))) return rc;
   h->cur = 0;
@@ -378,6 +383,8 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.speed_weight = h->cfg.speed_weight;
   a.seed = h->cfg.seed;
   a.reset_count = h->resets.p;
+  a.ray_order = h->cfg.ray_order;
+  a.slot_nenv = h->slot_n.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;
   if (phases & RX_PHASE_DYNAMICS) {
@@ -496,6 +503,17 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
   if (!ws_f32 || !ws_f64 || !grad || !stop || !kl_at_stop) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: null buffer");
   if ((rc = rx_launch_ppo_grad(b, m, stop, kl_at_stop, ws_f32, ws_f64, grad, (hipStream_t)stream)) != 0)
     return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_policy_act(const rx_policy_io* io, void* stream) {
+  if (!io) return fail(RX_EINVAL, "rx_policy_act: io is null");
+  if (io->obs_dim != 15 && io->obs_dim != 19) return fail(RX_EINVAL, "rx_policy_act: obs_dim=%d (15 or 19)", io->obs_dim);
+  if (io->n <= 0) return fail(RX_EINVAL, "rx_policy_act: n=%lld", (long long)io->n);
+  if (!io->obs || !io->eps || !io->params || !io->log_std || !io->actions || !io->logprobs || !io->values)
+    return fail(RX_EINVAL, "rx_policy_act: null buffer");
+  const int rc = rx_launch_policy_act(io, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "policy launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }
 

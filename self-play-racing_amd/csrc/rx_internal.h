@@ -56,6 +56,8 @@ struct rx_kargs {
   int32_t autoreset;
   int32_t mode;
   int32_t cull_chunk;         // segments per culling chunk G (0 = brute force over all segments)
+  int32_t ray_order;          // rx_config.ray_order
+  const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;
   uint32_t* reset_count;  // [N] (2-car envs), advanced by k_dyn2 at every reset
@@ -68,6 +70,7 @@ extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, flo
                               const double* lr, const uint8_t* stop, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
+extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);
 extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, hipStream_t s);
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, float* kl_at_stop, float* partial,
                                   double* klp, float* grad, hipStream_t s);

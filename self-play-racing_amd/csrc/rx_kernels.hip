@@ -397,7 +397,12 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   // non-ray observation columns of the CURRENT state (racing_env.py:58-75)
   {
     double s, co;
-    rx_sincos(c.angle, &s, &co);
+    if (moving && !do_reset) {  // car_kinematics already evaluated sin/cos of this angle
+      co = cs[0];
+      s = cs[1];
+    } else {
+      rx_sincos(c.angle, &s, &co);
+    }
     double vf = c.vx * co + c.vy * s;
     double vl = (-c.vx) * s + c.vy * co;
     float* o = a.io.obs + (size_t)e * a.D + a.n_sensors;
@@ -510,6 +515,10 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   double rw[2] = {0.0, 0.0};
   int place[2] = {0, 0};
   bool term = false, trunc = false;
+  // sin/cos of each car's CURRENT angle, evaluated at most once per step
+  // (kinematics, car-car contact and the observation all need them)
+  double sn[2], cn[2];
+  bool have_sc[2] = {false, false};
   if (stepping) {
     const float4 act = reinterpret_cast<const float4*>(a.io.actions)[e];
     const float av[4] = {act.x, act.y, act.z, act.w};
@@ -520,7 +529,12 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
       last_steering[q] = (double)clipf(av[2 * q], -1.0f, 1.0f);
       const float thr = clipf((av[2 * q + 1] + 1.0f) / 2.0f, 0.0f, 1.0f);
       mv[q] = !c[q].crashed;
-      if (mv[q]) car_kinematics(c[q], last_steering[q], (double)thr, cs[q], cx[q], cy[q]);
+      if (mv[q]) {
+        car_kinematics(c[q], last_steering[q], (double)thr, cs[q], cx[q], cy[q]);
+        cn[q] = cs[q][0];
+        sn[q] = cs[q][1];
+        have_sc[q] = true;
+      }
     }
     if (mv[0] || mv[1]) {
       double px[10], py[10];
@@ -554,11 +568,15 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     }
     // car-car contact, multi_racing_env.py:222-231 (corners of the current state)
     {
-      double ax[4], ay[4], bx[4], by[4], s0, c0, s1, c1;
-      rx_sincos(c[0].angle, &s0, &c0);
-      rx_sincos(c[1].angle, &s1, &c1);
-      corners(c[0].x, c[0].y, c0, s0, ax, ay);
-      corners(c[1].x, c[1].y, c1, s1, bx, by);
+      double ax[4], ay[4], bx[4], by[4];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (!have_sc[q]) {
+          rx_sincos(c[q].angle, &sn[q], &cn[q]);
+          have_sc[q] = true;
+        }
+      corners(c[0].x, c[0].y, cn[0], sn[0], ax, ay);
+      corners(c[1].x, c[1].y, cn[1], sn[1], bx, by);
       if (rect_intersect(ax, ay, bx, by)) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -625,6 +643,7 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     }
   }
   if (do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
+    have_sc[0] = have_sc[1] = false;  // angles are reset below
     const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.reset_count[e]++ << 32) ^ (uint64_t)e));
     const int first = (int)(h & 1ull);  // agent_order[0] after np.random.shuffle([0, 1])
 #pragma unroll
@@ -678,7 +697,12 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     const Car& me = c[q];
     const Car& o = c[1 - q];
     double s, co;
-    rx_sincos(me.angle, &s, &co);
+    if (have_sc[q]) {
+      s = sn[q];
+      co = cn[q];
+    } else {
+      rx_sincos(me.angle, &s, &co);
+    }
     double vf = me.vx * co + me.vy * s;
     double vl = (-me.vx) * s + me.vy * co;
     double rx_ = o.x - me.x, ry_ = o.y - me.y;
@@ -789,10 +813,19 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   if (lane >= we.count) return;
   const int R = a.n_sensors;
   const int task = we.task_start + lane;
-  const int env_local = task / (A * R);
-  const int rem = task - env_local * (A * R);
-  const int q = rem / R;
-  const int ray = rem - q * R;
+  int env_local, q, ray;
+  if (a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
+    env_local = task / (A * R);
+    const int rem = task - env_local * (A * R);
+    q = rem / R;
+    ray = rem - q * R;
+  } else {  // ray-major: one (agent, ray) over consecutive (position-sorted) envs
+    const int ng = uniform(a.slot_nenv[k]);
+    const int qr = task / ng;
+    env_local = task - qr * ng;
+    q = qr / R;
+    ray = qr - q * R;
+  }
   const int e = a.perm[we.perm_start + env_local];
   const int i = A * e + q;
   const double ox = a.st.x[i], oy = a.st.y[i];

@@ -42,6 +42,56 @@ struct ppo_args {
 
 __device__ __forceinline__ void put(float* p, float v, bool first) { *p = first ? v : *p + v; }
 
+// The two 64-wide tanh layers of one trunk (agent/ppo.py:20-29) for kRP rows:
+// lane = row, wave w computes hidden columns [16w, 16w+16) with the weights as
+// SGPR operands; h1 -> sH1, h2 -> sH2 (row stride kS).  Ends with the
+// barrier that publishes sH2.
+template <int D>
+__device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int oW1, int ob1, int oW2, int ob2,
+                                              const float* sX, float* sH1, float* sH2, int lane, int w) {
+  constexpr int XS = D + 1;
+  {
+    float x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = sX[lane * XS + d];
+    for (int cg = 0; cg < 4; ++cg) {
+      const int c0 = w * 16 + cg * 4;
+      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
+    }
+  }
+  __syncthreads();
+  {
+    float h[kH];
+#pragma unroll
+    for (int k = 0; k < kH; ++k) h[k] = sH1[lane * kS + k];
+    for (int cg = 0; cg < 4; ++cg) {
+      const int c0 = w * 16 + cg * 4;
+      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int k = 0; k < kH; ++k) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
+    }
+  }
+  __syncthreads();
+}
+
+// Normal(mu, exp(log_std)).log_prob(a) for one action dim, in torch's operation
+// order (torch/distributions/normal.py: -((a-mu)**2)/(2*var) - log(scale) - log(sqrt(2*pi))).
+__device__ __forceinline__ float normal_logp(float diff, float var, float log_scale) {
+  return -(diff * diff) / (2.0f * var) - log_scale - 0.91893853320467274178f;
+}
+
 // One workgroup = rows_per_wg minibatch rows, processed kRP at a time.  Per
 // pass and per network (actor, then critic):
 //   forward  : wave w computes hidden columns [16w, 16w+16) for the 64 rows
@@ -92,42 +142,7 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
       const int oW2 = net ? L::cW2 : L::aW2, ob2 = net ? L::cb2 : L::ab2;
       const int oW3 = net ? L::cW3 : L::aW3, ob3 = net ? L::cb3 : L::ab3;
       const int n_out = net ? 1 : kNA;
-      // ---- layer 1: h1 = tanh(W1 x + b1), columns [16w, 16w+16)
-      {
-        float x[D];
-#pragma unroll
-        for (int d = 0; d < D; ++d) x[d] = sX[lane * XS + d];
-        for (int cg = 0; cg < 4; ++cg) {
-          const int c0 = w * 16 + cg * 4;
-          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int d = 0; d < D; ++d) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
-        }
-      }
-      __syncthreads();
-      // ---- layer 2: h2 = tanh(W2 h1 + b2)
-      {
-        float h[kH];
-#pragma unroll
-        for (int k = 0; k < kH; ++k) h[k] = sH1[lane * kS + k];
-        for (int cg = 0; cg < 4; ++cg) {
-          const int c0 = w * 16 + cg * 4;
-          float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int k = 0; k < kH; ++k) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
-        }
-      }
-      __syncthreads();
+      hidden_layers<D>(W, oW1, ob1, oW2, ob2, sX, sH1, sH2, lane, w);
       // ---- head and loss gradient (wave 0, lane = row)
       if (w == 0) {
         float h[kH];
@@ -145,7 +160,7 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
             const float scale = expf(b.log_std[j]);
             var[j] = scale * scale;
             diff[j] = (live ? b.actions[src * kNA + j] : 0.0f) - mu[j];
-            logp += -(diff[j] * diff[j]) / (2.0f * var[j]) - logf(scale) - 0.91893853320467274178f;
+            logp += normal_logp(diff[j], var[j], logf(scale));
           }
           const float oldlp = live ? b.logprobs[src] : 0.0f;
           const float An = live ? (b.advantages[src] - mean) / (sd + 1e-8f) : 0.0f;
@@ -260,6 +275,64 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
   if (w == 0) {
     for (int o = 32; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
     if (lane == 0) a.kl_partial[blockIdx.x] = kl;
+  }
+}
+
+// Rollout policy step (agent/ppo.py:105-110, get_action_and_value on obs[t]):
+// actor + critic forward for kRP rows per workgroup, then per row
+//   action = clamp(eps * std + mu, -1, 1)        (Normal.sample() = normal_() * std + mu)
+//   logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs)
+// eps [N][2] is drawn by the caller with torch's normal_() so the sampling
+// stream is torch's.  Outputs go straight into the rollout buffers.
+template <int D>
+__global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const float* __restrict__ W) {
+  using L = Lay<D>;
+  constexpr int XS = D + 1;
+  __shared__ float sX[kRP * XS];
+  __shared__ float sH1[kRP * kS];
+  __shared__ float sH2[kRP * kS];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t base = (int64_t)blockIdx.x * kRP;
+  const int64_t row = base + lane;
+  const bool live = row < io.n;
+  for (int e = t; e < kRP * D; e += kT) {
+    const int r = e / D, d = e - r * D;
+    sX[r * XS + d] = base + r < io.n ? io.obs[(base + r) * D + d] : 0.0f;
+  }
+  __syncthreads();
+  float mu[kNA];
+  hidden_layers<D>(W, L::aW1, L::ab1, L::aW2, L::ab2, sX, sH1, sH2, lane, w);
+  if (w == 0) {
+    float h[kH];
+#pragma unroll
+    for (int k = 0; k < kH; ++k) h[k] = sH2[lane * kS + k];
+#pragma unroll
+    for (int j = 0; j < kNA; ++j) {
+      float z = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kH; ++k) z = fmaf(W[L::aW3 + j * kH + k], h[k], z);
+      mu[j] = tanhf(z + W[L::ab3 + j]);
+    }
+  }
+  __syncthreads();  // sH1/sH2 are rewritten by the critic trunk
+  hidden_layers<D>(W, L::cW1, L::cb1, L::cW2, L::cb2, sX, sH1, sH2, lane, w);
+  if (w == 0 && live) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kH; ++k) v = fmaf(W[L::cW3 + k], sH2[lane * kS + k], v);
+    io.values[row] = v + W[L::cb3];
+    float logp = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kNA; ++j) {
+      const float scale = expf(io.log_std[j]);
+      const float var = scale * scale;
+      const float smp = io.eps[row * kNA + j] * scale + mu[j];  // mul_(std).add_(mu): two roundings
+      const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
+      io.actions[row * kNA + j] = a;
+      logp += normal_logp(a - mu[j], var, logf(scale));
+    }
+    io.logprobs[row] = logp;
   }
 }
 
@@ -386,5 +459,14 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, f
   }
   hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 255) / 256), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
                      b->kl_target, grad, stop, kl_at_stop);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
+  const int n_wg = (int)((io->n + kRP - 1) / kRP);
+  if (io->obs_dim == 15)
+    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+  else
+    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
   return (int)hipGetLastError();
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -26,7 +26,7 @@ _P = ctypes.c_void_p
 EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sensor_angles", "rx_upload_tracks",
            "rx_assign", "rx_bind_state", "rx_set_speed_weight", "rx_reset", "rx_step", "rx_step_phases", "rx_gae",
            "rx_gae_scan", "rx_adam_clip_step", "rx_ppo_n_params", "rx_ppo_workspace_floats",
-           "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad")
+           "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
 
@@ -35,7 +35,8 @@ class RxConfig(ctypes.Structure):
     _fields_ = [("n_envs", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_sensors", ctypes.c_int32),
                 ("max_steps", ctypes.c_int32), ("autoreset", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double),
-                ("cull_chunk", ctypes.c_int32), ("sort_interval", ctypes.c_int32)]
+                ("cull_chunk", ctypes.c_int32), ("sort_interval", ctypes.c_int32),
+                ("ray_order", ctypes.c_int32)]
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
@@ -64,6 +65,11 @@ class RxPPOBatch(ctypes.Structure):
                [(k, _P) for k in ("obs", "actions", "logprobs", "advantages", "returns", "values", "perm", "params",
                                   "log_std", "adv_stats")] + \
                [("clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float), ("kl_target", ctypes.c_float)]
+
+
+class RxPolicyIO(ctypes.Structure):
+    _fields_ = [("obs_dim", ctypes.c_int32), ("n", ctypes.c_int64)] + \
+               [(k, _P) for k in ("obs", "eps", "params", "log_std", "actions", "logprobs", "values")]
 
 
 class RxError(RuntimeError):
@@ -111,6 +117,7 @@ def load(build_if_missing=True):
     L.rx_ppo_workspace_doubles.restype = ctypes.c_size_t
     L.rx_ppo_adv_stats.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P]
     L.rx_ppo_minibatch_grad.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P, _P, _P, _P, _P]
+    L.rx_policy_act.argtypes = [ctypes.POINTER(RxPolicyIO), _P]
     for name in EXPORTS:
         if name not in ("rx_last_error", "rx_abi_version", "rx_ppo_workspace_floats", "rx_ppo_workspace_doubles"):
             getattr(L, name).restype = ctypes.c_int

@@ -111,16 +111,34 @@ class PPO:
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False)
         return contextlib.nullcontext()
 
+    def _fused_policy(self, obs):
+        """rx_policy_act driver when config["fused_policy"] (default on) and the
+        policy is the reference layout in flat fp32 buffers; else None."""
+        from . import ppo_fused
+        c = self.config
+        if (not c.get("fused_policy", True) or c.get("policy_dtype", "fp32") != "fp32"
+                or getattr(self, "_flat", None) is None or obs.dim() != 3
+                or not ppo_fused.policy_supported(self.agent, obs.shape[2])):
+            return None
+        pa = self.__dict__.get("_policy_act")
+        if pa is None or pa.n != obs.shape[1] or pa.obs_dim != obs.shape[2]:
+            pa = self._policy_act = ppo_fused.PolicyAct(self.agent, self._flat, obs.shape[1], obs.shape[2])
+        return pa
+
     def _rollout_body(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
         T = obs.shape[0]
         obs[0].copy_(next_obs)
         dones[0].copy_(next_done)
+        fused = self._fused_policy(obs)
         for step in range(T):
-            with self._policy_ctx():
-                action, logprob, _, value = self.agent.get_action_and_value(obs[step])
-            actions[step].copy_(action)
-            logprobs[step].copy_(logprob)
-            values[step].copy_(value.flatten())
+            if fused is not None:  # one launch: forward, sample, log-prob, value into the buffers
+                action = fused(obs[step], actions[step], logprobs[step], values[step])
+            else:
+                with self._policy_ctx():
+                    action, logprob, _, value = self.agent.get_action_and_value(obs[step])
+                actions[step].copy_(action)
+                logprobs[step].copy_(logprob)
+                values[step].copy_(value.flatten())
             last = step + 1 == T
             self.envs.step_device(action,
                                   obs_out=next_obs if last else obs[step + 1],

@@ -62,3 +62,34 @@ class FusedMinibatchGrad:
         for m in range(self.n_mb):
             self.grad(m, stop, kl_at_stop)
             self.flat.step(stop=stop)
+
+
+class PolicyAct:
+    """rx_policy_act driver: one launch per rollout step instead of ~20 torch
+    launches.  The N(0, 1) noise is drawn with torch's normal_() into a
+    persistent [N, 2] buffer, exactly the draw Normal.sample() makes
+    (torch.normal(mu, std) = normal_() * std + mu), so the sampling stream is
+    unchanged; mu / value differ from the torch forward by float rounding."""
+
+    def __init__(self, agent, flat, n, obs_dim):
+        self.L = _lib.load()
+        self.agent, self.flat, self.n, self.obs_dim = agent, flat, int(n), int(obs_dim)
+        self.eps = torch.empty((self.n, 2), dtype=torch.float32, device=flat.flat_param.device)
+
+    def __call__(self, obs, actions_out, logprobs_out, values_out, stream=None):
+        for t, shape in ((obs, (self.n, self.obs_dim)), (actions_out, (self.n, 2)), (logprobs_out, (self.n,)),
+                         (values_out, (self.n,))):
+            if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"rx_policy_act: expected contiguous float32 {shape}, got {tuple(t.shape)}")
+        self.eps.normal_()
+        io = _lib.RxPolicyIO(self.obs_dim, self.n, _lib.ptr(obs), _lib.ptr(self.eps), _lib.ptr(self.flat.flat_param),
+                             _lib.ptr(self.agent.log_std), _lib.ptr(actions_out), _lib.ptr(logprobs_out),
+                             _lib.ptr(values_out))
+        _lib.check(self.L.rx_policy_act(io, _lib.stream_ptr(stream)), "rx_policy_act")
+        return actions_out
+
+
+def policy_supported(agent, obs_dim):
+    if obs_dim not in (15, 19):
+        return False
+    return sum(p.numel() for p in agent.parameters()) == _lib.load().rx_ppo_n_params(obs_dim)

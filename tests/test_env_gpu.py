@@ -271,14 +271,15 @@ def test_numpy_surface(rx, golden):
     v.close()
 
 
-@pytest.mark.parametrize("chunk,sort", [(16, 1), (8, 3), (32, 0)])
-def test_culling_and_sort_are_exact(rx, golden, chunk, sort):
-    """Chunk culling + spatial re-sorting change scheduling only: outputs are
-    bit-identical to the brute-force raycast over 300 steps of random play."""
+@pytest.mark.parametrize("chunk,sort,order", [(16, 1, 0), (8, 3, 0), (32, 0, 0), (16, 4, 1), (16, 0, 1)])
+def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order):
+    """Chunk culling, spatial re-sorting and the ray-major lane order change
+    scheduling only: outputs are bit-identical to the brute-force raycast over
+    300 steps of random play."""
     N = 1536
     tracks = np.arange(N) % golden.n_tracks
     vb = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=0, sort_interval=0)
-    vc = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=chunk, sort_interval=sort)
+    vc = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=chunk, sort_interval=sort, ray_order=order)
     assert torch.equal(vb.reset_device(), vc.reset_device())
     g = torch.Generator(device="cuda").manual_seed(5)
     for t in range(300):
@@ -331,3 +332,18 @@ def test_vector_env_from_table_file(tmp_path):
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
     a.close()
     b.close()
+
+
+def test_ray_major_two_car_is_exact(rx, golden):
+    """Ray-major lane order for the two-car kernel (agent, ray) x envs."""
+    N = 512
+    tracks = np.arange(N) % golden.n_tracks
+    va = _venv(rx, golden, tracks, n_agents=2, seed=3)
+    vb = _venv(rx, golden, tracks, n_agents=2, seed=3, sort_interval=2, ray_order=1)
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(8)
+    for t in range(200):
+        a = torch.rand((N, 2, 2), device="cuda", generator=g) * 2 - 1
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t

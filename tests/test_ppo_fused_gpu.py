@@ -122,3 +122,52 @@ def test_fused_update_early_stop_and_full_run(capsys):
     c = t2.config
     assert float(t2._flat.step_t) == c["update_epochs"] * (c["batch_size"] // c["minibatch_size"])
     assert not torch.equal(t2._flat.flat_param, before)
+
+
+@pytest.mark.parametrize("D,n", [(15, 16), (15, 4100), (19, 300)])
+def test_policy_act_matches_torch(D, n):
+    """rx_policy_act == get_action_and_value (agent/ppo.py:48-59) on the same N(0,1)
+    draw: actions / log-probs / values within float rounding."""
+    from rx.agent import Agent
+    from rx.optim import FlatAdam
+    from rx.ppo_fused import PolicyAct
+    from rx.spaces import Box
+    torch.manual_seed(2)
+    ag = Agent(Box(-1, 1, (D,)), Box(-1, 1, (2,))).cuda()
+    ag.log_std.fill_(-0.6)
+    with torch.no_grad():
+        ag.actor_mu[4].weight.mul_(80.0)  # mu spread over (-1, 1), some clamped samples
+    ref = copy.deepcopy(ag)
+    fl = FlatAdam(ag, torch.optim.Adam(ag.parameters(), lr=1e-3, eps=1e-5), 0.5)
+    pa = PolicyAct(ag, fl, n, D)
+    obs = torch.rand(n, D, device="cuda") * 2 - 1
+    act = torch.empty(n, 2, device="cuda")
+    lp = torch.empty(n, device="cuda")
+    val = torch.empty(n, device="cuda")
+    torch.manual_seed(77)
+    pa(obs, act, lp, val)
+    torch.manual_seed(77)
+    with torch.no_grad():
+        a_ref, lp_ref, _, v_ref = ref.get_action_and_value(obs)
+    assert (a_ref.abs() == 1.0).any()  # the clamp is exercised
+    torch.testing.assert_close(act, a_ref, rtol=0, atol=2e-6)
+    torch.testing.assert_close(lp, lp_ref, rtol=1e-5, atol=5e-5)
+    torch.testing.assert_close(val, v_ref.flatten(), rtol=1e-5, atol=1e-5)
+
+
+def test_fused_policy_rollout_runs_and_differs_only_by_rounding():
+    """A fused-policy rollout step == the torch-policy step on the same state and noise
+    (first step only: later steps may diverge chaotically through crash thresholds)."""
+    from tests.test_ppo_gpu import _train_single_style
+    ta, c = _train_single_style(num_envs=64, num_steps=1)
+    tb, _ = _train_single_style(num_envs=64, num_steps=1, fused_policy=False)
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    outs = []
+    for t in (ta, tb):
+        bufs = t._buffers()
+        nobs = t.envs.buf["obs"].clone()
+        nd = torch.zeros(64, device="cuda")
+        torch.manual_seed(3)
+        outs.append(t.collect_rollout(*bufs, nobs, nd))
+    for x, y in zip(outs[0][:6], outs[1][:6]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=5e-5)

@@ -44,7 +44,7 @@ def test_train_single_dropin_runs(tmp_path):
 def test_collect_rollout_equals_reference_loop():
     """The zero-copy rollout (env writes into obs[t+1]/rewards[t]/dones[t+1])
     produces exactly the buffers of the reference's copy-per-step loop."""
-    t1, c = _train_single_style(num_envs=64, num_steps=24)
+    t1, c = _train_single_style(num_envs=64, num_steps=24, fused_policy=False)
     t2, _ = _train_single_style(num_envs=64, num_steps=24)
     t2.agent.load_state_dict(t1.agent.state_dict())
     bufs1 = t1._buffers()

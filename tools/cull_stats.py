@@ -16,8 +16,8 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     pool, widths = seed1_pool(N)
     out = {}
-    for sort in (0, 1):
-        env = RacingVectorEnv(pool, widths, device="cuda", sort_interval=sort)
+    for order, sort in ((0, 0), (0, 1), (1, 0), (1, 16)):
+        env = RacingVectorEnv(pool, widths, device="cuda", sort_interval=sort, ray_order=order)
         env.reset_device()
         g = torch.Generator(device="cuda").manual_seed(0)
         for _ in range(30):
@@ -33,7 +33,7 @@ def main():
         c = env.read_counters()
         ray_waves = N * 11 / 64 * steps
         dyn_waves = N / 64 * steps
-        out[f"sort{sort}"] = {"ray_chunks_tested_per_wave": c["ray_chunk_tests"] / ray_waves,
+        out[f"order{order}_sort{sort}"] = {"ray_chunks_tested_per_wave": c["ray_chunk_tests"] / ray_waves,
                               "ray_chunks_scanned_per_wave": c["ray_chunks_scanned"] / ray_waves,
                               "wp_chunks_tested_per_wave": c["wp_chunk_tests"] / dyn_waves,
                               "wp_chunks_scanned_per_wave": c["wp_chunks_scanned"] / dyn_waves}
