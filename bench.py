@@ -109,9 +109,10 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--cull-chunk", type=int, default=16, help="raycast chunk culling (0 = brute force)")
+    ap.add_argument("--cull-chunk", type=int, default=12, help="raycast chunk culling (0 = brute force)")
     ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
     ap.add_argument("--ray-order", type=int, default=1, help="raycast lane order (0 env-major, 1 ray-major)")
+    ap.add_argument("--cull-super", type=int, default=6, help="chunks per super-chunk box (0 = one-level culling)")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -143,7 +144,8 @@ def main():
     pool, widths = seed1_pool(n_total)
     lo, hi = rank * E, (rank + 1) * E
     env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step",
-                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval, ray_order=args.ray_order)
+                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval, ray_order=args.ray_order,
+                          cull_super=args.cull_super)
     n_slots = len(env.tracks)
     S_of_env = 2 * np.diff(env.tracks.arrays()["wp_off"])[env.track_of_env]
     ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))
@@ -225,7 +227,7 @@ def main():
                                    "11 sensors, uniform random device actions, next-step autoreset)",
                        "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
-                       "ray_order": args.ray_order,
+                       "ray_order": args.ray_order, "cull_super": args.cull_super,
                        "kernel_timing": f"HIP events around k_dyn1 / k_rays on every {args.sample_every}th timed step",
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),

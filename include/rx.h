@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 5
+#define RX_ABI_VERSION 6
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -81,6 +81,7 @@ typedef struct {
                               1 = ray-major: one (agent, ray) of 64 consecutive envs per wave -- with
                               sort_interval > 0 those envs are track neighbours, so a wave's rays are
                               nearly parallel and share culling chunks.  Scheduling only: same results. */
+  int32_t cull_super;      /* two-level raycast culling: chunks per super-chunk box (0 = one level) */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are

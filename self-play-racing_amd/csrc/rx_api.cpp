@@ -77,6 +77,8 @@ struct rx_env {
   DevBuf<int32_t> chunk_off;
   DevBuf<double> chunk_box, slot_geo, wchunk_box;
   DevBuf<int32_t> wchunk_off;
+  DevBuf<int32_t> super_off;  // two-level culling: super-chunk boxes per slot
+  DevBuf<double> super_box;
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
@@ -106,8 +108,9 @@ namespace {
 int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* seg) {
   const int G = h->cfg.cull_chunk;
   if (G <= 0) return RX_OK;
-  std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0);
-  std::vector<double> boxes, wboxes, geo(4 * (size_t)n_tracks);
+  const int SG = h->cfg.cull_super;  // leaves per super-chunk (0 = one level)
+  std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0), soff(n_tracks + 1, 0);
+  std::vector<double> boxes, wboxes, sboxes, geo(4 * (size_t)n_tracks);
   for (int k = 0; k < n_tracks; ++k) {
     const int W = wp_off[k + 1] - wp_off[k];
     const int nch = (W + G - 1) / G;
@@ -148,6 +151,23 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
       }
     }
     off[k + 1] = off[k] + 2 * nch;
+    if (SG > 0) {  // super-chunk boxes: union of SG consecutive leaf boxes, per side
+      const int nsup = (nch + SG - 1) / SG;
+      const double* lb = boxes.data() + 4 * (size_t)off[k];
+      for (int side = 0; side < 2; ++side)
+        for (int u = 0; u < nsup; ++u) {
+          double bx0 = 1e300, by0 = 1e300, bx1 = -1e300, by1 = -1e300;
+          for (int c = u * SG; c < std::min(nch, (u + 1) * SG); ++c) {
+            const double* b = lb + 4 * (side * nch + c);
+            bx0 = std::min(bx0, b[0]);
+            by0 = std::min(by0, b[1]);
+            bx1 = std::max(bx1, b[2]);
+            by1 = std::max(by1, b[3]);
+          }
+          sboxes.insert(sboxes.end(), {bx0, by0, bx1, by1});
+        }
+      soff[k + 1] = soff[k] + 2 * nsup;
+    }
     // waypoint chunks (argmin culling): RX_WP_CHUNK consecutive waypoints each
     const double* w = wp + 2 * (size_t)wp_off[k];
     const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
@@ -169,6 +189,10 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
   if ((rc = upload(h->slot_geo, geo.data(), geo.size()))) return rc;
   if ((rc = upload(h->wchunk_off, woff.data(), woff.size()))) return rc;
   if ((rc = upload(h->wchunk_box, wboxes.data(), wboxes.size()))) return rc;
+  if (SG > 0) {
+    if ((rc = upload(h->super_off, soff.data(), soff.size()))) return rc;
+    if ((rc = upload(h->super_box, sboxes.data(), sboxes.size()))) return rc;
+  }
   return RX_OK;
 }
 }  // namespace
@@ -186,6 +210,7 @@ int rx_create(const rx_config* cfg, rx_env** out) {
   if (cfg->n_sensors <= 0 || cfg->n_sensors > 256) return fail(RX_EINVAL, "n_sensors out of range (%d)", cfg->n_sensors);
   if (cfg->max_steps <= 0) return fail(RX_EINVAL, "max_steps must be > 0");
   if (cfg->ray_order != 0 && cfg->ray_order != 1) return fail(RX_EINVAL, "ray_order must be 0 or 1 (got %d)", cfg->ray_order);
+  if (cfg->cull_super < 0 || cfg->cull_super > 64) return fail(RX_EINVAL, "cull_super out of range (%d)", cfg->cull_super);
   if (cfg->autoreset < RX_AUTORESET_NEXT_STEP || cfg->autoreset > RX_AUTORESET_DISABLED)
     return fail(RX_EINVAL, "bad autoreset mode %d", cfg->autoreset);
   if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
@@ -293,7 +318,8 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     int g1 = g0;
     while (g1 < N && track_of_env[perm[g1]] == k) ++g1;
     const int ng = g1 - g0;
-    for (int s = 0; s < ng; s += 64) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(64, ng - s)});
+    const int epw = A == 1 ? 64 / RX_DYN1_LPE : 64;  // envs per dynamics wave
+    for (int s = 0; s < ng; s += epw) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(epw, ng - s)});
     const long long tasks = (long long)ng * A * R;
     for (long long s = 0; s < tasks; s += 64)
       ray.push_back(rx_wave{k, g0, (int32_t)s, (int32_t)std::min<long long>(64, tasks - s)});
@@ -363,8 +389,9 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (!io->obs) return fail(RX_EINVAL, "io->obs is required");
   if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
   rx_kargs a{};
-  a.tr = rx_track_view{h->wp_off.p, h->wp.p, h->nrm.p, h->seg.p, h->meta.p,
-                       h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p};
+  a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
+                       h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
+                       h->super_off.p, h->super_box.p};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;
@@ -380,6 +407,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.autoreset = h->cfg.autoreset;
   a.mode = mode;
   a.cull_chunk = h->chunk_box.p ? h->cfg.cull_chunk : 0;
+  a.cull_super = h->super_box.p ? h->cfg.cull_super : 0;
   a.speed_weight = h->cfg.speed_weight;
   a.seed = h->cfg.seed;
   a.reset_count = h->resets.p;

@@ -33,9 +33,15 @@ struct rx_track_view {
   // closest-waypoint culling: chunks of RX_WP_CHUNK consecutive waypoints
   const int32_t* wchunk_off; // [n+1]
   const double* wchunk_box;  // [n_wchunks][4]
+  // two-level raycast culling: super-chunks of cull_super consecutive chunks
+  const int32_t* super_off;  // [n+1] first super-chunk of each slot (both sides)
+  const double* super_box;   // [n_super][4] union of the member chunk boxes
 };
 
 #define RX_WP_CHUNK 32
+
+// lanes per env in k_dyn1 (dynamics wave = 64 / RX_DYN1_LPE envs)
+#define RX_DYN1_LPE 1
 
 struct rx_kargs {
   rx_track_view tr;
@@ -57,6 +63,7 @@ struct rx_kargs {
   int32_t mode;
   int32_t cull_chunk;         // segments per culling chunk G (0 = brute force over all segments)
   int32_t ray_order;          // rx_config.ray_order
+  int32_t cull_super;         // leaves per super-chunk (0 = one-level culling)
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;

@@ -153,8 +153,20 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     if (__any(need)) {
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
-      for (int i = c * RX_WP_CHUNK; i < i1; ++i) {
-        const double2 w = wp[i];  // uniform -> s_load
+      int i = c * RX_WP_CHUNK;
+      for (; i + 4 <= i1; i += 4) {  // four waypoints per batch of scalar loads
+        const double2 w[4] = {wp[i], wp[i + 1], wp[i + 2], wp[i + 3]};  // uniform -> s_load
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            const double dx = w[u].x - px[p], dy = w[u].y - py[p];
+            argmin_take(dx * dx + dy * dy, i + u, best[p], idx[p]);
+          }
+        }
+      }
+      for (; i < i1; ++i) {
+        const double2 w = wp[i];
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const double dx = w.x - px[p], dy = w.y - py[p];
@@ -235,13 +247,25 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 // ============================================================ k_dyn, A == 1
-// RacingEnv.step / reset (environment/racing_env.py:86-167) for one env per
-// lane, plus RecordEpisodeStatistics and SyncVectorEnv autoreset.
+// RacingEnv.step / reset (environment/racing_env.py:86-167), plus
+// RecordEpisodeStatistics and SyncVectorEnv autoreset.  RX_DYN1_LPE lanes per
+// env: every lane of an env evaluates the (cheap) dynamics, the five argmins
+// (centre + 4 corners) are split over the lanes, the progress index and the
+// crash flag are combined with lane shuffles, and lane 0 of the env does the
+// rest.  4x the waves of one-env-per-lane: the argmin's scalar-load chains are
+// latency-bound, and more waves per SIMD hide them.
+__device__ __forceinline__ double pick5(const double v[5], int P) {
+  return P == 0 ? v[0] : P == 1 ? v[1] : P == 2 ? v[2] : P == 3 ? v[3] : v[4];
+}
+
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
+  constexpr int LPE = RX_DYN1_LPE;
+  constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
-  const int lane = threadIdx.x & 63;
+  const int lane = (threadIdx.x & 63) / LPE;  // env slot in the wave
+  const int sub = threadIdx.x & (LPE - 1);
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
   const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
@@ -280,22 +304,38 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
     if (moving) car_kinematics(c, steering, throttle, cs, cx, cy);
   }
   if (moving) {
-    double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
-    double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
-    int idx[5];
+    const double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
+    const double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
+    // this lane's points: P = sub + LPE*j (point 0 = centre, 1..4 = corners);
+    // slots past point 4 repeat the lane's first point and are ignored
+    double qx[NPL], qy[NPL];
+    int idx[NPL];
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) {
+      const int P = sub + LPE * j < 5 ? sub + LPE * j : sub;
+      qx[j] = pick5(px, P);
+      qy[j] = pick5(py, P);
+    }
     if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
-      argmin_culled<5, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, px, py, prev, idx,
-                          a.io.counters);
+      argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, qx, qy, prev, idx,
+                            a.io.counters);
     } else {
-      argmin_pts<5>(wp, W, px, py, idx);
+      argmin_pts<NPL>(wp, W, qx, qy, idx);
     }
-    c.progress = (double)idx[0] / (double)W;  // track.py:159-161
-    bool out = false;
+    int out = 0;  // Track.check_collision: any corner outside (track.py:163-171)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out = out || corner_out(wp, nrm, idx[q + 1], cx[q], cy[q], width);
-    c.crashed = out;
+    for (int j = 0; j < NPL; ++j) {
+      const int P = sub + LPE * j;
+      if (P >= 1 && P < 5) out |= corner_out(wp, nrm, idx[j], qx[j], qy[j], width) ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 1; o < LPE; o <<= 1) out |= __shfl_xor(out, o, 64);
+    const int i0 = __shfl(idx[0], (int)(threadIdx.x & 63) - sub, 64);  // centre argmin lives on sub 0
+    c.progress = (double)i0 / (double)W;  // track.py:159-161
+    c.crashed = out != 0;
   }
+  if (sub != 0) return;  // one lane per env from here on
   if (stepping) {
     steps += 1;
     const double last_progress = S.last_progress[e];
@@ -738,25 +778,36 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
 //   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
 // (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
 // range its rounding cannot cross the threshold).  Only hit segments divide.
+__device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, double v3x, double v3y, double& best) {
+  const double v1x = ox - g.x, v1y = oy - g.y;
+  const double dotp = g.z * v3x + g.w * v3y;
+  const double cross = g.z * v1y - g.w * v1x;
+  const double dot = v1x * v3x + v1y * v3y;
+  const double D = __builtin_fabs(dotp);
+  const bool neg = dotp < 0.0;
+  const double C = neg ? -cross : cross;
+  const double N = neg ? -dot : dot;
+  const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
+  if (hit) {
+    const double t = C / D;
+    best = t < best ? t : best;
+  }
+}
+
+// Segments [j0, j1) of a wave-uniform slot, four scalar loads in flight at a
+// time (each test ends in a divergent branch, so a plain loop would wait for
+// every s_load on its own).
 __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
                                              double v3x, double v3y, double& best) {
-#pragma unroll 4
-  for (int j = j0; j < j1; ++j) {
-    const double4 g = seg[j];  // wave-uniform -> s_load_dwordx8
-    const double v1x = ox - g.x, v1y = oy - g.y;
-    const double dotp = g.z * v3x + g.w * v3y;
-    const double cross = g.z * v1y - g.w * v1x;
-    const double dot = v1x * v3x + v1y * v3y;
-    const double D = __builtin_fabs(dotp);
-    const bool neg = dotp < 0.0;
-    const double C = neg ? -cross : cross;
-    const double N = neg ? -dot : dot;
-    const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
-    if (hit) {
-      const double t = C / D;
-      best = t < best ? t : best;
-    }
+  int j = j0;
+  for (; j + 4 <= j1; j += 4) {
+    const double4 g0 = seg[j], g1 = seg[j + 1], g2 = seg[j + 2], g3 = seg[j + 3];  // wave-uniform -> s_load
+    seg_test(g0, ox, oy, v3x, v3y, best);
+    seg_test(g1, ox, oy, v3x, v3y, best);
+    seg_test(g2, ox, oy, v3x, v3y, best);
+    seg_test(g3, ox, oy, v3x, v3y, best);
   }
+  for (; j < j1; ++j) seg_test(seg[j], ox, oy, v3x, v3y, best);
 }
 
 // Chunk culling (exact; derivation in DESIGN.md §3).  The 2W boundary
@@ -854,24 +905,55 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
     int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
     const int c0 = uniform(w0 / G);
-    int scanned = 0;
-    for (int s = 0; s < nch; ++s) {
-      const int off = (s + 1) >> 1;
-      int c = (s & 1) ? c0 - off : c0 + off;
-      c = c < 0 ? c + nch : (c >= nch ? c - nch : c);
+    int scanned = 0, tested = 0;
+    const int SG = a.cull_super;
+    if (SG <= 0) {
+      for (int s = 0; s < nch; ++s) {
+        const int off = (s + 1) >> 1;
+        int c = (s & 1) ? c0 - off : c0 + off;
+        c = c < 0 ? c + nch : (c >= nch ? c - nch : c);
 #pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const bool need = chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best);
-        if (__any(need)) {
-          ++scanned;
-          const int j0 = side * W + c * G;
-          const int j1 = side * W + min(W, (c + 1) * G);
-          ray_segments(seg, j0, j1, ox, oy, v3x, v3y, best);
+        for (int side = 0; side < 2; ++side) {
+          ++tested;
+          const bool need = chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best);
+          if (__any(need)) {
+            ++scanned;
+            ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best);
+          }
+        }
+      }
+    } else {
+      // two levels: a super-chunk box (union of SG chunk boxes) first; its
+      // chunks are tested only if some lane may need it.  A chunk inside a
+      // skipped super-chunk is skipped by the same bound, so the result is
+      // unchanged (exactness argument of chunk_needed applies to any box that
+      // contains the segments).
+      const int nsup = (nch + SG - 1) / SG;
+      const double* __restrict__ sboxes = a.tr.super_box + 4 * (size_t)uniform(a.tr.super_off[k]);
+      const int u0 = uniform(c0 / SG);
+      for (int s = 0; s < nsup; ++s) {
+        const int off = (s + 1) >> 1;
+        const bool back = (s & 1) != 0;
+        int u = back ? u0 - off : u0 + off;
+        u = u < 0 ? u + nsup : (u >= nsup ? u - nsup : u);
+        const int l0 = u * SG, nl = min(nch, l0 + SG) - l0;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          ++tested;
+          if (!__any(chunk_needed(sboxes + 4 * (side * nsup + u), mb, mt, ox, oy, cs, sn, idx_, idy_, best))) continue;
+          for (int q = 0; q < nl; ++q) {
+            const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
+            ++tested;
+            if (__any(chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best))) {
+              ++scanned;
+              ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best);
+            }
+          }
         }
       }
     }
     if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
-      atomicAdd(&a.io.counters[0], (unsigned long long)(2 * nch));
+      atomicAdd(&a.io.counters[0], (unsigned long long)tested);
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
   }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -36,7 +36,7 @@ class RxConfig(ctypes.Structure):
                 ("max_steps", ctypes.c_int32), ("autoreset", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double),
                 ("cull_chunk", ctypes.c_int32), ("sort_interval", ctypes.c_int32),
-                ("ray_order", ctypes.c_int32)]
+                ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)]
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",

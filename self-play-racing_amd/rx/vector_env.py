@@ -56,8 +56,8 @@ class RacingVectorEnv:
     (multi_racing_env.py:50)."""
 
     def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
-                 seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=16,
-                 sort_interval=0, ray_order=0):
+                 seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=12,
+                 sort_interval=16, ray_order=1, cull_super=6):
         self.L = _lib.load()
         self.device = torch.device(device) if device is not None else _default_device()
         if self.device.type != "cuda":
@@ -111,7 +111,7 @@ class RacingVectorEnv:
             )
             cfg = _lib.RxConfig(N, A, R, self.max_steps, _AUTORESET[autoreset], dev.index or 0, int(seed) & (2**64 - 1),
                                 float(half_cone), self.speed_weight, int(cull_chunk), int(sort_interval),
-                                int(ray_order))
+                                int(ray_order), int(cull_super))
             h = _lib._P()
             _lib.check(self.L.rx_create(cfg, h), "rx_create")
             self._h = h

@@ -271,15 +271,17 @@ def test_numpy_surface(rx, golden):
     v.close()
 
 
-@pytest.mark.parametrize("chunk,sort,order", [(16, 1, 0), (8, 3, 0), (32, 0, 0), (16, 4, 1), (16, 0, 1)])
-def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order):
+@pytest.mark.parametrize("chunk,sort,order,sup", [(16, 1, 0, 0), (8, 3, 0, 0), (32, 0, 0, 0), (16, 4, 1, 0),
+                                                  (16, 0, 1, 0), (8, 16, 1, 8), (6, 0, 0, 5), (24, 16, 1, 3)])
+def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
     """Chunk culling, spatial re-sorting and the ray-major lane order change
     scheduling only: outputs are bit-identical to the brute-force raycast over
     300 steps of random play."""
     N = 1536
     tracks = np.arange(N) % golden.n_tracks
     vb = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=0, sort_interval=0)
-    vc = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=chunk, sort_interval=sort, ray_order=order)
+    vc = _venv(rx, golden, tracks, autoreset="next_step", cull_chunk=chunk, sort_interval=sort, ray_order=order,
+              cull_super=sup)
     assert torch.equal(vb.reset_device(), vc.reset_device())
     g = torch.Generator(device="cuda").manual_seed(5)
     for t in range(300):

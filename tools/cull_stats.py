@@ -32,7 +32,7 @@ def main():
             env.step_device(a)
         c = env.read_counters()
         ray_waves = N * 11 / 64 * steps
-        dyn_waves = N / 64 * steps
+        dyn_waves = N / 64 * steps  # k_dyn1: 64 / RX_DYN1_LPE envs per wave (LPE = 1)
         out[f"order{order}_sort{sort}"] = {"ray_chunks_tested_per_wave": c["ray_chunk_tests"] / ray_waves,
                               "ray_chunks_scanned_per_wave": c["ray_chunks_scanned"] / ray_waves,
                               "wp_chunks_tested_per_wave": c["wp_chunk_tests"] / dyn_waves,
