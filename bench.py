@@ -155,9 +155,11 @@ def main():
     shift = torch.tensor([-1.0, 0.0], device=dev)
     actions = torch.empty((E, 2), device=dev)
 
-    def draw_actions():
-        torch.rand((E, 2), device=dev, out=actions)
-        actions.mul_(scale).add_(shift)
+    u = torch.empty((E, 2), device=dev)
+
+    def draw_actions():  # steer ~ U(-1, 1), throttle ~ U(0, 1): two launches
+        torch.rand((E, 2), device=dev, out=u)
+        torch.addcmul(shift, u, scale, out=actions)
 
     env.reset_device()
 

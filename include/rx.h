@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 6
+#define RX_ABI_VERSION 7
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -266,13 +266,15 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
 typedef struct rx_policy_io {
   int32_t obs_dim;        /* 15 or 19 */
   int64_t n;              /* rows */
-  const float* obs;       /* [n][D] */
+  const float* obs;       /* [n] rows of D floats, obs_stride floats apart (0 = D) */
   const float* eps;       /* [n][2] */
   const float* params;    /* flat parameters */
   const float* log_std;   /* [2] */
-  float* actions;         /* [n][2] out */
+  float* actions;         /* [n] rows of 2 floats, act_stride floats apart (0 = 2) out */
   float* logprobs;        /* [n] out */
   float* values;          /* [n] out */
+  int64_t obs_stride;     /* e.g. 2*19 for one car's rows of a two-car [n][2][19] buffer */
+  int64_t act_stride;     /* e.g. 4 for one car's actions in [n][2][2] */
 } rx_policy_io;
 int rx_policy_act(const rx_policy_io* io, void* stream);
 

@@ -79,6 +79,8 @@ struct rx_env {
   DevBuf<int32_t> wchunk_off;
   DevBuf<int32_t> super_off;  // two-level culling: super-chunk boxes per slot
   DevBuf<double> super_box;
+  DevBuf<int32_t> wsuper_off;  // two-level closest-waypoint culling
+  DevBuf<double> wsuper_box;
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
@@ -109,8 +111,8 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
   const int G = h->cfg.cull_chunk;
   if (G <= 0) return RX_OK;
   const int SG = h->cfg.cull_super;  // leaves per super-chunk (0 = one level)
-  std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0), soff(n_tracks + 1, 0);
-  std::vector<double> boxes, wboxes, sboxes, geo(4 * (size_t)n_tracks);
+  std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0), soff(n_tracks + 1, 0), wsoff(n_tracks + 1, 0);
+  std::vector<double> boxes, wboxes, sboxes, wsboxes, geo(4 * (size_t)n_tracks);
   for (int k = 0; k < n_tracks; ++k) {
     const int W = wp_off[k + 1] - wp_off[k];
     const int nch = (W + G - 1) / G;
@@ -182,6 +184,19 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
       wboxes.insert(wboxes.end(), {bx0, by0, bx1, by1});
     }
     woff[k + 1] = woff[k] + nwc;
+    const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;
+    for (int u = 0; u < nws; ++u) {
+      double bx0 = 1e300, by0 = 1e300, bx1 = -1e300, by1 = -1e300;
+      for (int c = u * RX_WP_SUPER; c < std::min(nwc, (u + 1) * RX_WP_SUPER); ++c) {
+        const double* b = wboxes.data() + 4 * ((size_t)woff[k] + c);
+        bx0 = std::min(bx0, b[0]);
+        by0 = std::min(by0, b[1]);
+        bx1 = std::max(bx1, b[2]);
+        by1 = std::max(by1, b[3]);
+      }
+      wsboxes.insert(wsboxes.end(), {bx0, by0, bx1, by1});
+    }
+    wsoff[k + 1] = wsoff[k] + nws;
   }
   int rc;
   if ((rc = upload(h->chunk_off, off.data(), off.size()))) return rc;
@@ -189,6 +204,8 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
   if ((rc = upload(h->slot_geo, geo.data(), geo.size()))) return rc;
   if ((rc = upload(h->wchunk_off, woff.data(), woff.size()))) return rc;
   if ((rc = upload(h->wchunk_box, wboxes.data(), wboxes.size()))) return rc;
+  if ((rc = upload(h->wsuper_off, wsoff.data(), wsoff.size()))) return rc;
+  if ((rc = upload(h->wsuper_box, wsboxes.data(), wsboxes.size()))) return rc;
   if (SG > 0) {
     if ((rc = upload(h->super_off, soff.data(), soff.size()))) return rc;
     if ((rc = upload(h->super_box, sboxes.data(), sboxes.size()))) return rc;
@@ -259,9 +276,13 @@ int rx_sensor_angles(const rx_env* h, double* out) {
 int rx_destroy(rx_env* h) {
   if (!h) return RX_OK;
   (void)hipSetDevice(h->cfg.device);
-  for (auto* b : {&h->wp, &h->nrm, &h->seg, &h->meta, &h->chunk_box, &h->slot_geo, &h->wchunk_box, &h->rel_angles})
+  for (auto* b : {&h->wp, &h->nrm, &h->seg, &h->meta, &h->chunk_box, &h->slot_geo, &h->wchunk_box, &h->super_box,
+                  &h->wsuper_box, &h->rel_angles})
     b->release();
-  for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->perm[0], &h->perm[1], &h->vals_in}) b->release();
+  for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->super_off, &h->wsuper_off, &h->perm[0], &h->perm[1],
+                  &h->vals_in, &h->slot_n})
+    b->release();
+  h->resets.release();
   h->dyn_waves.release();
   h->ray_waves.release();
   h->keys_in.release();
@@ -391,7 +412,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   rx_kargs a{};
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
-                       h->super_off.p, h->super_box.p};
+                       h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;
@@ -538,6 +559,9 @@ int rx_policy_act(const rx_policy_io* io, void* stream) {
   if (!io) return fail(RX_EINVAL, "rx_policy_act: io is null");
   if (io->obs_dim != 15 && io->obs_dim != 19) return fail(RX_EINVAL, "rx_policy_act: obs_dim=%d (15 or 19)", io->obs_dim);
   if (io->n <= 0) return fail(RX_EINVAL, "rx_policy_act: n=%lld", (long long)io->n);
+  if ((io->obs_stride != 0 && io->obs_stride < io->obs_dim) || (io->act_stride != 0 && io->act_stride < 2))
+    return fail(RX_EINVAL, "rx_policy_act: row strides overlap (obs %lld, act %lld)", (long long)io->obs_stride,
+                (long long)io->act_stride);
   if (!io->obs || !io->eps || !io->params || !io->log_std || !io->actions || !io->logprobs || !io->values)
     return fail(RX_EINVAL, "rx_policy_act: null buffer");
   const int rc = rx_launch_policy_act(io, (hipStream_t)stream);

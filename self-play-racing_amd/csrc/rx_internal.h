@@ -36,9 +36,13 @@ struct rx_track_view {
   // two-level raycast culling: super-chunks of cull_super consecutive chunks
   const int32_t* super_off;  // [n+1] first super-chunk of each slot (both sides)
   const double* super_box;   // [n_super][4] union of the member chunk boxes
+  // closest-waypoint super-chunks: RX_WP_SUPER consecutive waypoint chunks
+  const int32_t* wsuper_off; // [n+1]
+  const double* wsuper_box;  // [n_wsuper][4]
 };
 
-#define RX_WP_CHUNK 32
+#define RX_WP_CHUNK 8
+#define RX_WP_SUPER 4  // leaves per waypoint super-chunk
 
 // lanes per env in k_dyn1 (dynamics wave = 64 / RX_DYN1_LPE envs)
 #define RX_DYN1_LPE 1

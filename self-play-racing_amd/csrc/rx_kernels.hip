@@ -99,6 +99,25 @@ __device__ __forceinline__ void argmin_take(double d, int i, double& best, int& 
   idx = take ? i : idx;
 }
 
+// May the box [x0, y0, x1, y1] hold a waypoint at squared distance <= best[p]
+// from some point p?  The squared-distance lower bound is shrunk by 2^-46
+// relative, far beyond the few-ulp rounding of both the bound and the
+// per-waypoint distances, so "no" is safe: such a box can neither beat nor tie.
+template <int NP>
+__device__ __forceinline__ bool box_may_hold(const double* __restrict__ b, const double px[NP], const double py[NP],
+                                             const double best[NP]) {
+  const double x0 = b[0], y0 = b[1], x1 = b[2], y1 = b[3];
+  bool need = false;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const double gx = __builtin_fmax(__builtin_fmax(x0 - px[p], px[p] - x1), 0.0);
+    const double gy = __builtin_fmax(__builtin_fmax(y0 - py[p], py[p] - y1), 0.0);
+    const double lb = (gx * gx + gy * gy) * (1.0 - 0x1p-46);
+    need = need | !(lb > best[p]);
+  }
+  return need;
+}
+
 // The same argmin with culling (exact).  Phase 1: every lane scans a window
 // of 2H+1 waypoints around ITS car's previous closest waypoint (per-lane
 // gathers; the car moved <= 1.5 units, so the window nearly always holds the
@@ -109,7 +128,8 @@ __device__ __forceinline__ void argmin_take(double d, int i, double& best, int& 
 // both the bound and the per-waypoint distances, so a skipped chunk can
 // neither beat nor tie the best (ties are broken by index, argmin_take).
 template <int NP, int NC>
-__device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, const double* __restrict__ wbox, int W,
+__device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, const double* __restrict__ wbox,
+                                              const double* __restrict__ wsbox, int W,
                                               const double px[NP], const double py[NP], const int prev[NC],
                                               int idx[NP], unsigned long long* counters) {
   constexpr int PPC = NP / NC;  // points per car
@@ -133,35 +153,37 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
       }
     }
   }
+  // two levels: super-chunks of RX_WP_SUPER leaves of RX_WP_CHUNK waypoints,
+  // visited outward from the wave's first car; a leaf is scanned only if its
+  // super-chunk and then the leaf itself may hold a closer (or equally close,
+  // lower-index) waypoint for some lane and point
   const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
-  const int c0 = uniform(prev[0] / RX_WP_CHUNK);
-  int scanned = 0;
-  for (int s = 0; s < nwc; ++s) {
+  const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;
+  const int u0 = uniform(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
+  int scanned = 0, tested = 0;
+  for (int s = 0; s < nws; ++s) {
     const int off = (s + 1) >> 1;
-    int c = (s & 1) ? c0 - off : c0 + off;
-    c = c < 0 ? c + nwc : (c >= nwc ? c - nwc : c);
-    const double* b = wbox + 4 * c;
-    const double x0 = b[0], y0 = b[1], x1 = b[2], y1 = b[3];
-    bool need = false;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const double gx = __builtin_fmax(__builtin_fmax(x0 - px[p], px[p] - x1), 0.0);
-      const double gy = __builtin_fmax(__builtin_fmax(y0 - py[p], py[p] - y1), 0.0);
-      const double lb = (gx * gx + gy * gy) * (1.0 - 0x1p-46);
-      need = need | !(lb > best[p]);
-    }
-    if (__any(need)) {
+    const bool back = (s & 1) != 0;
+    int u = back ? u0 - off : u0 + off;
+    u = u < 0 ? u + nws : (u >= nws ? u - nws : u);
+    ++tested;
+    if (!__any(box_may_hold<NP>(wsbox + 4 * u, px, py, best))) continue;
+    const int l0 = u * RX_WP_SUPER, nl = min(nwc, l0 + RX_WP_SUPER) - l0;
+    for (int q = 0; q < nl; ++q) {
+      const int c = l0 + (back ? nl - 1 - q : q);
+      ++tested;
+      if (!__any(box_may_hold<NP>(wbox + 4 * c, px, py, best))) continue;
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
       int i = c * RX_WP_CHUNK;
       for (; i + 4 <= i1; i += 4) {  // four waypoints per batch of scalar loads
         const double2 w[4] = {wp[i], wp[i + 1], wp[i + 2], wp[i + 3]};  // uniform -> s_load
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int v = 0; v < 4; ++v) {
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            const double dx = w[u].x - px[p], dy = w[u].y - py[p];
-            argmin_take(dx * dx + dy * dy, i + u, best[p], idx[p]);
+            const double dx = w[v].x - px[p], dy = w[v].y - py[p];
+            argmin_take(dx * dx + dy * dy, i + v, best[p], idx[p]);
           }
         }
       }
@@ -176,7 +198,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     }
   }
   if (counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
-    atomicAdd(&counters[2], (unsigned long long)nwc);
+    atomicAdd(&counters[2], (unsigned long long)tested);
     atomicAdd(&counters[3], (unsigned long long)scanned);
   }
 }
@@ -318,7 +340,8 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
     }
     if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
-      argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, qx, qy, prev, idx,
+      argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
+                            a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, qx, qy, prev, idx,
                             a.io.counters);
     } else {
       argmin_pts<NPL>(wp, W, qx, qy, idx);
@@ -591,7 +614,8 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
       int idx[10];
       if (a.cull_chunk > 0) {
         const int prev[2] = {prev_waypoint(c[0].progress, W), prev_waypoint(c[1].progress, W)};
-        argmin_culled<10, 2>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]), W, px, py, prev, idx,
+        argmin_culled<10, 2>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
+                             a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, idx,
                              a.io.counters);
       } else {
         argmin_pts<10>(wp, W, px, py, idx);

@@ -296,9 +296,10 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
   const int64_t base = (int64_t)blockIdx.x * kRP;
   const int64_t row = base + lane;
   const bool live = row < io.n;
+  const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
   for (int e = t; e < kRP * D; e += kT) {
     const int r = e / D, d = e - r * D;
-    sX[r * XS + d] = base + r < io.n ? io.obs[(base + r) * D + d] : 0.0f;
+    sX[r * XS + d] = base + r < io.n ? io.obs[(base + r) * os + d] : 0.0f;
   }
   __syncthreads();
   float mu[kNA];
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
       const float var = scale * scale;
       const float smp = io.eps[row * kNA + j] * scale + mu[j];  // mul_(std).add_(mu): two roundings
       const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
-      io.actions[row * kNA + j] = a;
+      io.actions[row * as + j] = a;
       logp += normal_logp(a - mu[j], var, logf(scale));
     }
     io.logprobs[row] = logp;

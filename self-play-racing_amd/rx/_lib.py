@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -69,7 +69,8 @@ class RxPPOBatch(ctypes.Structure):
 
 class RxPolicyIO(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("n", ctypes.c_int64)] + \
-               [(k, _P) for k in ("obs", "eps", "params", "log_std", "actions", "logprobs", "values")]
+               [(k, _P) for k in ("obs", "eps", "params", "log_std", "actions", "logprobs", "values")] + \
+               [("obs_stride", ctypes.c_int64), ("act_stride", ctypes.c_int64)]
 
 
 class RxError(RuntimeError):
@@ -141,6 +142,11 @@ def ptr(t):
         assert t.is_contiguous(), "tensors handed to librx must be contiguous"
         return _P(t.data_ptr())
     return _P(t.ctypes.data)
+
+
+def view_ptr(t):
+    """Pointer of a strided view whose row stride the caller passes explicitly."""
+    return _P(t.data_ptr())
 
 
 def stream_ptr(stream=None):

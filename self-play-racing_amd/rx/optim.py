@@ -24,6 +24,26 @@ import torch
 from . import _lib
 
 
+class FlatParams:
+    """A module's float32 parameters moved into ONE contiguous buffer (``p.data``
+    become views; names, state_dict and load_state_dict are unchanged).  What
+    rx_policy_act needs for a module that is never optimised (the frozen
+    self-play opponent)."""
+
+    def __init__(self, module):
+        params = [p for p in module.parameters()]
+        if not params or any(p.dtype != torch.float32 for p in params):
+            raise ValueError("FlatParams expects float32 parameters")
+        self.flat_param = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=params[0].device)
+        o = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                self.flat_param[o:o + k].copy_(p.reshape(-1))
+                p.data = self.flat_param[o:o + k].view_as(p)
+                o += k
+
+
 class FlatAdam:
     def __init__(self, module, optimizer, max_grad_norm):
         self.module = module

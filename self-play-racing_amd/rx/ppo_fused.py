@@ -74,17 +74,31 @@ class PolicyAct:
     def __init__(self, agent, flat, n, obs_dim):
         self.L = _lib.load()
         self.agent, self.flat, self.n, self.obs_dim = agent, flat, int(n), int(obs_dim)
-        self.eps = torch.empty((self.n, 2), dtype=torch.float32, device=flat.flat_param.device)
+        dev = flat.flat_param.device
+        self.eps = torch.empty((self.n, 2), dtype=torch.float32, device=dev)
+        self._lp = torch.empty(self.n, dtype=torch.float32, device=dev)  # sinks when the caller
+        self._val = torch.empty(self.n, dtype=torch.float32, device=dev)  # wants actions only
 
-    def __call__(self, obs, actions_out, logprobs_out, values_out, stream=None):
-        for t, shape in ((obs, (self.n, self.obs_dim)), (actions_out, (self.n, 2)), (logprobs_out, (self.n,)),
-                         (values_out, (self.n,))):
-            if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous():
-                raise ValueError(f"rx_policy_act: expected contiguous float32 {shape}, got {tuple(t.shape)}")
+    @staticmethod
+    def _rows(t, n, width, name):
+        """Row stride (floats) of a float32 [n, width] view whose rows may be spaced out."""
+        if t.dtype != torch.float32 or t.dim() != 2 or tuple(t.shape) != (n, width) or t.stride(1) != 1:
+            raise ValueError(f"rx_policy_act: {name} must be a float32 [{n}, {width}] view with unit column "
+                             f"stride, got {tuple(t.shape)} / {t.stride()}")
+        return t.stride(0)
+
+    def __call__(self, obs, actions_out, logprobs_out=None, values_out=None, stream=None):
+        os_ = self._rows(obs, self.n, self.obs_dim, "obs")
+        as_ = self._rows(actions_out, self.n, 2, "actions")
+        lp = self._lp if logprobs_out is None else logprobs_out
+        val = self._val if values_out is None else values_out
+        for t in (lp, val):
+            if tuple(t.shape) != (self.n,) or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("rx_policy_act: log-prob / value outputs must be contiguous float32 [n]")
         self.eps.normal_()
-        io = _lib.RxPolicyIO(self.obs_dim, self.n, _lib.ptr(obs), _lib.ptr(self.eps), _lib.ptr(self.flat.flat_param),
-                             _lib.ptr(self.agent.log_std), _lib.ptr(actions_out), _lib.ptr(logprobs_out),
-                             _lib.ptr(values_out))
+        io = _lib.RxPolicyIO(self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(self.eps),
+                             _lib.ptr(self.flat.flat_param), _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out),
+                             _lib.ptr(lp), _lib.ptr(val), os_, as_)
         _lib.check(self.L.rx_policy_act(io, _lib.stream_ptr(stream)), "rx_policy_act")
         return actions_out
 

@@ -40,11 +40,19 @@ class SelfPlayVectorEnv:
         self.single_action_space = venv.single_action_space
         self.envs = venv.envs
         self.opponent_policy = None
+        self._opp_fused = None
         self._act = torch.zeros((self.num_envs, 2, 2), dtype=torch.float32, device=self.device)
         self.buf = {"obs": self.venv.buf["obs"][:, agent_idx]}
 
-    def set_opponent(self, policy):
+    def set_opponent(self, policy, flat=None):
+        """policy: an Agent (or None = random actions).  With ``flat`` (an
+        rx.optim.FlatParams of that policy) the opponent's forward + sampling is
+        one rx_policy_act launch reading the two-car obs buffer in place."""
+        from . import ppo_fused
         self.opponent_policy = policy
+        self._opp_fused = None
+        if policy is not None and flat is not None and ppo_fused.policy_supported(policy, self.venv.D):
+            self._opp_fused = ppo_fused.PolicyAct(policy, flat, self.num_envs, self.venv.D)
 
     def _opponent_actions(self):
         o = self._act[:, self.opp_idx]
@@ -52,6 +60,8 @@ class SelfPlayVectorEnv:
             u = torch.rand((self.num_envs, 2), device=self.device)  # default generator: graph-capturable
             u[:, 0].mul_(2.0).sub_(1.0)  # steer ~ U(-1, 1); throttle ~ U(0, 1)
             o.copy_(u)
+        elif self._opp_fused is not None:  # writes agent 1's actions straight into _act
+            self._opp_fused(self.venv.buf["obs"][:, self.opp_idx], o)
         else:
             with torch.no_grad():
                 a = self.opponent_policy.get_action_and_value(self.venv.buf["obs"][:, self.opp_idx])[0]
@@ -125,11 +135,14 @@ class SelfPlayPPO(PPO):
             self.envs.set_opponent(None)
         else:
             if getattr(self, "_opp_static", None) is None:
+                from .optim import FlatParams
                 self._opp_static = self.snapshot_agent()
+                self._opp_flat = FlatParams(self._opp_static)  # before any graph captures its addresses
             with torch.no_grad():
                 for dst, src in zip(self._opp_static.state_dict().values(), self.curr_opponent.state_dict().values()):
                     dst.copy_(src)
-            self.envs.set_opponent(self._opp_static)
+            fused = self.config.get("fused_policy", True) and self.config.get("policy_dtype", "fp32") == "fp32"
+            self.envs.set_opponent(self._opp_static, self._opp_flat if fused else None)
         self.envs.reset_device()
 
     def collect_rollout(self, *bufs):

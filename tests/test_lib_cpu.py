@@ -44,3 +44,27 @@ def test_create_without_device_fails_loudly():
     bad = _lib.RxConfig(16, 3, 11, 3000, 0, 0, 0, 1.0, 8.0)
     assert L.rx_create(bad, h) == _lib.RX_EINVAL
     assert b"n_agents" in L.rx_last_error()
+
+
+def test_update_abi_validates_without_device():
+    """The PPO-update / policy entry points check their arguments before any HIP call."""
+    import ctypes
+    from rx import _lib
+    L = _lib.load()
+    assert L.rx_ppo_n_params(15) == 10563 and L.rx_ppo_n_params(19) == 11075 and L.rx_ppo_n_params(7) == 0
+    assert L.rx_ppo_workspace_floats(15, 32768) % 64 == 0 and L.rx_ppo_workspace_doubles(32768) >= 1
+    assert L.rx_ppo_workspace_floats(3, 64) == 0
+    b = _lib.RxPPOBatch()
+    b.obs_dim, b.mb, b.n_rows = 11, 64, 128
+    assert L.rx_ppo_adv_stats(ctypes.byref(b), 2, None, None) == _lib.RX_EINVAL
+    assert b"obs_dim" in L.rx_last_error()
+    b.obs_dim = 15
+    assert L.rx_ppo_minibatch_grad(ctypes.byref(b), 0, None, None, None, None, None, None) == _lib.RX_EINVAL
+    assert b"null" in L.rx_last_error()
+    io = _lib.RxPolicyIO()
+    io.obs_dim, io.n = 15, 4
+    assert L.rx_policy_act(ctypes.byref(io), None) == _lib.RX_EINVAL
+    cfg = _lib.RxAdamConfig()
+    cfg.n_tensors = 0
+    assert L.rx_adam_clip_step(ctypes.byref(cfg), None, None, None, None, None, None, None, None) == _lib.RX_EINVAL
+    assert b"n_tensors" in L.rx_last_error()

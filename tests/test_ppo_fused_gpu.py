@@ -171,3 +171,36 @@ def test_fused_policy_rollout_runs_and_differs_only_by_rounding():
         outs.append(t.collect_rollout(*bufs, nobs, nd))
     for x, y in zip(outs[0][:6], outs[1][:6]):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=5e-5)
+
+
+def test_selfplay_fused_opponent_matches_torch_opponent():
+    """SelfPlayVectorEnv with the frozen opponent on rx_policy_act (strided two-car
+    obs read in place, actions written into the [N, 2, 2] buffer) == the torch
+    forward of the same opponent on the same N(0, 1) draw, within rounding."""
+    from rx.agent import Agent
+    from rx.optim import FlatParams
+    from rx.selfplay import SelfPlayVectorEnv
+    from rx.track import gen_tracks
+    from rx.vector_env import RacingVectorEnv
+    np.random.seed(1)
+    pool = gen_tracks(4, seed=1)
+    N = 300
+    v = RacingVectorEnv([pool[i % 4] for i in range(N)], [7] * N, n_agents=2, device="cuda")
+    sp = SelfPlayVectorEnv(v)
+    sp.reset_device()
+    torch.manual_seed(0)
+    opp = Agent(v.single_observation_space, v.single_action_space).cuda()
+    opp.log_std.fill_(-0.5)
+    with torch.no_grad():
+        opp.actor_mu[4].weight.mul_(50.0)
+    ref = copy.deepcopy(opp)
+    sp.set_opponent(opp, FlatParams(opp))
+    assert sp._opp_fused is not None
+    torch.manual_seed(9)
+    sp._opponent_actions()
+    got = sp._act[:, 1].clone()
+    torch.manual_seed(9)
+    with torch.no_grad():
+        want = ref.get_action_and_value(v.buf["obs"][:, 1])[0]
+    torch.testing.assert_close(got, want, rtol=0, atol=2e-6)
+    assert torch.equal(sp._act[:, 0], torch.zeros_like(sp._act[:, 0]))  # agent 0's slot untouched
