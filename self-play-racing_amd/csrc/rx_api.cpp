@@ -300,6 +300,8 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
   for (int k = 0; k < n_tracks; ++k) {
     const int W = wp_off[k + 1] - wp_off[k];
     if (W < 2) return fail(RX_EINVAL, "track %d has %d waypoints (need >= 2)", k, W);
+    if (W > 64 * RX_WP_CHUNK * RX_WP_SUPER)  // closest-waypoint super-chunk mask is 64 bits
+      return fail(RX_EINVAL, "track %d has %d waypoints (at most %d)", k, W, 64 * RX_WP_CHUNK * RX_WP_SUPER);
     if (!(meta[8 * k + 3] >= 0)) return fail(RX_EINVAL, "track %d width invalid", k);
     if (!(meta[8 * k + 4] > 0)) return fail(RX_EINVAL, "track %d max_track_distance must be > 0", k);
   }

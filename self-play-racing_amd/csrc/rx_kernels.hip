@@ -39,6 +39,11 @@ struct Car {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // f32 np.clip with Python-float bounds (stays float32 under NEP 50)
 __device__ __forceinline__ float clipf(float a, float lo, float hi) {
   float y = a < lo ? lo : a;
@@ -153,21 +158,27 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
       }
     }
   }
-  // two levels: super-chunks of RX_WP_SUPER leaves of RX_WP_CHUNK waypoints,
-  // visited outward from the wave's first car; a leaf is scanned only if its
-  // super-chunk and then the leaf itself may hold a closer (or equally close,
-  // lower-index) waypoint for some lane and point
+  // two levels: super-chunks of RX_WP_SUPER leaves of RX_WP_CHUNK waypoints.
+  // The super-chunk tests use the window's bests (an upper bound of the final
+  // ones, so the set is conservative) and are branch-free, so their scalar
+  // loads are all in flight together -- one latency instead of one per super.
+  // Needed super-chunks are then visited outward from the wave's first car and
+  // their leaves tested against the running bests.
   const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
-  const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;
+  const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;  // <= 64 (W <= 64 * RX_WP_CHUNK * RX_WP_SUPER)
+  unsigned long long smask = 0;
+#pragma unroll 4
+  for (int u = 0; u < nws; ++u)
+    smask |= (unsigned long long)(__any(box_may_hold<NP>(wsbox + 4 * u, px, py, best)) ? 1 : 0) << u;
+  smask = uniform64(smask);
   const int u0 = uniform(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
-  int scanned = 0, tested = 0;
+  int scanned = 0, tested = nws;
   for (int s = 0; s < nws; ++s) {
     const int off = (s + 1) >> 1;
     const bool back = (s & 1) != 0;
     int u = back ? u0 - off : u0 + off;
     u = u < 0 ? u + nws : (u >= nws ? u - nws : u);
-    ++tested;
-    if (!__any(box_may_hold<NP>(wsbox + 4 * u, px, py, best))) continue;
+    if (!((smask >> u) & 1ull)) continue;
     const int l0 = u * RX_WP_SUPER, nl = min(nwc, l0 + RX_WP_SUPER) - l0;
     for (int q = 0; q < nl; ++q) {
       const int c = l0 + (back ? nl - 1 - q : q);
