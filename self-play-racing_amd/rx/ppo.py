@@ -92,6 +92,10 @@ class PPO:
         self.optimizer = optim.Adam(self.agent.parameters(), lr=config["learning_rate"], eps=1e-5)
         # parameters move into one flat buffer here, BEFORE any graph captures their addresses
         self._flat = FlatAdam(self.agent, self.optimizer, config["max_grad_norm"])
+        # one forward now: BLAS handle / kernel-module initialisation belongs to
+        # construction, not to the first rollout (no RNG is drawn by get_value)
+        with torch.no_grad():
+            self.agent.get_value(self.envs.buf["obs"].reshape(-1, self.envs.buf["obs"].shape[-1])[:1])
         self._fresh_obs = True
 
     def _make_envs(self, env_fn):
@@ -148,11 +152,13 @@ class PPO:
     def collect_rollout(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
         """agent/ppo.py:97-132 on the device.  Buffers are [T, N_local, ...].
 
-        With config["graph_rollout"] (default on) the whole T-step rollout --
-        policy forward, sampling, env kernels -- is captured once into a HIP
-        graph and replayed every update: one launch instead of ~25 per step."""
+        With config["graph_rollout"] (default "auto": on below 2,048 envs, where
+        the per-step launches cost more than the kernels) the whole T-step
+        rollout -- noise, policy, env kernels -- is captured once into a HIP
+        graph and replayed every update."""
         with torch.no_grad():
-            if self.config.get("graph_rollout", True):
+            # capture when per-step launches would outpace the GPU work (few envs)
+            if self._want_graph("graph_rollout", self.num_local_envs < 2048):
                 key = tuple(t.data_ptr() for t in (obs, actions, logprobs, dones, rewards, values, next_obs,
                                                     next_done))
                 g = self._graphs.get(key) if hasattr(self, "_graphs") else None
@@ -243,22 +249,33 @@ class PPO:
         """agent/ppo.py:156-209; distributed-aware (rx.dist).
 
         Optimizer step = rx_adam_clip_step (clip_grad_norm_ + Adam in one HIP
-        launch on flat buffers, rx.optim).  On one GPU with
-        config["graph_update"] (default on) each epoch's 16 minibatch steps --
-        gather, forward, loss, backward, KL check, clip + Adam -- are ONE
-        captured HIP graph: the KL early stop becomes a device flag that turns
-        the remaining optimizer launches into no-ops, read by the host once per
-        epoch, so parameters, Adam state and np.random consumption end exactly
-        where the reference's immediate return leaves them."""
+        launch on flat buffers, rx.optim).  On one GPU a minibatch step is the
+        fused gradient kernel (config["fused_update"], default on) and, with
+        config["graph_update"] (default "auto": below 8,192-row minibatches),
+        each epoch's minibatch steps are ONE captured HIP graph.  The KL early
+        stop is a device flag that turns the remaining optimizer launches into
+        no-ops, read by the host once per epoch, so parameters, Adam state and
+        np.random consumption end exactly where the reference's immediate
+        return leaves them."""
         b = self._flat_batch(advantages, returns, values, logprobs, actions, obs)
         flat = getattr(self, "_flat", None)
         if flat is None:
             return self._update_torch(b)
         flat.rebind()
         flat.sync_lr()
-        if rdist.world() == 1 and self.config.get("graph_update", True):
-            return self._update_graphed(b)
+        if rdist.world() == 1:
+            from . import ppo_fused
+            mb = self._minibatch_size()
+            fused = self.config.get("fused_update", True) and ppo_fused.supported(self.agent, b, mb)
+            # capture when launches would outpace the GPU work (small minibatches)
+            capture = self._want_graph("graph_update", mb < 8192)
+            if fused or capture:
+                return self._update_epochs(b, fused, capture)
         return self._update_flat_eager(b)
+
+    def _want_graph(self, key, auto):
+        v = self.config.get(key, "auto")
+        return auto if v == "auto" else bool(v)
 
     def _update_torch(self, b):
         """Reference control flow with torch.optim (no flat buffers: CPU tests)."""
@@ -308,17 +325,15 @@ class PPO:
         loss.backward()
         self._flat.step(stop=self._stop)
 
-    def _epoch_graph(self, b, B, mb):
-        """One captured graph per (buffers, batch, minibatch, dtype, kernel): all
-        minibatch steps of an epoch over the static index tensor ``perm``.
-
-        With config["fused_update"] (default on) and the reference policy
-        layout, a minibatch step is rx_ppo_minibatch_grad + rx_adam_clip_step
-        (rx.ppo_fused: 3 launches); otherwise it is torch autograd + the flat
-        Adam launch."""
+    def _epoch_runner(self, b, B, mb, fused, capture):
+        """The work of one epoch over the static index tensor ``perm``: with
+        ``fused`` (config["fused_update"], default on, reference policy layout)
+        a minibatch step is rx_ppo_minibatch_grad + rx_adam_clip_step
+        (rx.ppo_fused: 3 launches), otherwise torch autograd + the flat Adam
+        launch; with ``capture`` the epoch is one HIP graph.  Cached per
+        (buffers, batch, minibatch, dtype, kernel, capture)."""
         from . import ppo_fused
-        fused = self.config.get("fused_update", True) and ppo_fused.supported(self.agent, b, mb)
-        key = tuple(t.data_ptr() for t in b) + (B, mb, self.config.get("policy_dtype", "fp32"), fused)
+        key = tuple(t.data_ptr() for t in b) + (B, mb, self.config.get("policy_dtype", "fp32"), fused, capture)
         graphs = self.__dict__.setdefault("_upd_graphs", {})
         if key in graphs:
             return graphs[key]
@@ -326,13 +341,19 @@ class PPO:
         ent = types.SimpleNamespace(
             perm=torch.arange(B, device=dev), perm_host=torch.empty(B, dtype=torch.int64).pin_memory(),
             stop=torch.ones(1, dtype=torch.bool, device=dev),  # a warm-up must not move anything
-            kl=torch.zeros(1, dtype=torch.float32, device=dev), graph=torch.cuda.CUDAGraph(), fused=None)
+            kl=torch.zeros(1, dtype=torch.float32, device=dev), graph=None, fused=None, run=None)
         if fused:
             ent.fused = ppo_fused.FusedMinibatchGrad(self.agent, self._flat, b, mb, ent.perm, self.config)
-            torch.cuda.synchronize(dev)
-            with torch.cuda.graph(ent.graph):
-                ent.fused.epoch(ent.stop, ent.kl)
+            if capture:
+                ent.graph = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(dev)
+                with torch.cuda.graph(ent.graph):
+                    ent.fused.epoch(ent.stop, ent.kl)
+                ent.run = ent.graph.replay
+            else:
+                ent.run = lambda: ent.fused.epoch(ent.stop, ent.kl)
         else:
+            ent.graph = torch.cuda.CUDAGraph()
             self._stop, self._kl_at_stop = ent.stop, ent.kl
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -344,13 +365,14 @@ class PPO:
             with torch.cuda.graph(ent.graph):
                 for start in range(0, B, mb):
                     self._graph_minibatch(b, ent.perm[start:start + mb])
+            ent.run = ent.graph.replay
         graphs[key] = ent
         return ent
 
-    def _update_graphed(self, b):
+    def _update_epochs(self, b, fused, capture):
         c = self.config
         B, mb = b[0].shape[0], self._minibatch_size()
-        ent = self._epoch_graph(b, B, mb)
+        ent = self._epoch_runner(b, B, mb, fused, capture)
         device_shuffle = c.get("shuffle", "numpy") == "device"
         b_inds = np.arange(B)
         nxt = None
@@ -365,7 +387,7 @@ class PPO:
                     b_inds = nxt
                 ent.perm_host.numpy()[:] = b_inds
                 ent.perm.copy_(ent.perm_host, non_blocking=True)
-            ent.graph.replay()
+            ent.run()
             rng = None
             if not device_shuffle and epoch + 1 < c["update_epochs"]:
                 # shuffle the next epoch while this one runs; undone if it stopped

@@ -204,3 +204,19 @@ def test_selfplay_fused_opponent_matches_torch_opponent():
         want = ref.get_action_and_value(v.buf["obs"][:, 1])[0]
     torch.testing.assert_close(got, want, rtol=0, atol=2e-6)
     assert torch.equal(sp._act[:, 0], torch.zeros_like(sp._act[:, 0]))  # agent 0's slot untouched
+
+
+def test_fused_update_graph_equals_eager():
+    """The fused update replayed from captured epoch graphs == the same launches issued eagerly."""
+    res = []
+    for graph in (True, False):
+        t = _trainer(graph_update=graph, kl_target=1e9)
+        data = _rollout(t)
+        np.random.seed(4)
+        for u in range(2):
+            t._anneal(u, 4)
+            t.ppo_update(*data)
+        ent = next(iter(t._upd_graphs.values()))
+        assert ent.fused is not None and (ent.graph is not None) == graph
+        res.append((t._flat.flat_param.clone(), t._flat.exp_avg_sq.clone(), float(t._flat.step_t)))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]

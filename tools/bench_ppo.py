@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--updates", type=int, default=3)
     ap.add_argument("--bf16", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager rollout (no captured rollout graph)")
+    ap.add_argument("--no-graph-update", action="store_true", help="eager fused update (no captured epoch graphs)")
+    ap.add_argument("--device-shuffle", action="store_true")
     args = ap.parse_args()
     from rx.configs import base_config, self_play_config
     from rx.envs import MultiRacingEnv, RacingEnv
@@ -37,7 +39,9 @@ def main():
     from rx.track import gen_tracks
     mk = base_config if args.mode == "single" else self_play_config
     cfg = mk(num_envs=args.envs, num_steps=args.steps, policy_dtype="bf16" if args.bf16 else "fp32",
-             graph_rollout=not args.no_graph, kl_target=1e9)  # no early stop: time the full update
+             graph_rollout=False if args.no_graph else "auto", graph_update=False if args.no_graph_update else "auto",
+             kl_target=1e9,
+             shuffle="device" if args.device_shuffle else "numpy")  # no early stop: time the full update
     cfg["total_timesteps"] = (args.updates + 1) * cfg["batch_size"]
     random.seed(1)
     np.random.seed(1)
@@ -75,6 +79,8 @@ def main():
     B = cfg["batch_size"]
     res = {"mode": args.mode, "envs": args.envs, "num_steps": args.steps, "batch": B,
            "policy_dtype": cfg["policy_dtype"], "graph_rollout": cfg["graph_rollout"],
+           "graph_update": cfg["graph_update"], "shuffle": cfg["shuffle"],
+           "first_rollout_s": rows[0][0], "first_update_only_s": rows[0][2],
            "rollout_s": float(r[:, 0].mean()), "gae_s": float(r[:, 1].mean()), "update_s": float(r[:, 2].mean()),
            "rollout_env_steps_per_s": B / float(r[:, 0].mean()),
            "train_env_steps_per_s": B / float(r.sum(axis=1).mean()),
