@@ -286,6 +286,8 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
 // stream is torch's.  Outputs go straight into the rollout buffers.
 template <int D>
 __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const float* __restrict__ W) {
+  // blockIdx.y = trunk: 0 = actor (mu -> action, log-prob), 1 = critic (value);
+  // the two trunks are independent, so they run as separate workgroups
   using L = Lay<D>;
   constexpr int XS = D + 1;
   __shared__ float sX[kRP * XS];
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
   __shared__ float sH2[kRP * kS];
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool critic = blockIdx.y != 0;
   const int64_t base = (int64_t)blockIdx.x * kRP;
   const int64_t row = base + lane;
   const bool live = row < io.n;
@@ -302,38 +305,34 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
     sX[r * XS + d] = base + r < io.n ? io.obs[(base + r) * os + d] : 0.0f;
   }
   __syncthreads();
-  float mu[kNA];
-  hidden_layers<D>(W, L::aW1, L::ab1, L::aW2, L::ab2, sX, sH1, sH2, lane, w);
-  if (w == 0) {
+  if (!critic) {
+    hidden_layers<D>(W, L::aW1, L::ab1, L::aW2, L::ab2, sX, sH1, sH2, lane, w);
+    if (w != 0 || !live) return;
     float h[kH];
 #pragma unroll
     for (int k = 0; k < kH; ++k) h[k] = sH2[lane * kS + k];
+    float logp = 0.0f;
 #pragma unroll
     for (int j = 0; j < kNA; ++j) {
       float z = 0.0f;
 #pragma unroll
       for (int k = 0; k < kH; ++k) z = fmaf(W[L::aW3 + j * kH + k], h[k], z);
-      mu[j] = tanhf(z + W[L::ab3 + j]);
+      const float mu = tanhf(z + W[L::ab3 + j]);
+      const float scale = expf(io.log_std[j]);
+      const float var = scale * scale;
+      const float smp = io.eps[row * kNA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
+      const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
+      io.actions[row * as + j] = a;
+      logp += normal_logp(a - mu, var, logf(scale));
     }
-  }
-  __syncthreads();  // sH1/sH2 are rewritten by the critic trunk
-  hidden_layers<D>(W, L::cW1, L::cb1, L::cW2, L::cb2, sX, sH1, sH2, lane, w);
-  if (w == 0 && live) {
+    io.logprobs[row] = logp;
+  } else {
+    hidden_layers<D>(W, L::cW1, L::cb1, L::cW2, L::cb2, sX, sH1, sH2, lane, w);
+    if (w != 0 || !live) return;
     float v = 0.0f;
 #pragma unroll
     for (int k = 0; k < kH; ++k) v = fmaf(W[L::cW3 + k], sH2[lane * kS + k], v);
     io.values[row] = v + W[L::cb3];
-    float logp = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kNA; ++j) {
-      const float scale = expf(io.log_std[j]);
-      const float var = scale * scale;
-      const float smp = io.eps[row * kNA + j] * scale + mu[j];  // mul_(std).add_(mu): two roundings
-      const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
-      io.actions[row * as + j] = a;
-      logp += normal_logp(a - mu[j], var, logf(scale));
-    }
-    io.logprobs[row] = logp;
   }
 }
 
@@ -466,8 +465,8 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, f
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
   const int n_wg = (int)((io->n + kRP - 1) / kRP);
   if (io->obs_dim == 15)
-    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg, 2), dim3(kT), 0, s, *io, io->params);
   else
-    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg, 2), dim3(kT), 0, s, *io, io->params);
   return (int)hipGetLastError();
 }
