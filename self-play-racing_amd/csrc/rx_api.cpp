@@ -89,6 +89,7 @@ struct rx_env {
   DevBuf<int32_t> slot_n;   // envs per slot (ray-major decode)
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
+  int32_t dyn_lpe = 1;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
@@ -333,6 +334,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   std::iota(perm.begin(), perm.end(), 0);
   std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return track_of_env[a] < track_of_env[b]; });
   std::vector<rx_wave> dyn, ray;
+  h->dyn_lpe = (A == 1 && N <= RX_DYN1_SMALL_N) ? RX_DYN1_LPE_SMALL : 1;
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
   int g0 = 0;
@@ -341,7 +343,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     int g1 = g0;
     while (g1 < N && track_of_env[perm[g1]] == k) ++g1;
     const int ng = g1 - g0;
-    const int epw = A == 1 ? 64 / RX_DYN1_LPE : 64;  // envs per dynamics wave
+    const int epw = A == 1 ? 64 / h->dyn_lpe : 64;  // envs per dynamics wave
     for (int s = 0; s < ng; s += epw) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(epw, ng - s)});
     const long long tasks = (long long)ng * A * R;
     for (long long s = 0; s < tasks; s += 64)
@@ -435,6 +437,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.seed = h->cfg.seed;
   a.reset_count = h->resets.p;
   a.ray_order = h->cfg.ray_order;
+  a.dyn_lpe = h->dyn_lpe;
   a.slot_nenv = h->slot_n.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;

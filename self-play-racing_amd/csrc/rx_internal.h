@@ -44,8 +44,11 @@ struct rx_track_view {
 #define RX_WP_CHUNK 8
 #define RX_WP_SUPER 4  // leaves per waypoint super-chunk
 
-// lanes per env in k_dyn1 (dynamics wave = 64 / RX_DYN1_LPE envs)
-#define RX_DYN1_LPE 1
+// lanes per env in k_dyn1 (a dynamics wave holds 64 / lpe envs): 4 when there
+// are few envs (latency-bound: more lanes per env shorten the chain), 1 when
+// the chip is full (issue-bound: the replicated dynamics would cost more)
+#define RX_DYN1_LPE_SMALL 4
+#define RX_DYN1_SMALL_N 8192
 
 struct rx_kargs {
   rx_track_view tr;
@@ -68,6 +71,7 @@ struct rx_kargs {
   int32_t cull_chunk;         // segments per culling chunk G (0 = brute force over all segments)
   int32_t ray_order;          // rx_config.ray_order
   int32_t cull_super;         // leaves per super-chunk (0 = one-level culling)
+  int32_t dyn_lpe;            // k_dyn1 lanes per env (1 or RX_DYN1_LPE_SMALL)
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;

@@ -19,6 +19,8 @@
 //    sin/cos = rx_sincos (correctly rounded), pow(x,2) = x*x (rx_math.h).
 //  * k_gae / k_gae_scan: agent/ppo.py:134-154 in float32.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include "rx.h"
@@ -281,7 +283,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 
 // ============================================================ k_dyn, A == 1
 // RacingEnv.step / reset (environment/racing_env.py:86-167), plus
-// RecordEpisodeStatistics and SyncVectorEnv autoreset.  RX_DYN1_LPE lanes per
+// RecordEpisodeStatistics and SyncVectorEnv autoreset.  LPE lanes per
 // env: every lane of an env evaluates the (cheap) dynamics, the five argmins
 // (centre + 4 corners) are split over the lanes, the progress index and the
 // crash flag are combined with lane shuffles, and lane 0 of the env does the
@@ -291,8 +293,8 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
   return P == 0 ? v[0] : P == 1 ? v[1] : P == 2 ? v[2] : P == 3 ? v[3] : v[4];
 }
 
+template <int LPE>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
-  constexpr int LPE = RX_DYN1_LPE;
   constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
@@ -887,7 +889,7 @@ __device__ __forceinline__ bool chunk_needed(const double* __restrict__ box, dou
 
 template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
-  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_ray_waves) return;
   const rx_wave we = a.ray_waves[wave];
   const int lane = threadIdx.x & 63;
@@ -1103,17 +1105,25 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   const dim3 blk(256);
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
-    if (n_agents == 1)
-      hipLaunchKernelGGL(k_dyn1, grd, blk, 0, s, *a);
+    if (n_agents == 1 && a->dyn_lpe == RX_DYN1_LPE_SMALL)
+      hipLaunchKernelGGL(k_dyn1<RX_DYN1_LPE_SMALL>, grd, blk, 0, s, *a);
+    else if (n_agents == 1)
+      hipLaunchKernelGGL(k_dyn1<1>, grd, blk, 0, s, *a);
     else
       hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
   }
   if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
-    const dim3 grd((a->n_ray_waves + 3) / 4);
+    // waves per workgroup for the raycast (RX_RAYS_WPB: 1, 2 or 4; A/B knob)
+    static const int wpb = [] {
+      const char* e = getenv("RX_RAYS_WPB");
+      const int v = e ? atoi(e) : 1;
+      return (v == 1 || v == 2 || v == 4) ? v : 1;
+    }();
+    const dim3 rgrd((a->n_ray_waves + wpb - 1) / wpb), rblk(64 * wpb);
     if (n_agents == 1)
-      hipLaunchKernelGGL(k_rays<1>, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL(k_rays<1>, rgrd, rblk, 0, s, *a);
     else
-      hipLaunchKernelGGL(k_rays<2>, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL(k_rays<2>, rgrd, rblk, 0, s, *a);
   }
   return (int)hipGetLastError();
 }

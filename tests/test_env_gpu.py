@@ -349,3 +349,23 @@ def test_ray_major_two_car_is_exact(rx, golden):
         oa, ra, da = va.step_device(a)
         ob, rb, db = vb.step_device(a)
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+
+
+def test_dyn_lanes_per_env_paths_agree(rx, golden):
+    """k_dyn1 runs 4 lanes per env below 8,192 envs and 1 above: envs are
+    independent, so the first envs of a large vector env must step exactly
+    like a small one with the same tracks and actions."""
+    n_small, n_big = 1024, 8256
+    tracks = np.arange(n_big) % golden.n_tracks
+    big = _venv(rx, golden, tracks, autoreset="next_step")
+    small = _venv(rx, golden, tracks[:n_small], autoreset="next_step")
+    assert torch.equal(big.reset_device()[:n_small], small.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(21)
+    for t in range(150):
+        a = torch.rand((n_big, 2), device="cuda", generator=g) * torch.tensor([2.0, 1.0], device="cuda") - torch.tensor(
+            [1.0, 0.0], device="cuda")
+        ob, rb, db = big.step_device(a)
+        os_, rs, ds = small.step_device(a[:n_small].contiguous())
+        assert torch.equal(ob[:n_small], os_) and torch.equal(rb[:n_small], rs) and torch.equal(db[:n_small], ds), t
+    big.close()
+    small.close()
