@@ -1,4 +1,4 @@
-"""Batched evaluation -- evaluate.py:12-66,173-238 and utils/metrics.py:39-78.
+"""Batched evaluation -- evaluate.py:12-122,173-238 and utils/metrics.py:39-142.
 
 The reference evaluates a policy on 40 tracks (gen_tracks(40, seed=42)) x 5
 runs, run r using width RandomState(42+r).randint(4, 10) (note: indexed by
@@ -105,8 +105,100 @@ class Evaluator:
             "avg_speed": float(speed[ok].mean()) if ok.any() else 0,
             "avg_distance": float(total_dist[ok].mean()) if ok.any() else 0,
             "avg_steps_per_progress": float((steps[eff] / prog[eff]).mean()) if eff.any() else float("nan"),
+            "all_episodes": _episodes(total_reward, steps, prog, fin, crash, speed, total_dist),
         }
         return res
+
+    def close(self):
+        self.venv.close()
+
+
+def _episodes(total_reward, steps, prog, fin, crash, speed, dist, placement=None):
+    """Per-episode dicts (utils/metrics.py:70-78 / 131-141 keys), evaluate.py's 'all_episodes'."""
+    out = []
+    for i in range(len(steps)):
+        n = int(steps[i])
+        m = {"total_reward": float(total_reward[i]), "steps": n, "progress": float(prog[i]),
+             "finished": bool(fin[i]), "crashed": bool(crash[i]), "speed": float(speed[i]),
+             "total_distance": float(dist[i]), "distance_per_step": float(dist[i]) / n if n > 1 else 0.0}
+        if placement is not None:
+            m["placement"] = int(placement[i]) if placement[i] > 0 else None
+        out.append(m)
+    return out
+
+
+class MultiEvaluator:
+    """evaluate.py:68-122 + utils/metrics.py:80-142 (self-play model): every
+    two-car episode of the protocol at once, BOTH cars driven by the evaluated
+    policy (one batched forward over the 2N car observations per step), at
+    most 3,000 steps, stopping at dones['__all__'].  The reported agent is car
+    0 unless only car 1 finished (metrics.py:124-131)."""
+
+    def __init__(self, num_tracks=40, num_runs=5, seed=42, global_seed=0, max_steps=3000, device=None,
+                 n_sensors=11, env_seed=0):
+        from .vector_env import RacingVectorEnv
+        cps, ws, self.ids = eval_pool(num_tracks, num_runs, seed, global_seed)
+        self.max_steps = max_steps
+        self.venv = RacingVectorEnv(cps, ws, n_agents=2, n_sensors=n_sensors, device=device, autoreset="disabled",
+                                    seed=env_seed)
+        self.device = self.venv.device
+
+    @torch.no_grad()
+    def run(self, agent):
+        v = self.venv
+        N, D = v.num_envs, v.D
+        dev = self.device
+        obs = v.reset_device()
+        active = torch.ones(N, dtype=torch.bool, device=dev)
+        total_reward = torch.zeros((N, 2), dtype=torch.float64, device=dev)
+        total_dist = torch.zeros((N, 2), dtype=torch.float64, device=dev)
+        steps = torch.zeros(N, dtype=torch.int64, device=dev)
+        info_last = torch.zeros((N, 2, 4), dtype=torch.float64, device=dev)
+        flags_last = torch.zeros((N, 2), dtype=torch.uint8, device=dev)
+        x, y = v.state["x"].view(N, 2), v.state["y"].view(N, 2)
+        px, py = x.clone(), y.clone()
+        first = True
+        for t in range(self.max_steps):
+            a = agent.get_action_and_value(obs.reshape(2 * N, D))[0].reshape(N, 2, 2)
+            obs, _, done = v.step_device(a, full_info=True)
+            act2 = active.unsqueeze(1)
+            total_reward += torch.where(act2, v.buf["reward64"], torch.zeros_like(total_reward))
+            if not first:
+                d = torch.sqrt((x - px) ** 2 + (y - py) ** 2)
+                total_dist += torch.where(act2, d, torch.zeros_like(d))
+            first = False
+            px.copy_(x)
+            py.copy_(y)
+            steps += active.long()
+            info_last = torch.where(act2.unsqueeze(2), v.buf["info"], info_last)
+            flags_last = torch.where(act2, v.state["flags"].view(N, 2), flags_last)
+            active &= ~done.bool()
+            if t % 50 == 49 and not bool(active.any()):
+                break
+        fin = (flags_last & 2) != 0
+        crash = (flags_last & 1) != 0
+        pick = (~fin[:, 0] & fin[:, 1]).long()  # car 1 only if it finished and car 0 did not
+        ar = torch.arange(N, device=dev)
+        g = lambda t: t[ar, pick].cpu().numpy()  # noqa: E731
+        fin_c, crash_c = g(fin), g(crash)
+        prog, speed, place = g(info_last[:, :, 1]), g(info_last[:, :, 0]), g(info_last[:, :, 3])
+        rew, dist = g(total_reward), g(total_dist)
+        steps = steps.cpu().numpy()
+        ok = fin_c
+        eff = prog > 0.01
+        return {
+            "num_episodes": int(N),
+            "num_successful": int(ok.sum()),
+            "success_rate": float(ok.mean()),
+            "crash_rate": float(crash_c.mean()),
+            "avg_steps": float(steps[ok].mean()) if ok.any() else 0,
+            "avg_reward": float(rew[ok].mean()) if ok.any() else 0,
+            "avg_progress": float(prog[ok].mean()) if ok.any() else 0,
+            "avg_speed": float(speed[ok].mean()) if ok.any() else 0,
+            "avg_distance": float(dist[ok].mean()) if ok.any() else 0,
+            "avg_steps_per_progress": float((steps[eff] / prog[eff]).mean()) if eff.any() else float("nan"),
+            "all_episodes": _episodes(rew, steps, prog, fin_c, crash_c, speed, dist, place),
+        }
 
     def close(self):
         self.venv.close()

@@ -201,3 +201,19 @@ def test_evaluator_protocol_runs():
     assert res["num_episodes"] == 200 and 0.0 <= res["success_rate"] <= 1.0
     assert res["crash_rate"] > 0.5  # an untrained policy crashes
     ev.close()
+
+
+def test_multi_evaluator_protocol_runs():
+    """evaluate_multi_agent_overall on the device: 200 two-car episodes, both cars
+    driven by the policy, reference summary keys + per-episode list."""
+    from rx.agent import Agent
+    from rx.evaluate import MultiEvaluator
+    ev = MultiEvaluator(max_steps=200, device="cuda")
+    assert ev.venv.num_envs == 200 and ev.venv.n_agents == 2
+    torch.manual_seed(0)
+    ag = Agent(ev.venv.single_observation_space, ev.venv.single_action_space).cuda()
+    res = ev.run(ag)
+    assert res["num_episodes"] == 200 and 0.0 <= res["success_rate"] <= 1.0
+    assert len(res["all_episodes"]) == 200 and "placement" in res["all_episodes"][0]
+    assert all(1 <= e["steps"] <= 200 for e in res["all_episodes"])
+    ev.close()
