@@ -7,7 +7,12 @@ Workload = BASELINE.json configs[2] ("65536 parallel single-agent envs,
 random.seed(1); np.random.seed(1); gen_tracks(N, seed=1); widths
 randint(6, 10); track_id = env index), 11 sensors, uniform random actions
 generated on the device, gymnasium next-step autoreset.  One bench "step" =
-one env step of every env (random actions + rx_step).  With N GPUs
+one env step of every env (random actions + rx_step) through ONE env handle
+on one stream -- the configuration the PPO rollout uses, and the one whose
+per-launch kernel timing the roofline is computed from.  --stream-groups G
+steps the envs as G independent groups on G HIP streams instead (as an
+asynchronous rollout would); the JSON also reports that throughput for G = 4
+as "async_stream_groups", timed after the main region.  With N GPUs
 (torch.distributed.run, one rank per GPU) every rank owns 65,536 envs of a
 N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
 
@@ -113,6 +118,11 @@ def main():
     ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
     ap.add_argument("--ray-order", type=int, default=1, help="raycast lane order (0 env-major, 1 ray-major)")
     ap.add_argument("--cull-super", type=int, default=6, help="chunks per super-chunk box (0 = one-level culling)")
+    ap.add_argument("--stream-groups", type=int, default=1,
+                    help="independent env groups, one HIP stream each (1 = one handle on one stream)")
+    ap.add_argument("--async-probe-groups", type=int, default=4,
+                    help="after the timed region, also time the same workload as this many stream groups "
+                         "(reported as 'async_stream_groups'; 0 = skip)")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -140,76 +150,108 @@ def main():
 
     from rx.vector_env import RacingVectorEnv
     E = args.envs_per_gpu
+    G = args.stream_groups
+    if G < 1 or E % G:
+        raise SystemExit(f"--stream-groups {G} must divide --envs-per-gpu {E}")
     n_total = E * world
     pool, widths = seed1_pool(n_total)
-    lo, hi = rank * E, (rank + 1) * E
-    env = RacingVectorEnv(pool[lo:hi], widths[lo:hi], n_agents=1, n_sensors=11, device=dev, autoreset="next_step",
-                          cull_chunk=args.cull_chunk, sort_interval=args.sort_interval, ray_order=args.ray_order,
-                          cull_super=args.cull_super)
-    n_slots = len(env.tracks)
-    S_of_env = 2 * np.diff(env.tracks.arrays()["wp_off"])[env.track_of_env]
-    ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))
-
-    torch.manual_seed(1234 + rank)  # default CUDA generator: graph-capturable
+    lo = rank * E
+    torch.manual_seed(1234 + rank)
     scale = torch.tensor([2.0, 1.0], device=dev)
     shift = torch.tensor([-1.0, 0.0], device=dev)
-    actions = torch.empty((E, 2), device=dev)
 
-    u = torch.empty((E, 2), device=dev)
+    def make_groups(G):
+        """G independent env groups, each stepping on its own HIP stream (a group's
+        step depends only on its own envs, so different groups' kernels overlap)."""
+        n = E // G
+        envs = [RacingVectorEnv(pool[lo + g * n:lo + (g + 1) * n], widths[lo + g * n:lo + (g + 1) * n], n_agents=1,
+                                n_sensors=11, device=dev, autoreset="next_step", cull_chunk=args.cull_chunk,
+                                sort_interval=args.sort_interval, ray_order=args.ray_order,
+                                cull_super=args.cull_super)
+                for g in range(G)]
+        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(G - 1)]
+        acts = [torch.empty((n, 2), device=dev) for _ in range(G)]
+        us = [torch.empty((n, 2), device=dev) for _ in range(G)]
+        for e in envs:
+            e.reset_device()
 
-    def draw_actions():  # steer ~ U(-1, 1), throttle ~ U(0, 1): two launches
-        torch.rand((E, 2), device=dev, out=u)
-        torch.addcmul(shift, u, scale, out=actions)
+        def one_step(ev=None):
+            for g in range(G):
+                with torch.cuda.stream(streams[g]):
+                    torch.rand((n, 2), device=dev, out=us[g])  # steer ~ U(-1, 1), throttle ~ U(0, 1)
+                    torch.addcmul(shift, us[g], scale, out=acts[g])
+                    if ev is None or g:  # the production call: one rx_step, both kernels back to back
+                        envs[g].step_device(acts[g])
+                    else:  # instrumented (group 0): the two phases around HIP events on its stream
+                        ev[0].record()
+                        envs[g].step_device(acts[g], phases=1)
+                        ev[1].record()
+                        envs[g].step_device(acts[g], phases=2)
+                        ev[2].record()
+        return envs, one_step, n
 
-    env.reset_device()
+    def timed(one_step, steps, events=None):
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            one_step(events.get(k) if events else None)
+        torch.cuda.synchronize()  # all streams
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
-    def one_step(ev=None):
-        draw_actions()
-        if ev is None:  # the production call: one rx_step, both kernels back to back
-            env.step_device(actions)
-        else:           # instrumented step: split into the two phases around HIP events
-            ev[0].record()
-            env.step_device(actions, phases=1)
-            ev[1].record()
-            env.step_device(actions, phases=2)
-            ev[2].record()
-
+    envs, one_step, n = make_groups(G)
+    env0 = envs[0]
+    n_slots = len(env0.tracks)
+    S_of_env = 2 * np.diff(env0.tracks.arrays()["wp_off"])[env0.track_of_env]
+    ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))  # one launch = group 0's envs
     for _ in range(args.warmup):
         one_step()
     # every --sample-every'th timed step is instrumented (event records between the
     # kernels cost ~10 us of GPU idle per step, so not every step carries them)
-    timed = [k for k in range(args.steps) if k % args.sample_every == 0]
-    events = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for k in timed}
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(events.get(k))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    events = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for k in range(args.steps) if k % args.sample_every == 0}
+    elapsed = timed(one_step, args.steps, events)
     dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events.values()]))
     ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events.values()]))
-    ep = env.episode_stats()
+    ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
+    for e in envs:
+        e.close()
+    async_probe = None
+    Ga = args.async_probe_groups
+    if Ga > 1 and E % Ga == 0 and Ga != G:
+        a_envs, a_step, _ = make_groups(Ga)
+        for _ in range(args.warmup):
+            a_step()
+        a_el = timed(a_step, args.steps)
+        async_probe = {"groups": Ga, "envs_per_group": E // Ga, "value": round(n_total * args.steps / a_el, 1),
+                       "ms_per_step": round(a_el / args.steps * 1e3, 4),
+                       "note": "same workload as independent env groups on separate HIP streams (async rollout); "
+                               "timed after the main region, not the headline value"}
+        for e in a_envs:
+            e.close()
     gae = gae_roofline(E, dev) if rank == 0 else None
 
     if rank == 0:
         value = n_total * args.steps / elapsed
-        achieved_gbs = RAYS_BYTES_PER_ENV * E / (ray_ms * 1e-3) / 1e9
+        achieved_gbs = RAYS_BYTES_PER_ENV * n / (ray_ms * 1e-3) / 1e9
         achieved_tf = ray_flops_per_launch / (ray_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_rays.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                pj = json.load(open(pmc))
+                # PMC bytes are per launch: only valid for launches of the same size
+                traffic = pj.get("hbm_bytes_per_launch") if pj.get("envs_per_launch") == n else None
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -228,13 +270,15 @@ def main():
             "config": {"workload": "configs[2]: 65536 single-agent racing envs per GPU (seed-1 gen_tracks pool, "
                                    "11 sensors, uniform random device actions, next-step autoreset)",
                        "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
+                       "stream_groups": G, "envs_per_launch": n,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
-                       "kernel_timing": f"HIP events around k_dyn1 / k_rays on every {args.sample_every}th timed step",
+                       "kernel_timing": f"HIP events around group 0's k_dyn1 / k_rays (on its stream) on every "
+                                        f"{args.sample_every}th timed step",
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": traffic, "bytes_per_env": RAYS_BYTES_PER_ENV,
+                         "traffic": traffic, "bytes_per_env": RAYS_BYTES_PER_ENV, "envs_per_launch": n,
                          "avg_launch_ms": round(ray_ms, 5)},
             "compute_roofline": {"bound": "valu_fp64", "kernel": "k_rays", "achieved": round(achieved_tf, 3),
                                  "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TF,
@@ -242,11 +286,11 @@ def main():
             "kernels_ms": {"k_dyn1": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
             "gae": gae,
             "episodes_ended": ep[2],
+            "async_stream_groups": async_probe,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(pool, widths, budget_s=args.cpu_budget)
         print(json.dumps(out), flush=True)
-    env.close()
     if dist:
         dist.destroy_process_group()
 
