@@ -152,13 +152,15 @@ class PPO:
     def collect_rollout(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
         """agent/ppo.py:97-132 on the device.  Buffers are [T, N_local, ...].
 
-        With config["graph_rollout"] (default "auto": on below 2,048 envs, where
-        the per-step launches cost more than the kernels) the whole T-step
-        rollout -- noise, policy, env kernels -- is captured once into a HIP
-        graph and replayed every update."""
+        With config["graph_rollout"] = True the whole T-step rollout -- noise,
+        policy, env kernels -- is captured once into a HIP graph and replayed
+        every update (default "auto" = eager: the launches of one step cost
+        less host time than their kernels' GPU time, measured down to 16 envs,
+        so a capture would only add its one-time cost)."""
         with torch.no_grad():
-            # capture when per-step launches would outpace the GPU work (few envs)
-            if self._want_graph("graph_rollout", self.num_local_envs < 2048):
+            # eager by default: with the cached per-step ctypes structs the host
+            # keeps ahead of the GPU even at 16 envs, and a capture costs ~0.2 s
+            if self._want_graph("graph_rollout", False):
                 key = tuple(t.data_ptr() for t in (obs, actions, logprobs, dones, rewards, values, next_obs,
                                                     next_done))
                 g = self._graphs.get(key) if hasattr(self, "_graphs") else None

@@ -78,6 +78,7 @@ class PolicyAct:
         self.eps = torch.empty((self.n, 2), dtype=torch.float32, device=dev)
         self._lp = torch.empty(self.n, dtype=torch.float32, device=dev)  # sinks when the caller
         self._val = torch.empty(self.n, dtype=torch.float32, device=dev)  # wants actions only
+        self._io_cache = {}
 
     @staticmethod
     def _rows(t, n, width, name):
@@ -88,17 +89,24 @@ class PolicyAct:
         return t.stride(0)
 
     def __call__(self, obs, actions_out, logprobs_out=None, values_out=None, stream=None):
-        os_ = self._rows(obs, self.n, self.obs_dim, "obs")
-        as_ = self._rows(actions_out, self.n, 2, "actions")
         lp = self._lp if logprobs_out is None else logprobs_out
         val = self._val if values_out is None else values_out
-        for t in (lp, val):
-            if tuple(t.shape) != (self.n,) or t.dtype != torch.float32 or not t.is_contiguous():
-                raise ValueError("rx_policy_act: log-prob / value outputs must be contiguous float32 [n]")
+        key = (obs.data_ptr(), actions_out.data_ptr(), lp.data_ptr(), val.data_ptr())
+        io = self._io_cache.get(key) if self._io_cache.get("shapes") == (obs.shape, obs.stride(),
+                                                                         actions_out.stride()) else None
+        if io is None:  # validate once per buffer set (a rollout reuses the same rows every update)
+            os_ = self._rows(obs, self.n, self.obs_dim, "obs")
+            as_ = self._rows(actions_out, self.n, 2, "actions")
+            for t in (lp, val):
+                if tuple(t.shape) != (self.n,) or t.dtype != torch.float32 or not t.is_contiguous():
+                    raise ValueError("rx_policy_act: log-prob / value outputs must be contiguous float32 [n]")
+            if len(self._io_cache) > 8192:
+                self._io_cache.clear()
+            self._io_cache["shapes"] = (obs.shape, obs.stride(), actions_out.stride())
+            io = self._io_cache[key] = _lib.RxPolicyIO(
+                self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(self.eps), _lib.ptr(self.flat.flat_param),
+                _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out), _lib.ptr(lp), _lib.ptr(val), os_, as_)
         self.eps.normal_()
-        io = _lib.RxPolicyIO(self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(self.eps),
-                             _lib.ptr(self.flat.flat_param), _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out),
-                             _lib.ptr(lp), _lib.ptr(val), os_, as_)
         _lib.check(self.L.rx_policy_act(io, _lib.stream_ptr(stream)), "rx_policy_act")
         return actions_out
 

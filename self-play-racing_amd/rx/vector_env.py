@@ -130,6 +130,7 @@ class RacingVectorEnv:
                                 np.tile(self.single_action_space.high, (N, 1)), shape=(N, 2), dtype=np.float32)
         self.envs = [_EnvProxy(i) for i in range(N)]
         self.counters = None
+        self._io_cache = {}
         self._episode_start = np.full(N, time.perf_counter())
         self._closed = False
 
@@ -141,6 +142,19 @@ class RacingVectorEnv:
                                            _lib.ptr(t["seg"]), _lib.ptr(t["meta"])), "rx_upload_tracks")
 
     def _io(self, actions=None, obs=None, reward=None, done=None, full=False):
+        # per-step host cost matters (a captured 2,048-step rollout runs this
+        # 2,048 times): one dict lookup when the same buffers come back
+        key = (actions.data_ptr() if actions is not None else 0, obs.data_ptr() if obs is not None else 0,
+               reward.data_ptr() if reward is not None else 0, done.data_ptr() if done is not None else 0, full,
+               self.counters is not None)
+        io = self._io_cache.get(key)
+        if io is None:
+            if len(self._io_cache) > 8192:
+                self._io_cache.clear()
+            io = self._io_cache[key] = self._make_io(actions, obs, reward, done, full)
+        return io
+
+    def _make_io(self, actions, obs, reward, done, full):
         b = self.buf
         return _lib.RxIO(
             _lib.ptr(actions) if actions is not None else None,
@@ -188,6 +202,9 @@ class RacingVectorEnv:
         A = self.n_agents
         if isinstance(actions, torch.Tensor):
             a = actions
+            if a.dtype == torch.float32 and a.is_contiguous() and a.device == self.device and \
+                    a.numel() == self.num_envs * A * 2:
+                return a  # fast path: the rollout's own action rows
             if a.device != self.device or a.dtype != torch.float32:
                 a = a.to(self.device, torch.float32)
         else:
