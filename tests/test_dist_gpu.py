@@ -1,0 +1,107 @@
+"""Data-parallel PPO update on the device path (FlatAdam + rx_adam_clip_step,
+one flat-gradient all-reduce per optimizer step), 2 ranks sharing one GPU
+over gloo (the GPU box has one device; RCCL needs one GPU per rank).  Ranks
+must stay bit-identical and match one process over the union minibatch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    from rx.configs import base_config
+    return base_config(num_envs=8, num_steps=32, num_minibatches=4, update_epochs=2, kl_target=1e9)
+
+
+def _data():
+    g = torch.Generator().manual_seed(0)
+    T, N = 32, 8
+    obs = torch.rand(T, N, 15, generator=g) * 2 - 1
+    act = torch.rand(T, N, 2, generator=g) * 2 - 1
+    logp = torch.randn(T, N, generator=g) - 2
+    adv = torch.randn(T, N, generator=g) * 5
+    ret = torch.randn(T, N, generator=g) * 10
+    val = torch.randn(T, N, generator=g) * 10
+    return obs, act, logp, adv, ret, val
+
+
+def _make_ppo(cfg):
+    from rx.agent import Agent
+    from rx.optim import FlatAdam
+    from rx.ppo import PPO
+    from rx.spaces import Box
+    p = PPO.__new__(PPO)
+    p.config = cfg
+    p.device = torch.device("cuda")
+    torch.manual_seed(3)
+    p.agent = Agent(Box(-1, 1, shape=(15,)), Box(-1, 1, shape=(2,))).cuda()
+    p.optimizer = torch.optim.Adam(p.agent.parameters(), lr=3e-4, eps=1e-5)
+    p._flat = FlatAdam(p.agent, p.optimizer, cfg["max_grad_norm"])
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as td
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = _cfg()
+        p = _make_ppo(cfg)
+        sl = slice(rank * 4, (rank + 1) * 4)
+        d = [t[:, sl].contiguous().cuda() for t in _data()]
+        obs, act, logp, adv, ret, val = d
+        np.random.seed(cfg["seed"])
+        p.ppo_update(adv, ret, val, logp, act, obs)
+        q.put((rank, p._flat.flat_param.cpu().numpy().copy(), float(p._flat.step_t)))
+    finally:
+        td.destroy_process_group()
+
+
+def test_two_rank_flat_update_in_sync():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict((r, (a, s)) for r, a, s in (q.get(timeout=300) for _ in procs))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert np.array_equal(res[0][0], res[1][0])  # ranks bit-identical
+    cfg = _cfg()
+    assert res[0][1] == cfg["update_epochs"] * cfg["num_minibatches"]
+    # single process, same minibatch schedule over the union, global normalisation
+    import rx.dist as rd
+    p = _make_ppo(cfg)
+    obs, act, logp, adv, ret, val = [t.cuda() for t in _data()]
+    B, mb = 32 * 8, cfg["minibatch_size"]
+    np.random.seed(cfg["seed"])
+    inds = np.arange(B // 2)
+    b = p._flat_batch(adv, ret, val, logp, act, obs)
+    p._flat.sync_lr()
+    for epoch in range(cfg["update_epochs"]):
+        np.random.shuffle(inds)
+        for s in range(0, B // 2, mb // 2):
+            loc = inds[s:s + mb // 2]
+            t, c = loc // 4, loc % 4
+            gi = torch.from_numpy(np.concatenate([t * 8 + c, t * 8 + 4 + c])).cuda()
+            loss, _ = p._minibatch_loss(b, gi)
+            p._flat.zero_grad()
+            loss.backward()
+            p._flat.step()
+    assert rd.world() == 1
+    np.testing.assert_allclose(res[0][0], p._flat.flat_param.cpu().numpy(), rtol=1e-4, atol=1e-5)
