@@ -345,10 +345,29 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     const int ng = g1 - g0;
     const int epw = A == 1 ? 64 / h->dyn_lpe : 64;  // envs per dynamics wave
     for (int s = 0; s < ng; s += epw) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(epw, ng - s)});
-    const long long tasks = (long long)ng * A * R;
-    for (long long s = 0; s < tasks; s += 64)
-      ray.push_back(rx_wave{k, g0, (int32_t)s, (int32_t)std::min<long long>(64, tasks - s)});
+    if (h->cfg.ray_order == 0) {
+      const long long tasks = (long long)ng * A * R;
+      for (long long s = 0; s < tasks; s += 64)
+        ray.push_back(rx_wave{k, g0, (int32_t)s, (int32_t)std::min<long long>(64, tasks - s)});
+    } else {  // ray-major: one (agent, ray) x one 64-env block per wave, grouped by block
+      for (int b = 0; 64 * b < ng; ++b)
+        for (int qr = 0; qr < A * R; ++qr)
+          ray.push_back(rx_wave{k, g0, qr * ng + 64 * b, std::min(64, ng - 64 * b)});
+    }
     g0 = g1;
+  }
+  if (h->cfg.ray_order == 1) {
+    // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs
+    // (MI355X_MICROARCH.md, workgroup dispatch), and every wave of one 64-env
+    // block writes into the same obs rows, so the A*R waves of a block go to
+    // physical indices p = ((g / 8) * A*R + qr) * 8 + g % 8 -- one XCD, one L2
+    // to merge their partial-line writes.  Padding waves have count 0.
+    const int AR = A * R;
+    const size_t n_groups = ray.size() / AR, padded = (n_groups + 7) / 8 * 8;
+    std::vector<rx_wave> placed(padded * AR, rx_wave{0, 0, 0, 0});
+    for (size_t g = 0; g < n_groups; ++g)
+      for (int qr = 0; qr < AR; ++qr) placed[((g / 8) * AR + qr) * 8 + g % 8] = ray[g * AR + qr];
+    ray.swap(placed);
   }
   RX_HIP(hipSetDevice(h->cfg.device));
   int rc;
