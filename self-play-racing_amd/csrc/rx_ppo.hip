@@ -24,6 +24,10 @@ constexpr int kT = 256;  // threads per workgroup (4 waves)
 constexpr int kRP = 64;  // rows per pass (lane = row)
 constexpr int kS = 65;   // LDS row stride of the [64][64] tiles (lane-per-row reads hit distinct banks)
 constexpr int kMaxWG = 512;  // partials per minibatch (rows per workgroup grow beyond that)
+#ifndef RX_PPO_KQ
+#define RX_PPO_KQ 4
+#endif
+constexpr int kQ = RX_PPO_KQ;  // hidden columns per weight-load group (SGPR budget vs load batching)
 
 template <int D>
 struct Lay {  // flat parameter offsets, module.parameters() order; Pp = partial row stride
@@ -54,16 +58,16 @@ __device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int o
     float x[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) x[d] = sX[lane * XS + d];
-    for (int cg = 0; cg < 4; ++cg) {
-      const int c0 = w * 16 + cg * 4;
-      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int cg = 0; cg < 16 / kQ; ++cg) {
+      const int c0 = w * 16 + cg * kQ;
+      float z[kQ] = {};
 #pragma unroll
       for (int d = 0; d < D; ++d) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
+        for (int q = 0; q < kQ; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
+      for (int q = 0; q < kQ; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
     }
   }
   __syncthreads();
@@ -71,16 +75,16 @@ __device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int o
     float h[kH];
 #pragma unroll
     for (int k = 0; k < kH; ++k) h[k] = sH1[lane * kS + k];
-    for (int cg = 0; cg < 4; ++cg) {
-      const int c0 = w * 16 + cg * 4;
-      float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int cg = 0; cg < 16 / kQ; ++cg) {
+      const int c0 = w * 16 + cg * kQ;
+      float z[kQ] = {};
 #pragma unroll
       for (int k = 0; k < kH; ++k) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
+        for (int q = 0; q < kQ; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
+      for (int q = 0; q < kQ; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
     }
   }
   __syncthreads();
@@ -240,16 +244,16 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
         float dz[kH];
 #pragma unroll
         for (int c = 0; c < kH; ++c) dz[c] = sDZ[lane * kS + c];
-        for (int kg = 0; kg < 4; ++kg) {
-          const int k0 = w * 16 + kg * 4;
-          float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int kg = 0; kg < 16 / kQ; ++kg) {
+          const int k0 = w * 16 + kg * kQ;
+          float acc[kQ] = {};
 #pragma unroll
           for (int c = 0; c < kH; ++c) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = fmaf(W[oW2 + c * kH + k0 + q], dz[c], acc[q]);
+            for (int q = 0; q < kQ; ++q) acc[q] = fmaf(W[oW2 + c * kH + k0 + q], dz[c], acc[q]);
           }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < kQ; ++q) {
             const float h1 = sH1[lane * kS + k0 + q];
             sH2[lane * kS + k0 + q] = acc[q] * (1.0f - h1 * h1);
           }
