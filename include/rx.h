@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 7
+#define RX_ABI_VERSION 8
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -197,14 +197,17 @@ int rx_gae_scan(int32_t T, int32_t N, const float* rewards, const float* values,
  * nn.utils.clip_grad_norm_(params, max_grad_norm) then torch.optim.Adam.step()
  * (the default eps=1e-5 Adam of agent/ppo.py:83, no weight decay/amsgrad),
  * over parameters stored back to back in ONE float32 buffer: tensor k owns
- * elements [offsets[k], offsets[k+1]).  One workgroup: per-tensor gradient
- * norms -> global norm -> clip coefficient -> Adam update, one launch.
+ * elements [offsets[k], offsets[k+1]).  Two launches: per-slice, per-tensor
+ * sums of squares into ws, then per element: global norm -> clip coefficient
+ * -> Adam update.
  *
  *   step    device f32 scalar, the Adam step count (incremented here);
  *   lr      device f64 scalar (read at run time, so a captured graph follows
  *           the host-side lr anneal);
  *   stop    device bool or NULL: when *stop != 0 the launch changes nothing
- *           (the KL early stop of agent/ppo.py:178-182 without a host sync).
+ *           (the KL early stop of agent/ppo.py:178-182 without a host sync);
+ *   ws      device f32 scratch of rx_adam_workspace_floats(cfg) elements,
+ *           owned by the caller (one per concurrently stepping optimizer).
  * max_grad_norm <= 0 disables clipping.  Grads are scaled in place, as
  * clip_grad_norm_ does.  Equal to torch's clip + Adam within float rounding
  * (tests/test_optim_gpu.py), not bit for bit (reduction order). */
@@ -214,8 +217,10 @@ typedef struct rx_adam_config {
   int64_t offsets[RX_ADAM_MAX_TENSORS + 1];
   double beta1, beta2, eps, max_grad_norm;
 } rx_adam_config;
+#define RX_ADAM_NORM_ELEMS 1024
+size_t rx_adam_workspace_floats(const rx_adam_config* cfg); /* 0 for an invalid cfg */
 int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
-                      float* step, const double* lr, const uint8_t* stop, void* stream);
+                      float* step, const double* lr, const uint8_t* stop, float* ws, void* stream);
 
 /* Fused PPO minibatch gradient (agent/ppo.py:170-203) for the reference's
  * actor-critic (agent/ppo.py:11-62: Linear(D,64)-tanh-Linear(64,64)-tanh-

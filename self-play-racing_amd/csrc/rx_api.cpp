@@ -522,19 +522,31 @@ int rx_gae_scan(int32_t T, int32_t N, const float* r, const float* v, const floa
   return gae(T, N, r, v, d, nv, nd, gamma, lam, adv, ret, 1, stream);
 }
 
-int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
-                      float* step, const double* lr, const uint8_t* stop, void* stream) {
-  if (!cfg) return fail(RX_EINVAL, "rx_adam_clip_step: cfg is null");
+static int adam_cfg_error(const rx_adam_config* cfg) {
+  if (!cfg) return fail(RX_EINVAL, "rx_adam: cfg is null");
   if (cfg->n_tensors <= 0 || cfg->n_tensors > RX_ADAM_MAX_TENSORS)
-    return fail(RX_EINVAL, "rx_adam_clip_step: n_tensors=%d not in [1, %d]", cfg->n_tensors, RX_ADAM_MAX_TENSORS);
-  if (cfg->offsets[0] != 0) return fail(RX_EINVAL, "rx_adam_clip_step: offsets[0] must be 0");
+    return fail(RX_EINVAL, "rx_adam: n_tensors=%d not in [1, %d]", cfg->n_tensors, RX_ADAM_MAX_TENSORS);
+  if (cfg->offsets[0] != 0) return fail(RX_EINVAL, "rx_adam: offsets[0] must be 0");
   for (int k = 0; k < cfg->n_tensors; ++k)
-    if (cfg->offsets[k + 1] < cfg->offsets[k]) return fail(RX_EINVAL, "rx_adam_clip_step: offsets not ascending");
-  if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !lr)
-    return fail(RX_EINVAL, "rx_adam_clip_step: null buffer");
+    if (cfg->offsets[k + 1] < cfg->offsets[k]) return fail(RX_EINVAL, "rx_adam: offsets not ascending");
   if (!(cfg->beta1 >= 0.0 && cfg->beta1 < 1.0 && cfg->beta2 >= 0.0 && cfg->beta2 < 1.0 && cfg->eps >= 0.0))
-    return fail(RX_EINVAL, "rx_adam_clip_step: bad betas/eps");
-  const int rc = rx_launch_adam(cfg, params, grads, exp_avg, exp_avg_sq, step, lr, stop, (hipStream_t)stream);
+    return fail(RX_EINVAL, "rx_adam: bad betas/eps");
+  return RX_OK;
+}
+
+size_t rx_adam_workspace_floats(const rx_adam_config* cfg) {
+  if (adam_cfg_error(cfg) != RX_OK) return 0;
+  const int64_t n = cfg->offsets[cfg->n_tensors];
+  const int64_t nb = n > 0 ? (n + RX_ADAM_NORM_ELEMS - 1) / RX_ADAM_NORM_ELEMS : 1;
+  return (size_t)(nb * cfg->n_tensors);
+}
+
+int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                      float* step, const double* lr, const uint8_t* stop, float* ws, void* stream) {
+  if (const int rc = adam_cfg_error(cfg)) return rc;
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !lr || !ws)
+    return fail(RX_EINVAL, "rx_adam_clip_step: null buffer");
+  const int rc = rx_launch_adam(cfg, params, grads, exp_avg, exp_avg_sq, step, lr, stop, ws, (hipStream_t)stream);
   if (rc != 0) return fail(RX_EHIP, "adam launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }

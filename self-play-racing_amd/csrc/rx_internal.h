@@ -82,7 +82,7 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
-                              const double* lr, const uint8_t* stop, hipStream_t s);
+                              const double* lr, const uint8_t* stop, float* ws, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);

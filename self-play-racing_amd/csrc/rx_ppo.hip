@@ -340,33 +340,61 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
   }
 }
 
-// grad[p] = sum_w partial[w][p] in a fixed order: 16 interleaved slices of
-// the workgroups per 256-parameter block (float4 lanes), combined in slice
-// order.  Block 0's wave 0 also folds the KL partials into approx_kl and raises
-// the early-stop flag (agent/ppo.py:178-182).  Partials have row stride Pp
-// (P rounded up to 64) so every row is float4-aligned.
+// grad[p] = sum_w partial[w][p] in a fixed order.  One workgroup owns 64
+// parameters (16 float4 columns) and reads the partial rows in 64 interleaved
+// slices (a wave reads four 256-byte row pieces), so the ~Pp/64 workgroups
+// stream the partials from most CUs; the slices are combined in slice order.
+// Block 0's wave 1 also folds the KL partials into approx_kl and raises the
+// early-stop flag (agent/ppo.py:178-182).  Partials have row stride Pp (P
+// rounded up to 64) so every row is float4-aligned.
+constexpr int kRedCols = 16;                    // float4 columns per workgroup
+constexpr int kRedSlices = 1024 / kRedCols;     // 64
+constexpr int kRedBatch = 8;                    // partial rows loaded per thread per round trip
 __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
                                                      const double* __restrict__ klp, int n_wg, int P, int Pp, int mb,
                                                      float kl_target, float* grad, uint8_t* stop, float* kl_at_stop) {
   if (*stop) return;
-  __shared__ float4 red[16][64];
-  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int p4 = blockIdx.x * 256 + lane * 4;  // first of this lane's 4 parameters
+  __shared__ float4 red[kRedSlices][kRedCols];
+  const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int p4 = blockIdx.x * (4 * kRedCols) + c * 4;  // first of this thread's 4 parameters
   float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (p4 < Pp)
-    for (int w = sl; w < n_wg; w += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + (size_t)w * Pp + p4);
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+    for (int w0 = sl; w0 < n_wg; w0 += kRedBatch * kRedSlices) {
+      float4 v[kRedBatch];  // independent loads first: one memory round trip per batch
+#pragma unroll
+      for (int k = 0; k < kRedBatch; ++k) {
+        const int w = w0 + k * kRedSlices;
+        v[k] = w < n_wg ? *reinterpret_cast<const float4*>(partial + (size_t)w * Pp + p4)
+                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int k = 0; k < kRedBatch; ++k) {
+        s.x += v[k].x;
+        s.y += v[k].y;
+        s.z += v[k].z;
+        s.w += v[k].w;
+      }
     }
-  red[sl][lane] = s;
+  red[sl][c] = s;
   __syncthreads();
-  if (sl == 0 && p4 < P) {
-    float4 t = red[0][lane];
-    for (int k = 1; k < 16; ++k) {
-      const float4 v = red[k][lane];
+  // slices -> 8 groups (group q sums slices q, q+8, ...) -> column total, in order
+  __shared__ float4 red2[8][kRedCols];
+  if (sl < 8) {
+    float4 t = red[sl][c];
+    for (int k = sl + 8; k < kRedSlices; k += 8) {
+      const float4 v = red[k][c];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+    red2[sl][c] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < kRedCols && p4 < P) {
+    float4 t = red2[0][c];
+    for (int k = 1; k < 8; ++k) {
+      const float4 v = red2[k][c];
       t.x += v.x;
       t.y += v.y;
       t.z += v.z;
@@ -375,7 +403,8 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
     const float o[4] = {t.x, t.y, t.z, t.w};
     for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o[q];
   }
-  if (blockIdx.x == 0 && sl == 1) {
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
     double k = 0.0;
     for (int w = lane; w < n_wg; w += 64) k += klp[w];
     for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
@@ -461,7 +490,7 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, f
     hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
-  hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 255) / 256), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
+  hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 4 * kRedCols - 1) / (4 * kRedCols)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
                      b->kl_target, grad, stop, kl_at_stop);
   return (int)hipGetLastError();
 }

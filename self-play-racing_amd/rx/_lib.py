@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -25,7 +25,7 @@ _P = ctypes.c_void_p
 
 EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sensor_angles", "rx_upload_tracks",
            "rx_assign", "rx_bind_state", "rx_set_speed_weight", "rx_reset", "rx_step", "rx_step_phases", "rx_gae",
-           "rx_gae_scan", "rx_adam_clip_step", "rx_ppo_n_params", "rx_ppo_workspace_floats",
+           "rx_gae_scan", "rx_adam_workspace_floats", "rx_adam_clip_step", "rx_ppo_n_params", "rx_ppo_workspace_floats",
            "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -110,7 +110,9 @@ def load(build_if_missing=True):
     gae_args = [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _P, _P]
     L.rx_gae.argtypes = gae_args
     L.rx_gae_scan.argtypes = gae_args
-    L.rx_adam_clip_step.argtypes = [ctypes.POINTER(RxAdamConfig), _P, _P, _P, _P, _P, _P, _P, _P]
+    L.rx_adam_workspace_floats.argtypes = [ctypes.POINTER(RxAdamConfig)]
+    L.rx_adam_workspace_floats.restype = ctypes.c_size_t
+    L.rx_adam_clip_step.argtypes = [ctypes.POINTER(RxAdamConfig), _P, _P, _P, _P, _P, _P, _P, _P, _P]
     L.rx_ppo_n_params.argtypes = [ctypes.c_int32]
     L.rx_ppo_workspace_floats.argtypes = [ctypes.c_int32, ctypes.c_int32]
     L.rx_ppo_workspace_floats.restype = ctypes.c_size_t

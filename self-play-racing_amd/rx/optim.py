@@ -6,7 +6,7 @@ Parameter objects, their names and the module's state_dict are unchanged) and
 pre-assigns ``p.grad`` as views of one flat gradient buffer, which autograd
 then accumulates into in place.  That gives:
 
-* ``step(stop)``: clip_grad_norm_ + Adam in one launch (rx_adam_clip_step),
+* ``step(stop)``: clip_grad_norm_ + Adam in two launches (rx_adam_clip_step),
   with lr / step count / early-stop flag in device memory -> graph-capturable;
 * one flat gradient tensor for the data-parallel all-reduce (rx.dist);
 * the torch ``optimizer`` stays the source of truth for the API: its
@@ -86,6 +86,10 @@ class FlatAdam:
             offs.append(offs[-1] + k)
         self.cfg = _lib.RxAdamConfig(len(sizes), (ctypes.c_int64 * 33)(*offs), float(b1), float(b2),
                                      float(g["eps"]), self.max_grad_norm)
+        self.ws = torch.empty(_lib.load().rx_adam_workspace_floats(ctypes.byref(self.cfg)), dtype=torch.float32,
+                              device=dev)
+        if self.ws.numel() == 0:
+            raise RuntimeError(_lib.load().rx_last_error().decode())
         self.import_state()
 
     def zero_grad(self):
@@ -102,7 +106,7 @@ class FlatAdam:
         _lib.check(L.rx_adam_clip_step(ctypes.byref(self.cfg), _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad),
                                        _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), _lib.ptr(self.step_t),
                                        _lib.ptr(self.lr_t), _lib.ptr(stop) if stop is not None else None,
-                                       _lib.stream_ptr(stream)), "rx_adam_clip_step")
+                                       _lib.ptr(self.ws), _lib.stream_ptr(stream)), "rx_adam_clip_step")
 
     # ------------------------------------------------------------ torch.optim interop
     def export_state(self):

@@ -66,5 +66,10 @@ def test_update_abi_validates_without_device():
     assert L.rx_policy_act(ctypes.byref(io), None) == _lib.RX_EINVAL
     cfg = _lib.RxAdamConfig()
     cfg.n_tensors = 0
-    assert L.rx_adam_clip_step(ctypes.byref(cfg), None, None, None, None, None, None, None, None) == _lib.RX_EINVAL
+    assert L.rx_adam_clip_step(ctypes.byref(cfg), None, None, None, None, None, None, None, None, None) \
+        == _lib.RX_EINVAL
     assert b"n_tensors" in L.rx_last_error()
+    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 0
+    cfg.n_tensors, cfg.beta1, cfg.beta2 = 2, 0.9, 0.999
+    cfg.offsets[1], cfg.offsets[2] = 1000, 2050
+    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 3 * 2  # ceil(2050 / 1024) slices x 2 tensors
