@@ -12,7 +12,10 @@ on one stream -- the configuration the PPO rollout uses, and the one whose
 per-launch kernel timing the roofline is computed from.  --stream-groups G
 steps the envs as G independent groups on G HIP streams instead (as an
 asynchronous rollout would); the JSON also reports that throughput for G = 4
-as "async_stream_groups", timed after the main region.  With N GPUs
+as "async_stream_groups", timed after the main region, and PPO training
+throughput ("ppo_train": rollout + GAE + the 10 x 16 minibatch update, 4,096
+envs per GPU; at N GPUs the update all-reduces one gradient+KL bucket per
+optimizer step over RCCL).  With N GPUs
 (torch.distributed.run, one rank per GPU) every rank owns 65,536 envs of a
 N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
 
@@ -106,6 +109,57 @@ def cpu_baseline(pool, widths, budget_s=15.0, n_envs=16):
                       f"({steps * n_envs} env-steps, {dt:.1f} s), seed-1 pool, random actions, 1 host core"}
 
 
+def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
+    """PPO training throughput (BASELINE.json configs[1] per GPU; configs[4]'s
+    data-parallel update at N GPUs): rx.ppo.PPO on envs_per_gpu envs per rank,
+    each update = T-step rollout with the fused policy in the loop + GAE + the
+    reference's 10 epochs x 16 minibatches (KL early stop disabled so every
+    update does the same work; device shuffles).  With N ranks every optimizer
+    step all-reduces ONE bucket [flat gradient, KL] (42,256 B) over RCCL, plus
+    one advantage-moment all-reduce per epoch (rx.dist)."""
+    from rx.configs import base_config
+    from rx.envs import RacingEnv
+    from rx.ppo import PPO
+    from rx.track import gen_tracks
+    n = envs_per_gpu * world
+    cfg = base_config(num_envs=n, num_steps=T, kl_target=1e9, shuffle="device")
+    cfg["total_timesteps"] = (updates + 1) * cfg["batch_size"]
+    random.seed(1)
+    np.random.seed(1)
+    pool = gen_tracks(n, seed=1)
+    widths = [np.random.randint(6, 10) for _ in range(n)]
+    t = PPO(lambda i: RacingEnv(11, pool, i, widths[i]), cfg, device=dev)
+    it = t.train_iter()
+    next(it)  # warm-up update (workspaces, first launches)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(updates):
+        next(it)
+    sync()
+    el = time.perf_counter() - t0
+    if dist:
+        x = torch.tensor([el], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x.item())
+    B = T * n
+    c = t.config
+    n_mb = c["num_minibatches"]
+    t.envs.close()
+    return {"value": round(B * updates / el, 1), "unit": "train env-steps/s", "updates": updates,
+            "ms_per_update": round(el / updates * 1e3, 3), "envs_per_gpu": envs_per_gpu, "global_envs": n,
+            "num_steps": T, "batch": B, "epochs_x_minibatches": f"{c['update_epochs']}x{n_mb}",
+            "update_path": "fused HIP (rx_ppo_minibatch_grad" + ("_shard + bucket all-reduce)" if world > 1 else ")"),
+            "allreduce_per_update": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
+            "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
+            "note": "KL early stop off, device shuffles; timed after one warm-up update"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -125,6 +179,10 @@ def main():
                          "(reported as 'async_stream_groups'; 0 = skip)")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
+    ap.add_argument("--ppo-updates", type=int, default=2,
+                    help="also time this many PPO updates (configs[1] per GPU; 0 = skip), reported as 'ppo_train'")
+    ap.add_argument("--ppo-envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--ppo-steps", type=int, default=128)
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -240,6 +298,8 @@ def main():
         for e in a_envs:
             e.close()
     gae = gae_roofline(E, dev) if rank == 0 else None
+    ppo = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
+                  args.ppo_updates) if args.ppo_updates > 0 else None
 
     if rank == 0:
         value = n_total * args.steps / elapsed
@@ -287,6 +347,7 @@ def main():
             "gae": gae,
             "episodes_ended": ep[2],
             "async_stream_groups": async_probe,
+            "ppo_train": ppo,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(pool, widths, budget_s=args.cpu_budget)

@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 8
+#define RX_ABI_VERSION 9
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -259,6 +259,34 @@ size_t rx_ppo_workspace_doubles(int32_t mb);
 int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* stream);
 int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, double* ws_f64, float* grad,
                           uint8_t* stop, float* kl_at_stop, void* stream);
+
+/* Data-parallel variant of the same minibatch step (one rank's shard of a
+ * global minibatch; rx.dist).  Replaces the per-rank part of
+ * agent/ppo.py:170-207 when the batch is sharded over W ranks:
+ *
+ *   rx_ppo_adv_moments     per minibatch (sum, square-sum) of this shard's
+ *                          advantages, f64 [n_mb][2] -> caller all-reduces;
+ *   rx_ppo_adv_finalize    (mean, unbiased std) from all-reduced moments over
+ *                          count = W*mb rows -> adv_stats of the batch
+ *                          (moments -> finalize with count = mb equals
+ *                          rx_ppo_adv_stats bit for bit);
+ *   rx_ppo_minibatch_grad_shard
+ *                          the shard's gradient times ``scale`` (= 1/W: an
+ *                          all-reduce SUM then gives the global-minibatch mean
+ *                          gradient) into grad, and scale * mean(old_logp -
+ *                          new_logp) into *kl_out.  Reads *stop (does nothing
+ *                          when set) but never writes it: with grad and kl_out
+ *                          adjacent in one buffer a single all-reduce carries
+ *                          both;
+ *   rx_ppo_kl_check        after the all-reduce: *kl > kl_target -> *stop = 1,
+ *                          *kl_at_stop = *kl (agent/ppo.py:178-182), so the
+ *                          rx_adam_clip_step that follows is skipped on every
+ *                          rank alike. */
+int rx_ppo_adv_moments(const rx_ppo_batch* b, int32_t n_mb, double* moments, void* stream);
+int rx_ppo_adv_finalize(const double* moments, int32_t n_mb, int64_t count, float* stats, void* stream);
+int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, float* ws_f32, double* ws_f64,
+                                float* grad, float* kl_out, const uint8_t* stop, void* stream);
+int rx_ppo_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, void* stream);
 
 /* Rollout policy step (agent/ppo.py:105-110: agent.get_action_and_value(obs)
  * under no_grad) for the same policy layout: per row, actor + critic forward,

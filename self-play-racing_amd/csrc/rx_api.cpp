@@ -574,8 +574,27 @@ int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* st
   if (rc) return rc;
   if (n_mb <= 0 || !stats) return fail(RX_EINVAL, "rx_ppo_adv_stats: n_mb=%d stats=%p", n_mb, (void*)stats);
   if ((int64_t)n_mb * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_adv_stats: n_mb*mb > n_rows");
-  if ((rc = rx_launch_adv_stats(b, n_mb, stats, (hipStream_t)stream)) != 0)
+  if ((rc = rx_launch_adv_stats(b, n_mb, stats, nullptr, (hipStream_t)stream)) != 0)
     return fail(RX_EHIP, "adv stats launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_adv_moments(const rx_ppo_batch* b, int32_t n_mb, double* moments, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if (n_mb <= 0 || !moments) return fail(RX_EINVAL, "rx_ppo_adv_moments: n_mb=%d moments=%p", n_mb, (void*)moments);
+  if ((int64_t)n_mb * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_adv_moments: n_mb*mb > n_rows");
+  if ((rc = rx_launch_adv_stats(b, n_mb, nullptr, moments, (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "adv moments launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_adv_finalize(const double* moments, int32_t n_mb, int64_t count, float* stats, void* stream) {
+  if (n_mb <= 0 || count <= 0 || !moments || !stats)
+    return fail(RX_EINVAL, "rx_ppo_adv_finalize: n_mb=%d count=%lld moments=%p stats=%p", n_mb, (long long)count,
+                (const void*)moments, (void*)stats);
+  const int rc = rx_launch_adv_finalize(moments, n_mb, count, stats, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "adv finalize launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }
 
@@ -586,8 +605,32 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
   if (!b->adv_stats) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: adv_stats is null");
   if (m < 0 || (int64_t)(m + 1) * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: m=%d out of range", m);
   if (!ws_f32 || !ws_f64 || !grad || !stop || !kl_at_stop) return fail(RX_EINVAL, "rx_ppo_minibatch_grad: null buffer");
-  if ((rc = rx_launch_ppo_grad(b, m, stop, kl_at_stop, ws_f32, ws_f64, grad, (hipStream_t)stream)) != 0)
+  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, (hipStream_t)stream)) != 0)
     return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, float* ws_f32, double* ws_f64,
+                                float* grad, float* kl_out, const uint8_t* stop, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if (!b->adv_stats) return fail(RX_EINVAL, "rx_ppo_minibatch_grad_shard: adv_stats is null");
+  if (m < 0 || (int64_t)(m + 1) * b->mb > b->n_rows)
+    return fail(RX_EINVAL, "rx_ppo_minibatch_grad_shard: m=%d out of range", m);
+  if (!(scale > 0.0f)) return fail(RX_EINVAL, "rx_ppo_minibatch_grad_shard: scale=%g", (double)scale);
+  if (!ws_f32 || !ws_f64 || !grad || !kl_out || !stop)
+    return fail(RX_EINVAL, "rx_ppo_minibatch_grad_shard: null buffer");
+  // the kernels only read *stop in shard mode (the decision is rx_ppo_kl_check's)
+  if ((rc = rx_launch_ppo_grad(b, m, scale, const_cast<uint8_t*>(stop), nullptr, kl_out, ws_f32, ws_f64, grad,
+                               (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
+int rx_ppo_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, void* stream) {
+  if (!kl || !stop || !kl_at_stop) return fail(RX_EINVAL, "rx_ppo_kl_check: null buffer");
+  const int rc = rx_launch_kl_check(kl, kl_target, stop, kl_at_stop, (hipStream_t)stream);
+  if (rc != 0) return fail(RX_EHIP, "kl check launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }
 

@@ -86,8 +86,10 @@ extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, flo
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);
-extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, hipStream_t s);
-extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, float* kl_at_stop, float* partial,
-                                  double* klp, float* grad, hipStream_t s);
+extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, double* moments, hipStream_t s);
+extern "C" int rx_launch_adv_finalize(const double* moments, int n_mb, int64_t count, float* stats, hipStream_t s);
+extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, hipStream_t s);
+extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
+                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s);
 extern "C" int rx_sort_pairs(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                              int32_t* vout, int n, int end_bit, hipStream_t s);

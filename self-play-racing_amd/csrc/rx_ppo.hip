@@ -352,7 +352,8 @@ constexpr int kRedSlices = 1024 / kRedCols;     // 64
 constexpr int kRedBatch = 8;                    // partial rows loaded per thread per round trip
 __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
                                                      const double* __restrict__ klp, int n_wg, int P, int Pp, int mb,
-                                                     float kl_target, float* grad, uint8_t* stop, float* kl_at_stop) {
+                                                     float kl_target, float scale, float* grad, uint8_t* stop,
+                                                     float* kl_at_stop, float* kl_out) {
   if (*stop) return;
   __shared__ float4 red[kRedSlices][kRedCols];
   const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
       t.w += v.w;
     }
     const float o[4] = {t.x, t.y, t.z, t.w};
-    for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o[q];
+    for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o[q] * scale;
   }
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
@@ -409,16 +410,28 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
     for (int w = lane; w < n_wg; w += 64) k += klp[w];
     for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
     const float kl = (float)(k / (double)mb);
-    if (lane == 0 && kl > kl_target) {
+    if (kl_out) {  // shard mode: this rank's share of the global KL, decided after the all-reduce
+      if (lane == 0) *kl_out = kl * scale;
+    } else if (lane == 0 && kl > kl_target) {
       *kl_at_stop = kl;
       *stop = 1;  // read by the optimizer launch that follows on the stream
     }
   }
 }
 
-// Per-minibatch (mean, unbiased std) of the advantages, one workgroup per minibatch.
+// Per-minibatch (mean, unbiased std) of the advantages, one workgroup per
+// minibatch; with ``moments`` set it writes the raw (sum, square-sum) instead,
+// for the cross-rank all-reduce of a data-parallel update (same summation
+// order, so moments -> k_adv_finalize == this kernel's stats bit for bit).
+__device__ __forceinline__ void adv_write(double a, double q, double count, float* stats, int i) {
+  const double mean = a / count;
+  const double var = count > 1.0 ? fmax(q - a * mean, 0.0) / (count - 1.0) : 0.0;
+  stats[2 * i] = (float)mean;
+  stats[2 * i + 1] = (float)sqrt(var);
+}
+
 __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ adv, const int64_t* __restrict__ perm,
-                                                    int mb, int64_t n_rows, float* stats) {
+                                                    int mb, int64_t n_rows, float* stats, double* moments) {
   __shared__ double red[2][16];
   const int64_t base = (int64_t)blockIdx.x * mb;
   double s = 0.0, s2 = 0.0;
@@ -443,10 +456,28 @@ __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ ad
       a += red[0][w];
       q += red[1][w];
     }
-    const double mean = a / mb;
-    const double var = mb > 1 ? fmax(q - a * mean, 0.0) / (mb - 1) : 0.0;
-    stats[2 * blockIdx.x] = (float)mean;
-    stats[2 * blockIdx.x + 1] = (float)sqrt(var);
+    if (moments) {
+      moments[2 * blockIdx.x] = a;
+      moments[2 * blockIdx.x + 1] = q;
+    } else {
+      adv_write(a, q, (double)mb, stats, blockIdx.x);
+    }
+  }
+}
+
+// (mean, unbiased std) of every minibatch from all-reduced moments over ``count`` rows.
+__global__ __launch_bounds__(64) void k_adv_finalize(const double* __restrict__ moments, int n_mb, double count,
+                                                     float* stats) {
+  for (int i = threadIdx.x; i < n_mb; i += 64) adv_write(moments[2 * i], moments[2 * i + 1], count, stats, i);
+}
+
+// The data-parallel KL early stop (agent/ppo.py:178-182) on the all-reduced
+// mean KL: raise *stop for the rx_adam_clip_step that follows.
+__global__ __launch_bounds__(64) void k_kl_check(const float* __restrict__ kl, float kl_target, uint8_t* stop,
+                                                 float* kl_at_stop) {
+  if (threadIdx.x == 0 && !*stop && *kl > kl_target) {
+    *kl_at_stop = *kl;
+    *stop = 1;
   }
 }
 
@@ -472,13 +503,24 @@ extern "C" int rx_ppo_n_params(int32_t obs_dim) {
   return obs_dim == 15 ? Lay<15>::P : obs_dim == 19 ? Lay<19>::P : 0;
 }
 
-extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL(k_adv_stats, dim3(n_mb), dim3(1024), 0, s, b->advantages, b->perm, b->mb, b->n_rows, stats);
+extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, double* moments, hipStream_t s) {
+  hipLaunchKernelGGL(k_adv_stats, dim3(n_mb), dim3(1024), 0, s, b->advantages, b->perm, b->mb, b->n_rows, stats,
+                     moments);
   return (int)hipGetLastError();
 }
 
-extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, float* kl_at_stop, float* partial,
-                                  double* klp, float* grad, hipStream_t s) {
+extern "C" int rx_launch_adv_finalize(const double* moments, int n_mb, int64_t count, float* stats, hipStream_t s) {
+  hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(64), 0, s, moments, n_mb, (double)count, stats);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, hipStream_t s) {
+  hipLaunchKernelGGL(k_kl_check, dim3(1), dim3(64), 0, s, kl, kl_target, stop, kl_at_stop);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
+                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s) {
   const int rp = rows_per_wg(b->mb);
   const int n_wg = (b->mb + rp - 1) / rp;
   ppo_args a{*b, m, rp, stop, klp};
@@ -491,7 +533,7 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, uint8_t* stop, f
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
   hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 4 * kRedCols - 1) / (4 * kRedCols)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
-                     b->kl_target, grad, stop, kl_at_stop);
+                     b->kl_target, scale, grad, stop, kl_at_stop, kl_out);
   return (int)hipGetLastError();
 }
 

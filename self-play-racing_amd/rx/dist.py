@@ -11,6 +11,11 @@ the only exchanges are, per optimizer step,
   so the KL early stop and the minibatch advantage normalisation are global
   (every rank stops in the same minibatch);
 
+with the fused HIP update (rx.ppo_fused.FusedMinibatchGrad.shard_epoch) the
+same exchanges shrink to ONE all-reduce per optimizer step of the bucket
+[flat gradient / W, KL / W] (FlatAdam.bucket) plus one per epoch of every
+minibatch's advantage (sum, square-sum);
+
 and one 3-float all-reduce of episode statistics per update.  Minibatch
 shuffles use np.random with the same seed on every rank, so all ranks walk
 the same minibatch schedule over their own shards.
@@ -82,6 +87,14 @@ def average_flat(flat):
         return
     td.all_reduce(flat)
     flat.div_(td.get_world_size())
+
+
+def all_reduce_sum(t):
+    """In-place SUM over ranks (the fused data-parallel update pre-scales its
+    shard gradient and KL by 1/world, so the sum is the global mean)."""
+    if active():
+        td.all_reduce(t)
+    return t
 
 
 def broadcast_parameters(module, src=0):

@@ -8,7 +8,9 @@ then accumulates into in place.  That gives:
 
 * ``step(stop)``: clip_grad_norm_ + Adam in two launches (rx_adam_clip_step),
   with lr / step count / early-stop flag in device memory -> graph-capturable;
-* one flat gradient tensor for the data-parallel all-reduce (rx.dist);
+* one flat gradient tensor for the data-parallel all-reduce (rx.dist), with
+  the minibatch KL in the slot after it (``bucket``: grad + KL in ONE
+  all-reduce);
 * the torch ``optimizer`` stays the source of truth for the API: its
   param_groups carry lr/betas/eps (the lr anneal writes there), and
   ``export_state()`` / ``import_state()`` move the moments and step count in
@@ -59,7 +61,11 @@ class FlatAdam:
         n = sum(sizes)
         self.numel = n
         self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        # one all-reduce bucket: the flat gradient and, right after it, the
+        # data-parallel update's KL slot (rx_ppo_minibatch_grad_shard)
+        self.bucket = torch.zeros(n + 1, dtype=torch.float32, device=dev)
+        self.flat_grad = self.bucket[:n]
+        self.kl_slot = self.bucket[n:]
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
         self.step_t = torch.zeros((), dtype=torch.float32, device=dev)

@@ -265,14 +265,16 @@ class PPO:
             return self._update_torch(b)
         flat.rebind()
         flat.sync_lr()
+        from . import ppo_fused
+        mb = self._minibatch_size()
+        fused = self.config.get("fused_update", True) and ppo_fused.supported(self.agent, b, mb)
         if rdist.world() == 1:
-            from . import ppo_fused
-            mb = self._minibatch_size()
-            fused = self.config.get("fused_update", True) and ppo_fused.supported(self.agent, b, mb)
             # capture when launches would outpace the GPU work (small minibatches)
             capture = self._want_graph("graph_update", mb < 8192)
             if fused or capture:
                 return self._update_epochs(b, fused, capture)
+        elif fused:  # data parallel: shard gradients + ONE bucket all-reduce per step, eager
+            return self._update_epochs(b, True, False)
         return self._update_flat_eager(b)
 
     def _want_graph(self, key, auto):
@@ -335,7 +337,8 @@ class PPO:
         launch; with ``capture`` the epoch is one HIP graph.  Cached per
         (buffers, batch, minibatch, dtype, kernel, capture)."""
         from . import ppo_fused
-        key = tuple(t.data_ptr() for t in b) + (B, mb, self.config.get("policy_dtype", "fp32"), fused, capture)
+        key = tuple(t.data_ptr() for t in b) + (B, mb, self.config.get("policy_dtype", "fp32"), fused, capture,
+                                                self.config.get("shard_update", False))
         graphs = self.__dict__.setdefault("_upd_graphs", {})
         if key in graphs:
             return graphs[key]
@@ -346,7 +349,11 @@ class PPO:
             kl=torch.zeros(1, dtype=torch.float32, device=dev), graph=None, fused=None, run=None)
         if fused:
             ent.fused = ppo_fused.FusedMinibatchGrad(self.agent, self._flat, b, mb, ent.perm, self.config)
-            if capture:
+            if rdist.world() > 1 or self.config.get("shard_update", False):
+                # collectives stay outside graphs; "shard_update" runs this path on one rank (tests)
+                w = rdist.world()
+                ent.run = lambda: ent.fused.shard_epoch(ent.stop, ent.kl, w, rdist.all_reduce_sum)
+            elif capture:
                 ent.graph = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(dev)
                 with torch.cuda.graph(ent.graph):

@@ -56,6 +56,30 @@ class FusedMinibatchGrad:
                                                 _lib.ptr(self.flat.flat_grad), _lib.ptr(stop), _lib.ptr(kl_at_stop),
                                                 _lib.stream_ptr(stream)), "rx_ppo_minibatch_grad")
 
+    def shard_epoch(self, stop, kl_at_stop, world, all_reduce):
+        """One epoch of a data-parallel update over this rank's shard: the
+        minibatch advantage moments are all-reduced once per epoch, then per
+        minibatch the shard gradient and KL (pre-scaled by 1/world) go out in
+        ONE all-reduce of FlatAdam.bucket, followed by the KL check and the
+        Adam launch.  ``all_reduce`` is an in-place SUM (rx.dist.all_reduce_sum)."""
+        L, s = self.L, _lib.stream_ptr(None)
+        mom = self.__dict__.get("moments")
+        if mom is None:
+            mom = self.moments = torch.empty((self.n_mb, 2), dtype=torch.float64, device=self.stats.device)
+        _lib.check(L.rx_ppo_adv_moments(self.batch, self.n_mb, _lib.ptr(mom), s), "rx_ppo_adv_moments")
+        all_reduce(mom)
+        _lib.check(L.rx_ppo_adv_finalize(_lib.ptr(mom), self.n_mb, self.mb * world, _lib.ptr(self.stats), s),
+                   "rx_ppo_adv_finalize")
+        flat, scale = self.flat, 1.0 / world
+        for m in range(self.n_mb):
+            _lib.check(L.rx_ppo_minibatch_grad_shard(self.batch, m, scale, _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
+                                                     _lib.ptr(flat.flat_grad), _lib.ptr(flat.kl_slot), _lib.ptr(stop),
+                                                     s), "rx_ppo_minibatch_grad_shard")
+            all_reduce(flat.bucket)
+            _lib.check(L.rx_ppo_kl_check(_lib.ptr(flat.kl_slot), self.batch.kl_target, _lib.ptr(stop),
+                                         _lib.ptr(kl_at_stop), s), "rx_ppo_kl_check")
+            flat.step(stop=stop)
+
     def epoch(self, stop, kl_at_stop):
         """All minibatch steps of one epoch over the current perm."""
         self.adv_stats()

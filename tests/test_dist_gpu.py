@@ -21,9 +21,10 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(fused=False):
     from rx.configs import base_config
-    return base_config(num_envs=8, num_steps=32, num_minibatches=4, update_epochs=2, kl_target=1e9)
+    return base_config(num_envs=8, num_steps=32, num_minibatches=4, update_epochs=2, kl_target=1e9,
+                       fused_update=fused)
 
 
 def _data():
@@ -53,12 +54,12 @@ def _make_ppo(cfg):
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, fused):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as td
     td.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        cfg = _cfg()
+        cfg = _cfg(fused)
         p = _make_ppo(cfg)
         sl = slice(rank * 4, (rank + 1) * 4)
         d = [t[:, sl].contiguous().cuda() for t in _data()]
@@ -70,11 +71,14 @@ def _worker(rank, world, port, q):
         td.destroy_process_group()
 
 
-def test_two_rank_flat_update_in_sync():
+@pytest.mark.parametrize("fused", [False, True], ids=["autograd", "fused_shard"])
+def test_two_rank_flat_update_in_sync(fused):
+    """fused: the HIP shard path (rx_ppo_minibatch_grad_shard + ONE bucket
+    all-reduce per step); autograd: torch autograd + flat-gradient all-reduce."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, fused)) for r in range(2)]
     for pr in procs:
         pr.start()
     res = dict((r, (a, s)) for r, a, s in (q.get(timeout=300) for _ in procs))

@@ -220,3 +220,55 @@ def test_fused_update_graph_equals_eager():
         assert ent.fused is not None and (ent.graph is not None) == graph
         res.append((t._flat.flat_param.clone(), t._flat.exp_avg_sq.clone(), float(t._flat.step_t)))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
+
+
+@pytest.mark.parametrize("kl_target", [1e9, -1.0])
+def test_shard_update_world1_equals_fused(kl_target):
+    """The data-parallel launch sequence (adv moments -> finalize, shard grad
+    scaled by 1/world with the KL in the bucket slot, rx_ppo_kl_check, Adam) at
+    world = 1 == the single-rank fused update bit for bit, early stop included."""
+    res = []
+    for shard in (False, True):
+        t = _trainer(graph_update=False, shard_update=shard, kl_target=kl_target)
+        data = _rollout(t)
+        np.random.seed(4)
+        for u in range(2):
+            t._anneal(u, 4)
+            t.ppo_update(*data)
+        res.append((t._flat.flat_param.clone(), t._flat.exp_avg.clone(), float(t._flat.step_t)))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
+    if kl_target < 0:
+        assert res[0][2] == 0.0
+
+
+def test_adv_moments_finalize_equals_adv_stats():
+    """rx_ppo_adv_moments -> rx_ppo_adv_finalize(count = mb) == rx_ppo_adv_stats bit for bit;
+    with moments summed over two shards, finalize matches float64 statistics of the union."""
+    from rx import _lib
+    L = _lib.load()
+    B, mb, D = 4096, 512, 15
+    obs, act, logp, adv, ret, val = _batch(B, D, seed=3)
+    perm = torch.randperm(B, device="cuda")
+    params = torch.zeros(L.rx_ppo_n_params(D), device="cuda")
+    log_std = torch.zeros(2, device="cuda")
+    stats = torch.zeros(2 * (B // mb), device="cuda")
+    b = _lib.RxPPOBatch(D, mb, B, *[_lib.ptr(t) for t in (obs, act, logp, adv, ret, val, perm, params, log_std,
+                                                           stats)], 0.2, 0.5, 0.015)
+    s = _lib.stream_ptr()
+    _lib.check(L.rx_ppo_adv_stats(b, B // mb, _lib.ptr(stats), s))
+    mom = torch.zeros((B // mb, 2), dtype=torch.float64, device="cuda")
+    st2 = torch.zeros_like(stats)
+    _lib.check(L.rx_ppo_adv_moments(b, B // mb, _lib.ptr(mom), s))
+    _lib.check(L.rx_ppo_adv_finalize(_lib.ptr(mom), B // mb, mb, _lib.ptr(st2), s))
+    assert torch.equal(stats, st2)
+    # two shards of half-minibatches: moments add, finalize over 2 * (mb / 2) rows
+    half = _lib.RxPPOBatch(D, mb // 2, B, *[_lib.ptr(t) for t in (obs, act, logp, adv, ret, val, perm, params,
+                                                                   log_std, stats)], 0.2, 0.5, 0.015)
+    m2 = torch.zeros((2 * (B // mb), 2), dtype=torch.float64, device="cuda")
+    _lib.check(L.rx_ppo_adv_moments(half, 2 * (B // mb), _lib.ptr(m2), s))
+    summed = (m2[0::2] + m2[1::2]).contiguous()  # minibatch m = half-minibatches 2m and 2m+1
+    st3 = torch.zeros_like(stats)
+    _lib.check(L.rx_ppo_adv_finalize(_lib.ptr(summed), B // mb, mb, _lib.ptr(st3), s))
+    a = adv.double()[perm].view(B // mb, mb)
+    ref = torch.stack([a.mean(1), a.std(1)], 1).reshape(-1).float()
+    torch.testing.assert_close(st3, ref, rtol=1e-6, atol=1e-6)
