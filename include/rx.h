@@ -80,7 +80,11 @@ typedef struct {
   int32_t ray_order;       /* raycast lane order: 0 = (env, agent, ray), 11 rays of ~6 envs per wave;
                               1 = ray-major: one (agent, ray) of 64 consecutive envs per wave -- with
                               sort_interval > 0 those envs are track neighbours, so a wave's rays are
-                              nearly parallel and share culling chunks.  Scheduling only: same results. */
+                              nearly parallel and share culling chunks; 2 = sorted ray tasks: every
+                              sort_interval steps all (env, agent, ray) tasks are radix-sorted by
+                              (slot, waypoint bucket, absolute-direction sector), so a wave holds rays
+                              with nearby origins and nearly equal directions from any envs.
+                              Scheduling only: same results. */
   int32_t cull_super;      /* two-level raycast culling: chunks per super-chunk box (0 = one level) */
 } rx_config;
 

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -99,6 +100,8 @@ struct rx_env {
   size_t sort_tmp_bytes = 0;
   int sort_bits = 16;
   uint64_t dyn_calls = 0;
+  // ray_order 2: direction-sorted (agent, ray) task ids, rewritten by k_dyn every step
+  DevBuf<int32_t> tasks;
   // state
   bool bound = false;
   rx_state st{};
@@ -227,7 +230,8 @@ int rx_create(const rx_config* cfg, rx_env** out) {
   if (cfg->n_agents != 1 && cfg->n_agents != 2) return fail(RX_EINVAL, "n_agents must be 1 or 2 (got %d)", cfg->n_agents);
   if (cfg->n_sensors <= 0 || cfg->n_sensors > 256) return fail(RX_EINVAL, "n_sensors out of range (%d)", cfg->n_sensors);
   if (cfg->max_steps <= 0) return fail(RX_EINVAL, "max_steps must be > 0");
-  if (cfg->ray_order != 0 && cfg->ray_order != 1) return fail(RX_EINVAL, "ray_order must be 0 or 1 (got %d)", cfg->ray_order);
+  if (cfg->ray_order < 0 || cfg->ray_order > 2)
+    return fail(RX_EINVAL, "ray_order must be 0, 1 or 2 (got %d)", cfg->ray_order);
   if (cfg->cull_super < 0 || cfg->cull_super > 64) return fail(RX_EINVAL, "cull_super out of range (%d)", cfg->cull_super);
   if (cfg->autoreset < RX_AUTORESET_NEXT_STEP || cfg->autoreset > RX_AUTORESET_DISABLED)
     return fail(RX_EINVAL, "bad autoreset mode %d", cfg->autoreset);
@@ -281,7 +285,7 @@ int rx_destroy(rx_env* h) {
                   &h->wsuper_box, &h->rel_angles})
     b->release();
   for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->super_off, &h->wsuper_off, &h->perm[0], &h->perm[1],
-                  &h->vals_in, &h->slot_n})
+                  &h->vals_in, &h->slot_n, &h->tasks})
     b->release();
   h->resets.release();
   h->dyn_waves.release();
@@ -334,7 +338,14 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   std::iota(perm.begin(), perm.end(), 0);
   std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return track_of_env[a] < track_of_env[b]; });
   std::vector<rx_wave> dyn, ray;
+  std::vector<int> ray_groups;  // end index (in ray) of each 64-env block's waves
+  if (h->cfg.ray_order == 2 && A * R > 16 * A)
+    return fail(RX_EINVAL, "ray_order 2 supports at most 16 sensors (got %d)", R);
   h->dyn_lpe = (A == 1 && N <= RX_DYN1_SMALL_N) ? RX_DYN1_LPE_SMALL : 1;
+  if (const char* ev = getenv("RX_DYN1_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
+    const int v = atoi(ev);
+    if (A == 1 && (v == 1 || v == 2 || v == 4)) h->dyn_lpe = v;
+  }
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
   int g0 = 0;
@@ -345,28 +356,40 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     const int ng = g1 - g0;
     const int epw = A == 1 ? 64 / h->dyn_lpe : 64;  // envs per dynamics wave
     for (int s = 0; s < ng; s += epw) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(epw, ng - s)});
-    if (h->cfg.ray_order == 0) {
+    if (h->cfg.ray_order == 2) {  // per dynamics wave: its envs' A*R tasks (direction-sorted by k_dyn), 64 a wave
+      for (int s = 0; s < ng; s += epw) {
+        const int cnt = std::min(epw, ng - s), nt = cnt * A * R, ps = g0 + s;
+        for (int j = 0; j < nt; j += 64) ray.push_back(rx_wave{k, ps, ps * A * R + j, std::min(64, nt - j)});
+        ray_groups.push_back((int)ray.size());
+      }
+    } else if (h->cfg.ray_order == 0) {
       const long long tasks = (long long)ng * A * R;
       for (long long s = 0; s < tasks; s += 64)
         ray.push_back(rx_wave{k, g0, (int32_t)s, (int32_t)std::min<long long>(64, tasks - s)});
     } else {  // ray-major: one (agent, ray) x one 64-env block per wave, grouped by block
-      for (int b = 0; 64 * b < ng; ++b)
+      for (int b = 0; 64 * b < ng; ++b) {
         for (int qr = 0; qr < A * R; ++qr)
           ray.push_back(rx_wave{k, g0, qr * ng + 64 * b, std::min(64, ng - 64 * b)});
+        ray_groups.push_back((int)ray.size());
+      }
     }
     g0 = g1;
   }
-  if (h->cfg.ray_order == 1) {
+  if (h->cfg.ray_order >= 1) {
     // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs
     // (MI355X_MICROARCH.md, workgroup dispatch), and every wave of one 64-env
-    // block writes into the same obs rows, so the A*R waves of a block go to
-    // physical indices p = ((g / 8) * A*R + qr) * 8 + g % 8 -- one XCD, one L2
-    // to merge their partial-line writes.  Padding waves have count 0.
-    const int AR = A * R;
-    const size_t n_groups = ray.size() / AR, padded = (n_groups + 7) / 8 * 8;
-    std::vector<rx_wave> placed(padded * AR, rx_wave{0, 0, 0, 0});
-    for (size_t g = 0; g < n_groups; ++g)
-      for (int qr = 0; qr < AR; ++qr) placed[((g / 8) * AR + qr) * 8 + g % 8] = ray[g * AR + qr];
+    // block writes into the same obs rows, so the (up to) A*R waves of block g
+    // go to physical indices p = ((g / 8) * maxw + j) * 8 + g % 8 -- one XCD,
+    // one L2 to merge their partial-line writes.  Padding waves have count 0.
+    const size_t n_groups = ray_groups.size();
+    int maxw = 0;
+    for (size_t g = 0; g < n_groups; ++g) maxw = std::max(maxw, ray_groups[g] - (g ? ray_groups[g - 1] : 0));
+    const size_t padded = (n_groups + 7) / 8 * 8;
+    std::vector<rx_wave> placed(padded * maxw, rx_wave{0, 0, 0, 0});
+    for (size_t g = 0; g < n_groups; ++g) {
+      const int w0 = g ? ray_groups[g - 1] : 0;
+      for (int j = 0; w0 + j < ray_groups[g]; ++j) placed[((g / 8) * maxw + j) * 8 + g % 8] = ray[w0 + j];
+    }
     ray.swap(placed);
   }
   RX_HIP(hipSetDevice(h->cfg.device));
@@ -394,6 +417,14 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     if (hipMalloc(&h->sort_tmp.p, std::max<size_t>(tmp, 16)) != hipSuccess) return fail(RX_ENOMEM, "sort temp alloc");
     h->sort_tmp.n = std::max<size_t>(tmp, 16);
     h->sort_tmp_bytes = tmp;
+  }
+  if (h->cfg.ray_order == 2) {  // task ids before the first k_dyn: (agent, ray) minor within each env
+    const size_t nt = (size_t)N * A * R;
+    std::vector<int32_t> t0(nt);
+    size_t o = 0;
+    for (int i = 0; i < N; ++i)
+      for (int qr = 0; qr < A * R; ++qr) t0[o++] = perm[i] * A * R + qr;
+    if ((rc = upload(h->tasks, t0.data(), nt))) return rc;
   }
   if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
   if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
@@ -458,6 +489,8 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.ray_order = h->cfg.ray_order;
   a.dyn_lpe = h->dyn_lpe;
   a.slot_nenv = h->slot_n.p;
+  a.tasks = h->tasks.p;
+  a.tasks_out = h->cfg.ray_order == 2 ? h->tasks.p : nullptr;
   hipStream_t s = (hipStream_t)stream;
   int rc;
   if (phases & RX_PHASE_DYNAMICS) {
@@ -482,6 +515,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (phases & RX_PHASE_RAYS) {
     a.sort_keys = nullptr;
     a.sort_vals = nullptr;
+    a.tasks_out = nullptr;
     if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_RAYS, s)) != 0)
       return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
   }

@@ -61,6 +61,11 @@ struct rx_kargs {
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
   uint32_t* sort_keys;        // [N] k_dyn writes (slot << 16 | waypoint) at its perm position, or nullptr
   int32_t* sort_vals;         // [N] k_dyn writes the env id at its perm position
+  // ray_order 2: k_dyn writes the direction-sorted (agent, ray) task ids of
+  // each dynamics wave's envs to tasks_out[perm_start*A*R ..]; k_rays reads
+  // tasks[task_start + lane] (the same buffer)
+  int32_t* tasks_out;
+  const int32_t* tasks;
   int32_t n_dyn_waves;
   int32_t n_ray_waves;
   int32_t n_sensors;

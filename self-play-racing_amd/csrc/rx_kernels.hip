@@ -274,6 +274,56 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
   a.sort_vals[pos] = e;
 }
 
+// ray_order 2: the (agent, ray) tasks of a dynamics wave's envs (64 track
+// neighbours after the spatial sort) are ordered by the absolute direction
+// of the ray (64 sectors) before k_rays runs, so each of the block's ray waves
+// holds nearly parallel rays from nearby origins, whichever env they belong to.
+// A per-wave counting sort in LDS: ds_add_rtn ranks every task in its sector,
+// a 64-lane scan turns the sector counts into offsets, and the task ids are
+// written to tasks_out[perm_start*A*R ..].  Runs every step with all 64 lanes
+// of the wave (env lanes have e >= 0).  The direction is the car's new angle
+// (the one k_rays casts from).  Scheduling only: no result depends on it.
+constexpr int kTaskSectors = 64;
+template <int A>
+__device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int e, const double* ang,
+                                                 int32_t* cnt) {
+  constexpr int kMaxT = 16 * A;  // rx_assign enforces n_sensors <= 16 for ray_order 2
+  const int R = a.n_sensors, AR = A * R;
+  const int lane = threadIdx.x & 63;
+  const float inv = (float)kTaskSectors * 0.15915494309189535f;  // sectors per radian
+  int pk[kMaxT];  // (rank << 6) | sector per task
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (e >= 0) {
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < AR) {
+        const int q = t / R, r = t - (t / R) * R;
+        const float th = (float)(ang[q] + a.rel_angles[r]);
+        const int sec = (int)__builtin_floorf(th * inv) & (kTaskSectors - 1);
+        pk[t] = (atomicAdd(&cnt[sec], 1) << 6) | sec;
+      }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int c0 = cnt[lane];
+  int c = c0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(c, o, 64);
+    if (lane >= o) c += v;
+  }
+  cnt[lane] = c - c0;  // exclusive offset of sector `lane`
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (e >= 0) {
+    int32_t* out = a.tasks_out + (size_t)perm_start * AR;
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < AR) out[cnt[pk[t] & 63] + (pk[t] >> 6)] = A * e * R + t;  // task id (A*e + q)*R + r
+  }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -294,7 +344,7 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
 }
 
 template <int LPE>
-__global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
+__device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int& e_out) {
   constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
@@ -488,6 +538,22 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
     o[3] = (float)last_steering;
   }
   write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
+  ang_out[0] = c.angle;
+  e_out = e;
+}
+
+template <int LPE>
+__global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (wave >= a.n_dyn_waves) return;
+  __shared__ int32_t tcnt[4][kTaskSectors];
+  int32_t* cnt = tcnt[threadIdx.x >> 6];
+  const bool sorting = a.tasks_out != nullptr;
+  if (sorting) cnt[threadIdx.x & 63] = 0;
+  double ang[1];
+  int e = -1;  // set on the lane that finishes an env (sub 0)
+  dyn1_env<LPE>(a, ang, e);
+  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
 }
 
 // ============================================================ k_dyn, A == 2
@@ -553,7 +619,7 @@ __device__ __forceinline__ bool rect_intersect(const double ax[4], const double 
   return !sep;
 }
 
-__global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
+__device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int& e_out) {
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
@@ -799,6 +865,22 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
     ob[7] = (float)rx_clip(lvy / RX_MAX_SPEED, -1.0, 1.0);
   }
   write_sort_key(a, we.perm_start + lane, k, e, c[0].progress, W);
+  ang_out[0] = c[0].angle;
+  ang_out[1] = c[1].angle;
+  e_out = e;
+}
+
+__global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (wave >= a.n_dyn_waves) return;
+  __shared__ int32_t tcnt[4][kTaskSectors];
+  int32_t* cnt = tcnt[threadIdx.x >> 6];
+  const bool sorting = a.tasks_out != nullptr;
+  if (sorting) cnt[threadIdx.x & 63] = 0;
+  double ang[2];
+  int e = -1;
+  dyn2_env(a, ang, e);
+  if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
 }
 
 // ============================================================ k_rays
@@ -901,8 +983,14 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   if (lane >= we.count) return;
   const int R = a.n_sensors;
   const int task = we.task_start + lane;
-  int env_local, q, ray;
-  if (a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
+  int env_local = 0, q, ray, e;
+  if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
+    const int t = a.tasks[task];
+    const int iq = t / R;
+    ray = t - iq * R;
+    e = iq / A;
+    q = iq - e * A;
+  } else if (a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
     env_local = task / (A * R);
     const int rem = task - env_local * (A * R);
     q = rem / R;
@@ -914,7 +1002,7 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
     q = qr / R;
     ray = qr - q * R;
   }
-  const int e = a.perm[we.perm_start + env_local];
+  if (a.ray_order != 2) e = a.perm[we.perm_start + env_local];
   const int i = A * e + q;
   const double ox = a.st.x[i], oy = a.st.y[i];
   const double theta = a.st.angle[i] + a.rel_angles[ray];  // racing_env.py:50
@@ -1105,8 +1193,10 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   const dim3 blk(256);
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
-    if (n_agents == 1 && a->dyn_lpe == RX_DYN1_LPE_SMALL)
-      hipLaunchKernelGGL(k_dyn1<RX_DYN1_LPE_SMALL>, grd, blk, 0, s, *a);
+    if (n_agents == 1 && a->dyn_lpe == 4)
+      hipLaunchKernelGGL(k_dyn1<4>, grd, blk, 0, s, *a);
+    else if (n_agents == 1 && a->dyn_lpe == 2)
+      hipLaunchKernelGGL(k_dyn1<2>, grd, blk, 0, s, *a);
     else if (n_agents == 1)
       hipLaunchKernelGGL(k_dyn1<1>, grd, blk, 0, s, *a);
     else

@@ -57,7 +57,7 @@ class RacingVectorEnv:
 
     def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
                  seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=12,
-                 sort_interval=16, ray_order=1, cull_super=6):
+                 sort_interval=16, ray_order=None, cull_super=6):
         self.L = _lib.load()
         self.device = torch.device(device) if device is not None else _default_device()
         if self.device.type != "cuda":
@@ -68,6 +68,8 @@ class RacingVectorEnv:
         self.num_envs = N
         self.n_agents = A = int(n_agents)
         self.n_sensors = R = int(n_sensors)
+        if ray_order is None:  # direction-sorted ray tasks (rx.h ray_order 2) cover up to 16 sensors
+            ray_order = 2 if R <= 16 else 1
         self.D = R + 4 + 4 * (A - 1)
         self.max_steps = int(max_steps)
         self.speed_weight = float(speed_weight)

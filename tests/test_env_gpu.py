@@ -272,7 +272,8 @@ def test_numpy_surface(rx, golden):
 
 
 @pytest.mark.parametrize("chunk,sort,order,sup", [(16, 1, 0, 0), (8, 3, 0, 0), (32, 0, 0, 0), (16, 4, 1, 0),
-                                                  (16, 0, 1, 0), (8, 16, 1, 8), (6, 0, 0, 5), (24, 16, 1, 3)])
+                                                  (16, 0, 1, 0), (8, 16, 1, 8), (6, 0, 0, 5), (24, 16, 1, 3),
+                                                  (12, 16, 2, 6), (16, 3, 2, 0), (12, 0, 2, 6)])
 def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
     """Chunk culling, spatial re-sorting and the ray-major lane order change
     scheduling only: outputs are bit-identical to the brute-force raycast over
@@ -336,12 +337,13 @@ def test_vector_env_from_table_file(tmp_path):
     b.close()
 
 
-def test_ray_major_two_car_is_exact(rx, golden):
-    """Ray-major lane order for the two-car kernel (agent, ray) x envs."""
+@pytest.mark.parametrize("order", [1, 2])
+def test_ray_major_two_car_is_exact(rx, golden, order):
+    """Ray-major (1) and sorted-task (2) lane orders for the two-car kernel (agent, ray) x envs."""
     N = 512
     tracks = np.arange(N) % golden.n_tracks
     va = _venv(rx, golden, tracks, n_agents=2, seed=3)
-    vb = _venv(rx, golden, tracks, n_agents=2, seed=3, sort_interval=2, ray_order=1)
+    vb = _venv(rx, golden, tracks, n_agents=2, seed=3, sort_interval=2, ray_order=order)
     assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(8)
     for t in range(200):

@@ -16,7 +16,8 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     pool, widths = seed1_pool(N)
     out = {}
-    for order, sort in ((0, 0), (0, 1), (1, 0), (1, 16)):
+    combos = [tuple(int(x) for x in c.split(",")) for c in sys.argv[2:]] or [(0, 0), (0, 1), (1, 0), (1, 16)]
+    for order, sort in combos:
         env = RacingVectorEnv(pool, widths, device="cuda", sort_interval=sort, ray_order=order)
         env.reset_device()
         g = torch.Generator(device="cuda").manual_seed(0)
@@ -31,7 +32,7 @@ def main():
             a[:, 1].abs_()
             env.step_device(a)
         c = env.read_counters()
-        ray_waves = N * 11 / 64 * steps
+        ray_waves = env.n_ray_waves * steps if hasattr(env, "n_ray_waves") else N * 11 / 64 * steps
         dyn_waves = N / 64 * steps  # k_dyn1: 64 / RX_DYN1_LPE envs per wave (LPE = 1)
         out[f"order{order}_sort{sort}"] = {"ray_chunks_tested_per_wave": c["ray_chunk_tests"] / ray_waves,
                               "ray_chunks_scanned_per_wave": c["ray_chunks_scanned"] / ray_waves,
