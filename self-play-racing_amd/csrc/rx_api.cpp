@@ -82,6 +82,7 @@ struct rx_env {
   DevBuf<double> super_box;
   DevBuf<int32_t> wsuper_off;  // two-level closest-waypoint culling
   DevBuf<double> wsuper_box;
+  DevBuf<float> chunk_box_f, super_box_f;  // outward-rounded float32 copies (raycast box tests)
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
@@ -202,7 +203,22 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
     }
     wsoff[k + 1] = wsoff[k] + nws;
   }
+  // float32 copies rounded outward (min corner down, max corner up): each f32
+  // box contains its f64 box, so a test that keeps the f32 box keeps the f64 one
+  auto to_f32 = [](const std::vector<double>& b) {
+    std::vector<float> f(b.size());
+    for (size_t i = 0; i < b.size(); ++i) {
+      float v = (float)b[i];
+      if ((i & 3) < 2 && (double)v > b[i]) v = std::nextafter(v, -HUGE_VALF);
+      if ((i & 3) >= 2 && (double)v < b[i]) v = std::nextafter(v, HUGE_VALF);
+      f[i] = v;
+    }
+    return f;
+  };
+  const std::vector<float> boxes_f = to_f32(boxes), sboxes_f = to_f32(sboxes);
   int rc;
+  if ((rc = upload(h->chunk_box_f, boxes_f.data(), boxes_f.size()))) return rc;
+  if (SG > 0 && (rc = upload(h->super_box_f, sboxes_f.data(), sboxes_f.size()))) return rc;
   if ((rc = upload(h->chunk_off, off.data(), off.size()))) return rc;
   if ((rc = upload(h->chunk_box, boxes.data(), boxes.size()))) return rc;
   if ((rc = upload(h->slot_geo, geo.data(), geo.size()))) return rc;
@@ -288,6 +304,8 @@ int rx_destroy(rx_env* h) {
                   &h->vals_in, &h->slot_n, &h->tasks})
     b->release();
   h->resets.release();
+  h->chunk_box_f.release();
+  h->super_box_f.release();
   h->dyn_waves.release();
   h->ray_waves.release();
   h->keys_in.release();
@@ -466,7 +484,8 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   rx_kargs a{};
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
-                       h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p};
+                       h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
+                       h->chunk_box_f.p, h->super_box_f.p};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;

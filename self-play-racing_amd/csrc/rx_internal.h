@@ -39,6 +39,8 @@ struct rx_track_view {
   // closest-waypoint super-chunks: RX_WP_SUPER consecutive waypoint chunks
   const int32_t* wsuper_off; // [n+1]
   const double* wsuper_box;  // [n_wsuper][4]
+  const float* chunk_box_f;  // chunk_box / super_box in float32, rounded outward (k_rays' packed-f32 box tests)
+  const float* super_box_f;
 };
 
 #define RX_WP_CHUNK 8

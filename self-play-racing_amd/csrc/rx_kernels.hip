@@ -897,7 +897,15 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
 //   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
 // (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
 // range its rounding cannot cross the threshold).  Only hit segments divide.
-__device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, double v3x, double v3y, double& best) {
+// Smallest float32 >= x (x >= 0): the f32 box tests compare against it.
+__device__ __forceinline__ float f32_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = __int_as_float(__float_as_int(f) + 1);
+  return f;
+}
+
+__device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, double v3x, double v3y, double& best,
+                                         float& bestf) {
   const double v1x = ox - g.x, v1y = oy - g.y;
   const double dotp = g.z * v3x + g.w * v3y;
   const double cross = g.z * v1y - g.w * v1x;
@@ -910,6 +918,7 @@ __device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, 
   if (hit) {
     const double t = C / D;
     best = t < best ? t : best;
+    bestf = f32_up(best);
   }
 }
 
@@ -917,16 +926,16 @@ __device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, 
 // time (each test ends in a divergent branch, so a plain loop would wait for
 // every s_load on its own).
 __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
-                                             double v3x, double v3y, double& best) {
+                                             double v3x, double v3y, double& best, float& bestf) {
   int j = j0;
   for (; j + 4 <= j1; j += 4) {
     const double4 g0 = seg[j], g1 = seg[j + 1], g2 = seg[j + 2], g3 = seg[j + 3];  // wave-uniform -> s_load
-    seg_test(g0, ox, oy, v3x, v3y, best);
-    seg_test(g1, ox, oy, v3x, v3y, best);
-    seg_test(g2, ox, oy, v3x, v3y, best);
-    seg_test(g3, ox, oy, v3x, v3y, best);
+    seg_test(g0, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g1, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g2, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g3, ox, oy, v3x, v3y, best, bestf);
   }
-  for (; j < j1; ++j) seg_test(seg[j], ox, oy, v3x, v3y, best);
+  for (; j < j1; ++j) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
 }
 
 // Chunk culling (exact; derivation in DESIGN.md §3).  The 2W boundary
@@ -943,30 +952,25 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
 // Chunks are visited outward from the wave's first car, so best tightens
 // early; envs are kept spatially sorted (write_sort_key) so a wave's cars
 // are neighbours.
-__device__ __forceinline__ bool chunk_needed(const double* __restrict__ box, double mb, double mt, double ox,
-                                             double oy, double dx, double dy, double idx_, double idy_, double best) {
-  const double x0 = box[0] - mb, y0 = box[1] - mb, x1 = box[2] + mb, y1 = box[3] + mb;
-  double lo = -mt, hi = __builtin_inf();
-  bool miss = false;
-  if (dx != 0.0) {
-    const double t1 = (x0 - ox) * idx_, t2 = (x1 - ox) * idx_;
-    lo = __builtin_fmax(lo, __builtin_fmin(t1, t2));
-    hi = __builtin_fmin(hi, __builtin_fmax(t1, t2));
-  } else {
-    miss = miss || ox < x0 || ox > x1;
-  }
-  if (dy != 0.0) {
-    const double t1 = (y0 - oy) * idy_, t2 = (y1 - oy) * idy_;
-    lo = __builtin_fmax(lo, __builtin_fmin(t1, t2));
-    hi = __builtin_fmin(hi, __builtin_fmax(t1, t2));
-  } else {
-    miss = miss || oy < y0 || oy > y1;
-  }
-  // slack for the rounding of the slab arithmetic itself
-  const double lo_s = lo - (__builtin_fabs(lo) * 0x1p-40 + 1e-9);
-  const double hi_s = hi + (__builtin_fabs(hi) * 0x1p-40 + 1e-9);
-  miss = miss || (lo_s > hi_s);
-  return !miss && (lo_s - mt < best);
+// The slab test runs in packed float32 on outward-rounded f32 boxes (x and y
+// slabs in one v_pk_add / v_pk_mul each).  Conservative by construction
+// (DESIGN.md §3): the per-lane box margin mbf adds 3(|ox|+|oy|+1)2^-24 for the
+// f32 rounding of the origin, every remaining rounding scales a slab endpoint
+// by at most 1 +- 6*2^-24, and the slack k = 2^-20 > 2 * 6*2^-24 on both the
+// empty-interval test and the entry distance absorbs it; bestf >= best.  An
+// f32 direction component of 0 gives +-inf slab bounds (NaN when the origin
+// sits on the slab plane, which fmin/fmax drop: the axis is then unconstrained).
+typedef float rx_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 nlo, rx_f2 nhi, rx_f2 id2,
+                                               float mtf, float bestf) {
+  const float4 b = *reinterpret_cast<const float4*>(box);
+  const rx_f2 t1 = (rx_f2{b.x, b.y} + nlo) * id2;
+  const rx_f2 t2 = (rx_f2{b.z, b.w} + nhi) * id2;
+  const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1.x, t2.x), __builtin_fminf(t1.y, t2.y)), -mtf);
+  const float hi = __builtin_fminf(__builtin_fmaxf(t1.x, t2.x), __builtin_fmaxf(t1.y, t2.y));
+  const float k = 0x1p-20f;
+  const bool miss = (lo - hi) > __builtin_fmaf(__builtin_fabsf(lo) + __builtin_fabsf(hi), k, 1e-6f);
+  return !miss && (__builtin_fmaf(-__builtin_fabsf(lo), k, lo) - mtf < bestf);
 }
 
 template <int A>
@@ -1010,12 +1014,13 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   rx_sincos(theta, &sn, &cs);
   const double v3x = -sn, v3y = cs;
   double best = __builtin_inf();
+  float bestf = __builtin_inff();
   const int G = a.cull_chunk;
   if (G <= 0) {
-    ray_segments(seg, 0, S_, ox, oy, v3x, v3y, best);
+    ray_segments(seg, 0, S_, ox, oy, v3x, v3y, best, bestf);
   } else {
     const int nch = (W + G - 1) / G;  // chunks per side
-    const double* __restrict__ boxes = a.tr.chunk_box + 4 * (size_t)uniform(a.tr.chunk_off[k]);
+    const float* __restrict__ fboxes = a.tr.chunk_box_f + 4 * (size_t)uniform(a.tr.chunk_off[k]);
     const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
     const double cx = sg[0], cy = sg[1], rad = sg[2], L = sg[3];
     const double ddx = ox - cx, ddy = oy - cy;
@@ -1024,8 +1029,13 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
     const double u2 = 0x1p-52;  // 2u: factor-2 safety on both bounds
     const double mt = u2 * L * (4.0 * Rr + 2.0 * T) * 1e10 + u2 * T + 1e-9;
     const double mb = u2 * (3.0 * Rr + 2.0 * L) * L * 1e10 + 1e-9;
-    const double idx_ = cs != 0.0 ? 1.0 / cs : 0.0;  // ray direction d = (cos, sin)
-    const double idy_ = sn != 0.0 ? 1.0 / sn : 0.0;
+    // float32 box-test operands (chunk_needed_f): origin, margins, inverse direction d = (cos, sin)
+    const float oxf = (float)ox, oyf = (float)oy;
+    const float mbf = (float)mb * (1.0f + 0x1p-20f) +
+                      3.0f * (__builtin_fabsf(oxf) + __builtin_fabsf(oyf) + 1.0f) * 0x1p-24f;
+    const float mtf = (float)mt * (1.0f + 0x1p-20f) + 1e-6f;
+    const rx_f2 nlo = {-(oxf + mbf), -(oyf + mbf)}, nhi = {mbf - oxf, mbf - oyf};
+    const rx_f2 id2 = {1.0f / (float)cs, 1.0f / (float)sn};
     // visit chunks outward from the wave's first car
     int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
@@ -1040,10 +1050,10 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
           ++tested;
-          const bool need = chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best);
+          const bool need = chunk_needed_f(fboxes + 4 * (side * nch + c), nlo, nhi, id2, mtf, bestf);
           if (__any(need)) {
             ++scanned;
-            ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best);
+            ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
           }
         }
       }
@@ -1054,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
       // unchanged (exactness argument of chunk_needed applies to any box that
       // contains the segments).
       const int nsup = (nch + SG - 1) / SG;
-      const double* __restrict__ sboxes = a.tr.super_box + 4 * (size_t)uniform(a.tr.super_off[k]);
+      const float* __restrict__ sboxes = a.tr.super_box_f + 4 * (size_t)uniform(a.tr.super_off[k]);
       const int u0 = uniform(c0 / SG);
       for (int s = 0; s < nsup; ++s) {
         const int off = (s + 1) >> 1;
@@ -1065,13 +1075,13 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
           ++tested;
-          if (!__any(chunk_needed(sboxes + 4 * (side * nsup + u), mb, mt, ox, oy, cs, sn, idx_, idy_, best))) continue;
+          if (!__any(chunk_needed_f(sboxes + 4 * (side * nsup + u), nlo, nhi, id2, mtf, bestf))) continue;
           for (int q = 0; q < nl; ++q) {
             const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
             ++tested;
-            if (__any(chunk_needed(boxes + 4 * (side * nch + c), mb, mt, ox, oy, cs, sn, idx_, idy_, best))) {
+            if (__any(chunk_needed_f(fboxes + 4 * (side * nch + c), nlo, nhi, id2, mtf, bestf))) {
               ++scanned;
-              ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best);
+              ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
             }
           }
         }
