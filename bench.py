@@ -168,11 +168,11 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--cull-chunk", type=int, default=12, help="raycast chunk culling (0 = brute force)")
+    ap.add_argument("--cull-chunk", type=int, default=8, help="raycast chunk culling (0 = brute force)")
     ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
     ap.add_argument("--ray-order", type=int, default=2,
                     help="raycast lane order (0 env-major, 1 ray-major, 2 direction-sorted tasks)")
-    ap.add_argument("--cull-super", type=int, default=6, help="chunks per super-chunk box (0 = one-level culling)")
+    ap.add_argument("--cull-super", type=int, default=8, help="chunks per super-chunk box (0 = one-level culling)")
     ap.add_argument("--stream-groups", type=int, default=1,
                     help="independent env groups, one HIP stream each (1 = one handle on one stream)")
     ap.add_argument("--async-probe-groups", type=int, default=4,

@@ -92,6 +92,7 @@ struct rx_env {
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   int32_t dyn_lpe = 1;
+  int32_t argmin_window = 2;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
@@ -360,6 +361,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if (h->cfg.ray_order == 2 && A * R > 16 * A)
     return fail(RX_EINVAL, "ray_order 2 supports at most 16 sensors (got %d)", R);
   h->dyn_lpe = (A == 1 && N <= RX_DYN1_SMALL_N) ? RX_DYN1_LPE_SMALL : 1;
+  if (const char* ev = getenv("RX_ARGMIN_WINDOW")) h->argmin_window = std::max(0, std::min(32, atoi(ev)));  // A/B knob
   if (const char* ev = getenv("RX_DYN1_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
     const int v = atoi(ev);
     if (A == 1 && (v == 1 || v == 2 || v == 4)) h->dyn_lpe = v;
@@ -507,6 +509,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.reset_count = h->resets.p;
   a.ray_order = h->cfg.ray_order;
   a.dyn_lpe = h->dyn_lpe;
+  a.argmin_window = h->argmin_window;
   a.slot_nenv = h->slot_n.p;
   a.tasks = h->tasks.p;
   a.tasks_out = h->cfg.ray_order == 2 ? h->tasks.p : nullptr;

@@ -79,6 +79,7 @@ struct rx_kargs {
   int32_t ray_order;          // rx_config.ray_order
   int32_t cull_super;         // leaves per super-chunk (0 = one-level culling)
   int32_t dyn_lpe;            // k_dyn1 lanes per env (1 or RX_DYN1_LPE_SMALL)
+  int32_t argmin_window;      // half-width of the closest-waypoint scan around the previous one
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;

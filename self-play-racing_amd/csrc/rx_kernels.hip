@@ -106,23 +106,39 @@ __device__ __forceinline__ void argmin_take(double d, int i, double& best, int& 
   idx = take ? i : idx;
 }
 
-// May the box [x0, y0, x1, y1] hold a waypoint at squared distance <= best[p]
-// from some point p?  The squared-distance lower bound is shrunk by 2^-46
-// relative, far beyond the few-ulp rounding of both the bound and the
-// per-waypoint distances, so "no" is safe: such a box can neither beat nor tie.
-template <int NP>
-__device__ __forceinline__ bool box_may_hold(const double* __restrict__ b, const double px[NP], const double py[NP],
-                                             const double best[NP]) {
+// May a waypoint box hold a waypoint at squared distance <= best[p] from some
+// point p of the lane?  Tested once per car, from the car centre: every point p
+// of car q lies within RX_CAR_RADIUS of the car centre c_q, so
+// dist(p, box) >= dist(c_q, box) - RX_CAR_RADIUS, and a box with
+// dist(c_q, box)^2 > T_q = (RX_CAR_RADIUS + sqrt(max_p best_p))^2 (inflated by
+// 2^-40 relative + 1e-12) can hold no waypoint at distance <= any of the car's
+// bests.  One distance bound per car instead of one per point.
+#define RX_CAR_RADIUS 2.23607  // >= |corner - centre| = sqrt(2^2 + 1^2) = 2.2360680 (car.py:26-43)
+template <int NC>
+__device__ __forceinline__ bool box_may_hold_c(const double* __restrict__ b, const double cxs[NC], const double cys[NC],
+                                               const double T[NC]) {
   const double x0 = b[0], y0 = b[1], x1 = b[2], y1 = b[3];
   bool need = false;
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const double gx = __builtin_fmax(__builtin_fmax(x0 - px[p], px[p] - x1), 0.0);
-    const double gy = __builtin_fmax(__builtin_fmax(y0 - py[p], py[p] - y1), 0.0);
-    const double lb = (gx * gx + gy * gy) * (1.0 - 0x1p-46);
-    need = need | !(lb > best[p]);
+  for (int q = 0; q < NC; ++q) {
+    const double gx = __builtin_fmax(__builtin_fmax(x0 - cxs[q], cxs[q] - x1), 0.0);
+    const double gy = __builtin_fmax(__builtin_fmax(y0 - cys[q], cys[q] - y1), 0.0);
+    need = need | !(gx * gx + gy * gy > T[q]);
   }
   return need;
+}
+
+template <int NP, int NC>
+__device__ __forceinline__ void car_thresholds(const double best[NP], double T[NC]) {
+  constexpr int PPC = NP / NC;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    double m = best[q * PPC];
+#pragma unroll
+    for (int p = q * PPC + 1; p < (q + 1) * PPC; ++p) m = __builtin_fmax(m, best[p]);
+    const double r = RX_CAR_RADIUS + __builtin_sqrt(m);
+    T[q] = (r * r) * (1.0 + 0x1p-40) + 1e-12;
+  }
 }
 
 // The same argmin with culling (exact).  Phase 1: every lane scans a window
@@ -138,9 +154,9 @@ template <int NP, int NC>
 __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, const double* __restrict__ wbox,
                                               const double* __restrict__ wsbox, int W,
                                               const double px[NP], const double py[NP], const int prev[NC],
-                                              int idx[NP], unsigned long long* counters) {
-  constexpr int PPC = NP / NC;  // points per car
-  constexpr int H = 6;
+                                              const double cxs[NC], const double cys[NC], int H, int idx[NP],
+                                              unsigned long long* counters) {
+  constexpr int PPC = NP / NC;  // points per car (the lane's points of each car)
   double best[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -169,9 +185,11 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
   const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;  // <= 64 (W <= 64 * RX_WP_CHUNK * RX_WP_SUPER)
   unsigned long long smask = 0;
+  double T[NC];
+  car_thresholds<NP, NC>(best, T);
 #pragma unroll 4
   for (int u = 0; u < nws; ++u)
-    smask |= (unsigned long long)(__any(box_may_hold<NP>(wsbox + 4 * u, px, py, best)) ? 1 : 0) << u;
+    smask |= (unsigned long long)(__any(box_may_hold_c<NC>(wsbox + 4 * u, cxs, cys, T)) ? 1 : 0) << u;
   smask = uniform64(smask);
   const int u0 = uniform(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
   int scanned = 0, tested = nws;
@@ -185,7 +203,8 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     for (int q = 0; q < nl; ++q) {
       const int c = l0 + (back ? nl - 1 - q : q);
       ++tested;
-      if (!__any(box_may_hold<NP>(wbox + 4 * c, px, py, best))) continue;
+      car_thresholds<NP, NC>(best, T);
+      if (!__any(box_may_hold_c<NC>(wbox + 4 * c, cxs, cys, T))) continue;
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
       int i = c * RX_WP_CHUNK;
@@ -343,8 +362,28 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
   return P == 0 ? v[0] : P == 1 ? v[1] : P == 2 ? v[2] : P == 3 ? v[3] : v[4];
 }
 
+// Profiling build only (-DRX_DYN_STAMPS, tools/dyn_stamps.py): per-wave
+// s_memtime stamps at phase boundaries of k_dyn1, each after a full
+// s_waitcnt so a phase includes the memory latency it waited for, written to
+// io.counters[16 + 8 * wave + j].
+#ifdef RX_DYN_STAMPS
+#define RX_STAMP(j)                                            \
+  do {                                                         \
+    __builtin_amdgcn_s_waitcnt(0);                             \
+    stamp[j] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define RX_STAMP(j) \
+  do {              \
+  } while (0)
+#endif
+
 template <int LPE>
-__device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int& e_out) {
+__device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int& e_out, double ep_out[3]) {
+#ifdef RX_DYN_STAMPS
+  unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  stamp[0] = __builtin_amdgcn_s_memtime();
+#endif
   constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
@@ -366,28 +405,36 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
   uint8_t fl = S.flags[e];
   Car c{S.x[e], S.y[e], S.angle[e], S.vx[e], S.vy[e], S.progress[e], (fl & RX_F_CRASHED) != 0};
   double last_steering = S.last_steering[e];
+  // every per-env load up front, so their latencies overlap (not one round trip per use)
+  const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
+  const float2 act = step_mode ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
+  const double last_progress = S.last_progress[e];
+  const double ep_ret0 = S.ep_return[e];
+  const int ep_len0 = S.ep_length[e];
+  const double speed_w = S.speed_weight ? S.speed_weight[e] : a.speed_weight;
+  int steps = S.steps[e];
+  RX_STAMP(1);
   bool do_reset;
   if (a.mode == RX_MODE_RESET)
     do_reset = (a.reset_mask == nullptr) || a.reset_mask[e];
   else
     do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
-  const bool stepping = (a.mode == RX_MODE_STEP) && !do_reset;
+  const bool stepping = step_mode && !do_reset;
 
   double reward = 0.0, pd = 0.0;
   bool term = false, trunc = false;
-  int steps = S.steps[e];
   // ---------------------------------------------------------------- step
   // Lanes that step run the argmin loop together; reset lanes are masked.
   bool moving = stepping && !c.crashed;
   double cs[2], cx[4], cy[4];
   double steering = 0.0;
   if (stepping) {
-    const float2 act = reinterpret_cast<const float2*>(a.io.actions)[e];
     steering = (double)clipf(act.x, -1.0f, 1.0f);  // racing_env.py:106
     double throttle = (double)clipf(act.y, 0.0f, 1.0f);
     last_steering = steering;
     if (moving) car_kinematics(c, steering, throttle, cs, cx, cy);
   }
+  RX_STAMP(2);
   if (moving) {
     const double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
     const double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
@@ -403,12 +450,14 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     }
     if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
+      const double ccx[1] = {c.x}, ccy[1] = {c.y};
       argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
-                            a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, qx, qy, prev, idx,
-                            a.io.counters);
+                            a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, qx, qy, prev, ccx, ccy,
+                            a.argmin_window, idx, a.io.counters);
     } else {
       argmin_pts<NPL>(wp, W, qx, qy, idx);
     }
+    RX_STAMP(3);
     int out = 0;  // Track.check_collision: any corner outside (track.py:163-171)
 #pragma unroll
     for (int j = 0; j < NPL; ++j) {
@@ -421,10 +470,12 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     c.progress = (double)i0 / (double)W;  // track.py:159-161
     c.crashed = out != 0;
   }
+  RX_STAMP(4);
   if (sub != 0) return;  // one lane per env from here on
+  bool ended = false;
+  double epr = 0.0, epl_d = 0.0;
   if (stepping) {
     steps += 1;
-    const double last_progress = S.last_progress[e];
     const double p = c.progress;
     pd = p - last_progress;  // racing_env.py:112-116
     if (last_progress > 0.9 && p < 0.1)
@@ -437,7 +488,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     if ((fl & RX_F_CP50) && !(fl & RX_F_CP75) && 0.75 <= p && p < 0.85) { fl |= RX_F_CP75; r += 20; }
     if (!c.crashed && pd > 0) {  // :137-140
       double ratio = rx_clip(speed_of(c.vx, c.vy) / RX_MAX_SPEED, 0.0, 1.0);
-      r += ratio * (S.speed_weight ? S.speed_weight[e] : a.speed_weight);
+      r += ratio * speed_w;
     }
     if (c.crashed) r -= 60;
     const uint8_t all_cp = RX_F_CP25 | RX_F_CP50 | RX_F_CP75;
@@ -452,17 +503,13 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     term = c.crashed || (fl & RX_F_FINISHED);
     trunc = steps >= a.max_steps;
     // RecordEpisodeStatistics.step
-    double epr = S.ep_return[e] + r;
-    int epl = S.ep_length[e] + 1;
+    epr = ep_ret0 + r;
+    const int epl = ep_len0 + 1;
+    epl_d = (double)epl;
     S.ep_return[e] = epr;
     S.ep_length[e] = epl;
-    const bool ended = term || trunc;
+    ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
-    if (ended && a.io.ep_stats) {
-      atomicAdd(&a.io.ep_stats[0], epr);
-      atomicAdd(&a.io.ep_stats[1], (double)epl);
-      atomicAdd(&a.io.ep_stats[2], 1.0);
-    }
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
     if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;  // reset AFTER the outputs
   } else if (a.io.ep_done) {
@@ -511,6 +558,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     S.flags[e] = fl;
     S.env_flags[e] = ef;
   }
+  RX_STAMP(5);
   // ---------------------------------------------------------------- outputs
   const bool wrote_step = stepping;  // reset-by-NEXT_STEP / explicit reset: reward 0, term = trunc = False
   const float rf = wrote_step ? (float)reward : 0.0f;
@@ -540,6 +588,35 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
   write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
   ang_out[0] = c.angle;
   e_out = e;
+  if (ended) {  // RecordEpisodeStatistics: summed per wave by the caller
+    ep_out[0] = epr;
+    ep_out[1] = epl_d;
+    ep_out[2] = 1.0;
+  }
+#ifdef RX_DYN_STAMPS
+  RX_STAMP(6);
+  if (a.io.counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
+    for (int j = 0; j < 7; ++j) a.io.counters[16 + 8 * wave + j] = stamp[j];
+#endif
+}
+
+// Episode statistics of the envs that ended this step, summed over the wave
+// (all 64 lanes present) and added with ONE atomic per counter per wave: per-
+// env device-scope atomics on the same three addresses serialised the launch.
+__device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const double v[3]) {
+  if (!a.io.ep_stats || !__any(v[2] != 0.0)) return;
+  double s0 = v[0], s1 = v[1], s2 = v[2];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&a.io.ep_stats[0], s0);
+    atomicAdd(&a.io.ep_stats[1], s1);
+    atomicAdd(&a.io.ep_stats[2], s2);
+  }
 }
 
 template <int LPE>
@@ -550,10 +627,16 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
-  double ang[1];
+  double ang[1], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;  // set on the lane that finishes an env (sub 0)
-  dyn1_env<LPE>(a, ang, e);
+  dyn1_env<LPE>(a, ang, e, ep);
+  add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
+#ifdef RX_DYN_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t7 = __builtin_amdgcn_s_memtime();
+  if (a.io.counters && (threadIdx.x & 63) == 0) a.io.counters[16 + 8 * wave + 7] = t7;
+#endif
 }
 
 // ============================================================ k_dyn, A == 2
@@ -619,7 +702,7 @@ __device__ __forceinline__ bool rect_intersect(const double ax[4], const double 
   return !sep;
 }
 
-__device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int& e_out) {
+__device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int& e_out, double ep_out[3]) {
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
@@ -693,9 +776,10 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       int idx[10];
       if (a.cull_chunk > 0) {
         const int prev[2] = {prev_waypoint(c[0].progress, W), prev_waypoint(c[1].progress, W)};
+        const double ccx[2] = {c[0].x, c[1].x}, ccy[2] = {c[0].y, c[1].y};
         argmin_culled<10, 2>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
-                             a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, idx,
-                             a.io.counters);
+                             a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, ccx, ccy,
+                             a.argmin_window, idx, a.io.counters);
       } else {
         argmin_pts<10>(wp, W, px, py, idx);
       }
@@ -764,10 +848,10 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
     S.ep_length[e] = epl;
     const bool ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
-    if (ended && a.io.ep_stats) {
-      atomicAdd(&a.io.ep_stats[0], epr);
-      atomicAdd(&a.io.ep_stats[1], (double)epl);
-      atomicAdd(&a.io.ep_stats[2], 1.0);
+    if (ended) {  // RecordEpisodeStatistics: summed per wave by the caller
+      ep_out[0] = epr;
+      ep_out[1] = (double)epl;
+      ep_out[2] = 1.0;
     }
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
     if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;
@@ -877,9 +961,10 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
-  double ang[2];
+  double ang[2], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;
-  dyn2_env(a, ang, e);
+  dyn2_env(a, ang, e, ep);
+  add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
 }
 

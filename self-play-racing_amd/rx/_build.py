@@ -42,28 +42,32 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile librx.so (out: another .so path, with extra -D defines: profiling variants)."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     cc = hipcc()
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
-        cmd = [cc] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if out is not None:
+            obj = os.path.splitext(out)[0] + "_" + os.path.splitext(src)[0] + ".o"
+        cmd = [cc] + FLAGS + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -90,7 +90,7 @@ def load(build_if_missing=True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = os.environ.get("RX_LIB_PATH") or _build.LIB  # override: profiling builds (tools/dyn_stamps.py)
     if not os.path.exists(path):
         if not build_if_missing:
             raise RxError(f"librx.so not built at {path} (run python -m rx._build)")

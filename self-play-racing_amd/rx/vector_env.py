@@ -56,8 +56,8 @@ class RacingVectorEnv:
     (multi_racing_env.py:50)."""
 
     def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
-                 seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=12,
-                 sort_interval=16, ray_order=None, cull_super=6):
+                 seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=8,
+                 sort_interval=16, ray_order=None, cull_super=8):
         self.L = _lib.load()
         self.device = torch.device(device) if device is not None else _default_device()
         if self.device.type != "cuda":

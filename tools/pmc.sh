@@ -6,7 +6,7 @@ set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${PMC_BENCH_ARGS:---steps 20 --warmup 2 --no-cpu-baseline --async-probe-groups 0}
+ARGS=${PMC_BENCH_ARGS:---steps 20 --warmup 2 --no-cpu-baseline --async-probe-groups 0 --ppo-updates 0}
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C -d "$OUT/$C" -o run --output-format csv -- python bench.py $ARGS \
     > "$OUT/$C.log" 2>&1 || { echo "rocprofv3 $C failed rc=$?"; tail -5 "$OUT/$C.log"; exit 1; }
