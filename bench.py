@@ -40,6 +40,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 FP64_VALU_PEAK_TF = 78.6  # MI355X FP64 vector peak (AMD spec)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each (16 lanes; FP64 FMA is
+# full rate: 1024 x 16 x 2 flop x 2.4 GHz = 78.6 TF), at 2.4 GHz
+VALU_WAVE_INST_PEAK_G = 1024 * 2.4e9 / 4 / 1e9  # 614.4 G wave-instructions/s
 RAY_FLOPS_PER_SEG = 13    # 2 sub, 3 dotp, 3 cross, 3 v1.v3, 2 div per ray x segment
 RAYS_BYTES_PER_ENV = 24 + 11 * 4   # k_rays algorithmic HBM bytes/env: read x,y,angle (f64), write 11 f32 obs
 STEP_BYTES_PER_ENV = 218           # whole step, SURVEY.md §8(d)
@@ -306,13 +309,15 @@ def main():
         value = n_total * args.steps / elapsed
         achieved_gbs = RAYS_BYTES_PER_ENV * n / (ray_ms * 1e-3) / 1e9
         achieved_tf = ray_flops_per_launch / (ray_ms * 1e-3) / 1e12
-        traffic = None
+        traffic = valu_insts = None
         pmc = os.path.join(ROOT, "profiles", "pmc_k_rays.json")
         if os.path.exists(pmc):
             try:
                 pj = json.load(open(pmc))
-                # PMC bytes are per launch: only valid for launches of the same size
-                traffic = pj.get("hbm_bytes_per_launch") if pj.get("envs_per_launch") == n else None
+                # PMC counts are per launch: only valid for launches of the same size
+                if pj.get("envs_per_launch") == n:
+                    traffic = pj.get("hbm_bytes_per_launch")
+                    valu_insts = pj.get("valu_insts_per_launch")
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -341,9 +346,18 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_env": RAYS_BYTES_PER_ENV, "envs_per_launch": n,
                          "avg_launch_ms": round(ray_ms, 5)},
-            "compute_roofline": {"bound": "valu_fp64", "kernel": "k_rays", "achieved": round(achieved_tf, 3),
-                                 "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "frac": achieved_tf / FP64_VALU_PEAK_TF,
-                                 "flops_per_launch": ray_flops_per_launch},
+            # the raycast is VALU-issue bound: wave-level VALU instructions per launch (PMC SQ_INSTS_VALU,
+            # profiles/pmc_k_rays.json) / launch time vs the chip's issue rate.  The SURVEY §8(d) algorithmic
+            # flop count assumes every segment is tested (brute force); culling skips most of them, so that
+            # rate is reported as an equivalent, not against the peak.
+            "compute_roofline": {"bound": "valu_issue", "kernel": "k_rays",
+                                 "achieved": round(valu_insts / (ray_ms * 1e-3) / 1e9, 1) if valu_insts else None,
+                                 "peak": VALU_WAVE_INST_PEAK_G, "unit": "G wave-VALU-instructions/s",
+                                 "frac": (valu_insts / (ray_ms * 1e-3) / 1e9 / VALU_WAVE_INST_PEAK_G)
+                                 if valu_insts else None,
+                                 "valu_insts_per_launch": valu_insts,
+                                 "brute_force_equiv_tflops": round(achieved_tf, 3),
+                                 "brute_force_flops_per_launch": ray_flops_per_launch},
             "kernels_ms": {"k_dyn1": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
             "gae": gae,
             "episodes_ended": ep[2],

@@ -24,6 +24,7 @@ def load(root, counter):
 def main(root):
     fetch = load(root, "FETCH_SIZE")
     write = load(root, "WRITE_SIZE")
+    valu = load(root, "SQ_INSTS_VALU")
     out = {"units": "bytes per launch (FETCH_SIZE/WRITE_SIZE are KiB in rocprofv3; x1024)",
            "note": "gfx950 FETCH_SIZE under-counts wide coalesced streaming reads by 2x (MI355X_MICROARCH.md "
                    "§HBM); these kernels read 8-byte f64 per lane, an uncalibrated width: raw counts reported, "
@@ -35,6 +36,9 @@ def main(root):
         wb = 1024 * sum(w) / len(w) if w else None
         out[k] = {"launches": max(len(f), len(w)), "fetch_bytes": fb, "write_bytes": wb,
                   "hbm_bytes_per_launch": (fb or 0) + (wb or 0), "hbm_bytes_per_launch_fetch_x2": 2 * (fb or 0) + (wb or 0)}
+        v = valu.get(k, [])
+        if v:
+            out[k]["valu_insts_per_launch"] = sum(v) / len(v)
     print(json.dumps(out, indent=1))
 
 
