@@ -339,7 +339,7 @@ def main():
                        "stream_groups": G, "envs_per_launch": n,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
-                       "kernel_timing": f"HIP events around group 0's k_dyn1 / k_rays (on its stream) on every "
+                       "kernel_timing": f"HIP events around group 0's dynamics phase / k_rays (on its stream) on every "
                                         f"{args.sample_every}th timed step",
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
@@ -358,7 +358,10 @@ def main():
                                  "valu_insts_per_launch": valu_insts,
                                  "brute_force_equiv_tflops": round(achieved_tf, 3),
                                  "brute_force_flops_per_launch": ray_flops_per_launch},
-            "kernels_ms": {"k_dyn1": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
+            # sampled steps split the step for timing: dynamics phase (k_kin1 + the REWARD half of k_step2
+            # launched alone) and the raycast alone; the production step runs REWARD and the raycast in ONE
+            # k_step2 launch, side by side
+            "kernels_ms": {"dynamics": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
             "gae": gae,
             "episodes_ended": ep[2],
             "async_stream_groups": async_probe,

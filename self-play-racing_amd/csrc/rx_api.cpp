@@ -104,6 +104,9 @@ struct rx_env {
   uint64_t dyn_calls = 0;
   // ray_order 2: direction-sorted (agent, ray) task ids, rewritten by k_dyn every step
   DevBuf<int32_t> tasks;
+  // split step (k_kin1 + k_step2): cos / sin of the stepped angles; RX_SPLIT=0 disables
+  DevBuf<double> cs_scratch;
+  bool split = true;
   // state
   bool bound = false;
   rx_state st{};
@@ -304,6 +307,7 @@ int rx_destroy(rx_env* h) {
   for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->super_off, &h->wsuper_off, &h->perm[0], &h->perm[1],
                   &h->vals_in, &h->slot_n, &h->tasks})
     b->release();
+  h->cs_scratch.release();
   h->resets.release();
   h->chunk_box_f.release();
   h->super_box_f.release();
@@ -446,6 +450,11 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       for (int qr = 0; qr < A * R; ++qr) t0[o++] = perm[i] * A * R + qr;
     if ((rc = upload(h->tasks, t0.data(), nt))) return rc;
   }
+  if (A == 1) {
+    std::vector<double> z(2 * (size_t)N, 0.0);
+    if ((rc = upload(h->cs_scratch, z.data(), z.size()))) return rc;
+  }
+  if (const char* ev = getenv("RX_SPLIT")) h->split = atoi(ev) != 0;  // A/B knob
   if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
   if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
   h->n_dyn_waves = (int32_t)dyn.size();
@@ -513,8 +522,42 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.slot_nenv = h->slot_n.p;
   a.tasks = h->tasks.p;
   a.tasks_out = h->cfg.ray_order == 2 ? h->tasks.p : nullptr;
+  a.cs_scratch = h->cs_scratch.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;
+  // Split step: k_kin1 (resets, kinematics, non-ray obs, ray-task sort), then
+  // k_step2 = the REWARD part (argmins, collision, reward, done) side by side
+  // with the raycast in ONE launch.  Single-agent STEP with next-step or no
+  // autoreset at one lane per env (same-step autoreset needs done before the
+  // observation; explicit resets and small N use the one-kernel path).
+  const bool split = h->split && mode == RX_MODE_STEP && h->cfg.n_agents == 1 && h->dyn_lpe == 1 &&
+                     h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
+  if (split) {
+    const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
+    const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
+    if (dyn && (rc = rx_launch_split(&a, RX_SPLIT_KIN, s)) != 0)
+      return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
+    a.tasks_out = nullptr;
+    if (sort) {
+      a.sort_keys = h->keys_in.p;
+      a.sort_vals = h->vals_in.p;
+    }
+    if (dyn) {
+      if ((rc = rx_launch_split(&a, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
+        return fail(RX_EHIP, "k_step2 launch failed: %s", hipGetErrorString((hipError_t)rc));
+    } else if ((rc = rx_launch_step(&a, 1, RX_PHASE_RAYS, s)) != 0) {
+      return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
+    }
+    if (sort) {  // keys written by k_step2: the new env order applies from the next step
+      size_t tmp = h->sort_tmp_bytes;
+      const int nxt = 1 - h->cur;
+      if ((rc = rx_sort_pairs(h->sort_tmp.p, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[nxt].p,
+                              h->cfg.n_envs, h->sort_bits, s)) != 0)
+        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
+      h->cur = nxt;
+    }
+    return RX_OK;
+  }
   if (phases & RX_PHASE_DYNAMICS) {
     // re-sort the env order every sort_interval dynamics launches (scheduling only)
     const bool sort = h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;

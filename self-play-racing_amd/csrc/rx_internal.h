@@ -80,6 +80,7 @@ struct rx_kargs {
   int32_t cull_super;         // leaves per super-chunk (0 = one-level culling)
   int32_t dyn_lpe;            // k_dyn1 lanes per env (1 or RX_DYN1_LPE_SMALL)
   int32_t argmin_window;      // half-width of the closest-waypoint scan around the previous one
+  double* cs_scratch;         // split step: [N][2] cos / sin of the stepped angle, k_kin1 -> k_step2
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;
@@ -87,6 +88,11 @@ struct rx_kargs {
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);
+// split step (A = 1, STEP mode, next-step / no autoreset): k_kin1, then k_step2
+#define RX_SPLIT_KIN 0
+#define RX_SPLIT_REWARD 1
+#define RX_SPLIT_REWARD_RAYS 2
+extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,

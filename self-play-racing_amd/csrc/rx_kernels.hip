@@ -155,7 +155,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
                                               const double* __restrict__ wsbox, int W,
                                               const double px[NP], const double py[NP], const int prev[NC],
                                               const double cxs[NC], const double cys[NC], int H, int idx[NP],
-                                              unsigned long long* counters) {
+                                              unsigned long long* counters, unsigned long long* stamps = nullptr) {
   constexpr int PPC = NP / NC;  // points per car (the lane's points of each car)
   double best[NP];
 #pragma unroll
@@ -182,6 +182,12 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   // loads are all in flight together -- one latency instead of one per super.
   // Needed super-chunks are then visited outward from the wave's first car and
   // their leaves tested against the running bests.
+#ifdef RX_DYN_STAMPS
+  if (stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamps[0] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   const int nwc = (W + RX_WP_CHUNK - 1) / RX_WP_CHUNK;
   const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;  // <= 64 (W <= 64 * RX_WP_CHUNK * RX_WP_SUPER)
   unsigned long long smask = 0;
@@ -191,6 +197,12 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   for (int u = 0; u < nws; ++u)
     smask |= (unsigned long long)(__any(box_may_hold_c<NC>(wsbox + 4 * u, cxs, cys, T)) ? 1 : 0) << u;
   smask = uniform64(smask);
+#ifdef RX_DYN_STAMPS
+  if (stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamps[1] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   const int u0 = uniform(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
   int scanned = 0, tested = nws;
   for (int s = 0; s < nws; ++s) {
@@ -378,14 +390,27 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
   } while (0)
 #endif
 
-template <int LPE>
-__device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int& e_out, double ep_out[3]) {
+// Which part of RacingEnv.step a dyn1_env instance runs.  FULL: everything
+// (k_dyn1).  The split step (k_kin1 then k_step2; rx_api.cpp)
+// lets the raycast run concurrently with the expensive half: KIN = resets,
+// actions, Car.update's kinematics, the non-ray obs columns and the ray-task
+// sort -- all the raycast needs -- and REWARD = the closest-waypoint argmins,
+// wall collision, progress, reward, done and episode statistics of the envs
+// KIN stepped (KIN marks the envs it reset with RX_EF_RESET_NOW; REWARD skips
+// and clears them).  The arithmetic is the same code either way.
+#define RX_PART_FULL 0
+#define RX_PART_KIN 1
+#define RX_PART_REWARD 2
+#define RX_EF_RESET_NOW 2u
+
+template <int LPE, int PART>
+__device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3]) {
+  constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
 #ifdef RX_DYN_STAMPS
-  unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   stamp[0] = __builtin_amdgcn_s_memtime();
 #endif
   constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
-  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
   const int lane = (threadIdx.x & 63) / LPE;  // env slot in the wave
@@ -404,18 +429,27 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
   uint8_t ef = S.env_flags[e];
   uint8_t fl = S.flags[e];
   Car c{S.x[e], S.y[e], S.angle[e], S.vx[e], S.vy[e], S.progress[e], (fl & RX_F_CRASHED) != 0};
-  double last_steering = S.last_steering[e];
+  double last_steering = REW ? 0.0 : S.last_steering[e];
   // every per-env load up front, so their latencies overlap (not one round trip per use)
   const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
-  const float2 act = step_mode ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
-  const double last_progress = S.last_progress[e];
-  const double ep_ret0 = S.ep_return[e];
-  const int ep_len0 = S.ep_length[e];
-  const double speed_w = S.speed_weight ? S.speed_weight[e] : a.speed_weight;
-  int steps = S.steps[e];
+  const float2 act =
+      (step_mode && !REW) ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
+  const double last_progress = KIN ? 0.0 : S.last_progress[e];
+  const double ep_ret0 = KIN ? 0.0 : S.ep_return[e];
+  const int ep_len0 = KIN ? 0 : S.ep_length[e];
+  const double speed_w = KIN ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);
+  int steps = S.steps[e];  // REWARD: already advanced by KIN
+  double cs[2] = {0.0, 0.0};
+  if (REW) {
+    const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[e];
+    cs[0] = sc.x;
+    cs[1] = sc.y;
+  }
   RX_STAMP(1);
   bool do_reset;
-  if (a.mode == RX_MODE_RESET)
+  if (REW)
+    do_reset = (ef & RX_EF_RESET_NOW) != 0;
+  else if (a.mode == RX_MODE_RESET)
     do_reset = (a.reset_mask == nullptr) || a.reset_mask[e];
   else
     do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
@@ -426,16 +460,16 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
   // ---------------------------------------------------------------- step
   // Lanes that step run the argmin loop together; reset lanes are masked.
   bool moving = stepping && !c.crashed;
-  double cs[2], cx[4], cy[4];
-  double steering = 0.0;
-  if (stepping) {
-    steering = (double)clipf(act.x, -1.0f, 1.0f);  // racing_env.py:106
-    double throttle = (double)clipf(act.y, 0.0f, 1.0f);
+  double cx[4], cy[4];
+  if (!REW && stepping) {
+    const double steering = (double)clipf(act.x, -1.0f, 1.0f);  // racing_env.py:106
+    const double throttle = (double)clipf(act.y, 0.0f, 1.0f);
     last_steering = steering;
     if (moving) car_kinematics(c, steering, throttle, cs, cx, cy);
   }
+  if (REW && moving) corners(c.x, c.y, cs[0], cs[1], cx, cy);  // car.py:26-43 of the stepped state
   RX_STAMP(2);
-  if (moving) {
+  if (!KIN && moving) {
     const double px[5] = {c.x, cx[0], cx[1], cx[2], cx[3]};
     const double py[5] = {c.y, cy[0], cy[1], cy[2], cy[3]};
     // this lane's points: P = sub + LPE*j (point 0 = centre, 1..4 = corners);
@@ -453,11 +487,15 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
       const double ccx[1] = {c.x}, ccy[1] = {c.y};
       argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
                             a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, qx, qy, prev, ccx, ccy,
-                            a.argmin_window, idx, a.io.counters);
+                            a.argmin_window, idx, a.io.counters
+#ifdef RX_DYN_STAMPS
+                            , stamp + 3
+#endif
+      );
     } else {
       argmin_pts<NPL>(wp, W, qx, qy, idx);
     }
-    RX_STAMP(3);
+    RX_STAMP(5);
     int out = 0;  // Track.check_collision: any corner outside (track.py:163-171)
 #pragma unroll
     for (int j = 0; j < NPL; ++j) {
@@ -470,12 +508,12 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     c.progress = (double)i0 / (double)W;  // track.py:159-161
     c.crashed = out != 0;
   }
-  RX_STAMP(4);
+  RX_STAMP(6);
   if (sub != 0) return;  // one lane per env from here on
   bool ended = false;
   double epr = 0.0, epl_d = 0.0;
-  if (stepping) {
-    steps += 1;
+  if (!REW && stepping) steps += 1;
+  if (!KIN && stepping) {
     const double p = c.progress;
     pd = p - last_progress;  // racing_env.py:112-116
     if (last_progress > 0.9 && p < 0.1)
@@ -511,12 +549,12 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
-    if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;  // reset AFTER the outputs
-  } else if (a.io.ep_done) {
+    if (FULL && ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;  // reset AFTER the outputs
+  } else if (!REW && !stepping && a.io.ep_done) {
     a.io.ep_done[e] = 0;
   }
   // info of the stepped state (racing_env.py:77-84,156-159)
-  if (a.io.info) {
+  if ((FULL || (REW && stepping)) && a.io.info) {
     double* inf = a.io.info + (size_t)e * RX_INFO_W;
     inf[RX_INFO_SPEED] = speed_of(c.vx, c.vy);
     inf[RX_INFO_PROGRESS] = (fl & RX_F_FINISHED) ? 1.0 : c.progress;
@@ -524,7 +562,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     inf[RX_INFO_PLACEMENT] = 0.0;
   }
   // ---------------------------------------------------------------- reset
-  if (do_reset) {  // RacingEnv.reset + Car.reset, racing_env.py:86-102, car.py:17-24
+  if (!REW && do_reset) {  // RacingEnv.reset + Car.reset, racing_env.py:86-102, car.py:17-24
     c.x = meta[0];
     c.y = meta[1];
     c.angle = meta[2];
@@ -536,6 +574,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     steps = 0;
     last_steering = 0.0;
     ef &= (uint8_t)~RX_EF_PENDING_RESET;
+    if (KIN) ef |= RX_EF_RESET_NOW;
     S.ep_return[e] = 0.0;
     S.ep_length[e] = 0;
     if (a.io.info && (a.mode == RX_MODE_RESET || a.autoreset == RX_AUTORESET_NEXT_STEP)) {
@@ -543,9 +582,11 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
       inf[RX_INFO_SPEED] = 0.0;
       inf[RX_INFO_PROGRESS] = 0.0;
       inf[RX_INFO_PROGRESS_DELTA] = 0.0;
+      if (KIN) inf[RX_INFO_PLACEMENT] = 0.0;
     }
   }
-  if (stepping || do_reset) {
+  if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
+  if (FULL && (stepping || do_reset)) {
     S.x[e] = c.x;
     S.y[e] = c.y;
     S.angle[e] = c.angle;
@@ -558,18 +599,45 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     S.flags[e] = fl;
     S.env_flags[e] = ef;
   }
-  RX_STAMP(5);
+  if (KIN && (stepping || do_reset)) {
+    S.x[e] = c.x;
+    S.y[e] = c.y;
+    S.angle[e] = c.angle;
+    S.vx[e] = c.vx;
+    S.vy[e] = c.vy;
+    S.last_steering[e] = last_steering;
+    S.steps[e] = steps;
+    if (moving) reinterpret_cast<double2*>(a.cs_scratch)[e] = make_double2(cs[0], cs[1]);
+    if (do_reset) {
+      S.progress[e] = 0.0;
+      S.last_progress[e] = 0.0;
+      S.flags[e] = fl;
+      S.env_flags[e] = ef;
+    }
+  }
+  if (REW && (stepping || do_reset)) {
+    if (stepping) {
+      S.progress[e] = c.progress;
+      S.last_progress[e] = c.progress;  // racing_env.py:165
+      S.flags[e] = fl;
+    }
+    S.env_flags[e] = ef;
+  }
+  RX_STAMP(7);
   // ---------------------------------------------------------------- outputs
-  const bool wrote_step = stepping;  // reset-by-NEXT_STEP / explicit reset: reward 0, term = trunc = False
-  const float rf = wrote_step ? (float)reward : 0.0f;
-  if (a.io.reward) a.io.reward[e] = rf;
-  if (a.io.reward64) a.io.reward64[e] = wrote_step ? reward : 0.0;
-  const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
-  if (a.io.terminated) a.io.terminated[e] = t_out;
-  if (a.io.truncated) a.io.truncated[e] = u_out;
-  if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  // reset-by-NEXT_STEP / explicit reset: reward 0, term = trunc = False
+  if (FULL || (REW && stepping) || (KIN && do_reset)) {
+    const bool wrote_step = stepping;
+    const float rf = wrote_step ? (float)reward : 0.0f;
+    if (a.io.reward) a.io.reward[e] = rf;
+    if (a.io.reward64) a.io.reward64[e] = wrote_step ? reward : 0.0;
+    const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
+    if (a.io.terminated) a.io.terminated[e] = t_out;
+    if (a.io.truncated) a.io.truncated[e] = u_out;
+    if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  }
   // non-ray observation columns of the CURRENT state (racing_env.py:58-75)
-  {
+  if (!REW) {
     double s, co;
     if (moving && !do_reset) {  // car_kinematics already evaluated sin/cos of this angle
       co = cs[0];
@@ -585,18 +653,20 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, double* ang_out, int
     o[2] = (float)rx_clip(0.0 / 3.0, -1.0, 1.0);  // angular_velocity is always 0
     o[3] = (float)last_steering;
   }
-  write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
-  ang_out[0] = c.angle;
-  e_out = e;
+  if (!KIN) write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
+  if (!REW) {
+    ang_out[0] = c.angle;
+    e_out = e;
+  }
   if (ended) {  // RecordEpisodeStatistics: summed per wave by the caller
     ep_out[0] = epr;
     ep_out[1] = epl_d;
     ep_out[2] = 1.0;
   }
 #ifdef RX_DYN_STAMPS
-  RX_STAMP(6);
+  RX_STAMP(8);
   if (a.io.counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
-    for (int j = 0; j < 7; ++j) a.io.counters[16 + 8 * wave + j] = stamp[j];
+    for (int j = 0; j < 9; ++j) a.io.counters[16 + 12 * wave + j] = stamp[j];
 #endif
 }
 
@@ -619,7 +689,8 @@ __device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const doubl
   }
 }
 
-template <int LPE>
+// k_dyn1 (PART = FULL) and k_kin1 (PART = KIN): 4 waves per workgroup.
+template <int LPE, int PART>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
@@ -629,13 +700,13 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   if (sorting) cnt[threadIdx.x & 63] = 0;
   double ang[1], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;  // set on the lane that finishes an env (sub 0)
-  dyn1_env<LPE>(a, ang, e, ep);
-  add_episode_stats(a, ep);
+  dyn1_env<LPE, PART>(a, wave, ang, e, ep);
+  if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
 #ifdef RX_DYN_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t7 = __builtin_amdgcn_s_memtime();
-  if (a.io.counters && (threadIdx.x & 63) == 0) a.io.counters[16 + 8 * wave + 7] = t7;
+  if (a.io.counters && (threadIdx.x & 63) == 0) a.io.counters[16 + 12 * wave + 9] = t7;
 #endif
 }
 
@@ -1059,8 +1130,7 @@ __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx
 }
 
 template <int A>
-__global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
-  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+__device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
   const rx_wave we = a.ray_waves[wave];
   const int lane = threadIdx.x & 63;
@@ -1205,6 +1275,34 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   a.io.obs[(size_t)i * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 
+template <int A>
+__global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
+  rays_body<A>(a, uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+}
+
+// Second kernel of the split step (A = 1, rx_api.cpp): one wave per
+// workgroup; workgroups [0, n_rw) run the REWARD part of RacingEnv.step for
+// dynamics wave blockIdx (n_rw = n_dyn_waves rounded up to 8, so the raycast
+// waves keep their XCD placement), the rest cast rays for ray wave
+// blockIdx - n_rw.  The two halves share no data they write (REWARD reads the
+// stepped positions k_kin1 wrote; the raycast reads them and, as an ordering
+// hint only, progress), so they run side by side: the latency-bound argmin
+// hides under the VALU-bound raycast.
+#ifndef RX_STEP2_MINW
+#define RX_STEP2_MINW 8  // min waves per SIMD: caps VGPRs at 64 so the raycast half keeps full occupancy (some spills in the REWARD half)
+#endif
+__global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_rw) {
+  const int b = uniform((int)blockIdx.x);
+  if (b < n_rw) {
+    double ang[1], ep[3] = {0.0, 0.0, 0.0};
+    int e = -1;
+    dyn1_env<1, RX_PART_REWARD>(a, b, ang, e, ep);
+    add_episode_stats(a, ep);
+    return;
+  }
+  rays_body<1>(a, b - n_rw);
+}
+
 // ============================================================ GAE
 // PPO.compute_advantages, agent/ppo.py:134-154: float32, no FMA, lane = env.
 __global__ __launch_bounds__(256) void k_gae(int T, int N, const float* __restrict__ r, const float* __restrict__ v,
@@ -1284,16 +1382,28 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 }  // namespace
 
 // ------------------------------------------------------------ launchers
+extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s) {
+  const int n_rw = (a->n_dyn_waves + 7) / 8 * 8;
+  if (part == RX_SPLIT_KIN) {
+    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3((a->n_dyn_waves + 3) / 4), dim3(256), 0, s, *a);
+  } else if (part == RX_SPLIT_REWARD) {
+    hipLaunchKernelGGL(k_step2, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
+  } else {  // RX_SPLIT_REWARD_RAYS: both halves in one launch
+    hipLaunchKernelGGL(k_step2, dim3(n_rw + a->n_ray_waves), dim3(64), 0, s, *a, n_rw);
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s) {
   const dim3 blk(256);
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
     if (n_agents == 1 && a->dyn_lpe == 4)
-      hipLaunchKernelGGL(k_dyn1<4>, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<4, RX_PART_FULL>), grd, blk, 0, s, *a);
     else if (n_agents == 1 && a->dyn_lpe == 2)
-      hipLaunchKernelGGL(k_dyn1<2>, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<2, RX_PART_FULL>), grd, blk, 0, s, *a);
     else if (n_agents == 1)
-      hipLaunchKernelGGL(k_dyn1<1>, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<1, RX_PART_FULL>), grd, blk, 0, s, *a);
     else
       hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
   }
@@ -1304,11 +1414,16 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
       const int v = e ? atoi(e) : 1;
       return (v == 1 || v == 2 || v == 4) ? v : 1;
     }();
+    // RX_RAYS_LDS (A/B knob): dynamic LDS bytes per workgroup, to cap the raycast's occupancy
+    static const int lds = [] {
+      const char* e = getenv("RX_RAYS_LDS");
+      return e ? atoi(e) : 0;
+    }();
     const dim3 rgrd((a->n_ray_waves + wpb - 1) / wpb), rblk(64 * wpb);
     if (n_agents == 1)
-      hipLaunchKernelGGL(k_rays<1>, rgrd, rblk, 0, s, *a);
+      hipLaunchKernelGGL(k_rays<1>, rgrd, rblk, lds, s, *a);
     else
-      hipLaunchKernelGGL(k_rays<2>, rgrd, rblk, 0, s, *a);
+      hipLaunchKernelGGL(k_rays<2>, rgrd, rblk, lds, s, *a);
   }
   return (int)hipGetLastError();
 }

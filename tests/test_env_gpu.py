@@ -29,6 +29,17 @@ def rx():
     return ve
 
 
+@pytest.fixture(params=["default", "split"])
+def dyn_path(request, monkeypatch):
+    """Run a test on the default kernel choice (one k_dyn1 at <= 8,192 envs)
+    and on the split step (k_kin1 + k_step2: REWARD half beside the raycast),
+    which librx uses at one lane per env -- forced here via RX_DYN1_LPE=1."""
+    if request.param == "split":
+        monkeypatch.setenv("RX_DYN1_LPE", "1")
+        monkeypatch.setenv("RX_SPLIT", "1")
+    return request.param
+
+
 def _venv(rx, golden, tracks, n_agents=1, **kw):
     cps = [golden.tracks[k]["cp"] if golden.tracks[k]["label"] != "default" else None for k in tracks]
     ws = [golden.tracks[k]["width"] for k in tracks]
@@ -52,7 +63,7 @@ def _inject(v, st):
     v.set_state(env_flags=np.zeros(v.num_envs, np.uint8))
 
 
-def test_single_step_vs_golden_and_oracle(rx, golden, oracle_dev):
+def test_single_step_vs_golden_and_oracle(rx, golden, oracle_dev, dyn_path):
     step = golden["step_single"]
     n = len(step["x"])
     v = _venv(rx, golden, step["track"], autoreset="disabled")
@@ -98,7 +109,7 @@ def test_single_step_vs_golden_and_oracle(rx, golden, oracle_dev):
     assert np.array_equal(info[:, :3], o_info)
 
 
-def test_single_trajectories_vs_golden(rx, golden):
+def test_single_trajectories_vs_golden(rx, golden, dyn_path):
     tr = golden["traj_single"]
     tracks = list(tr["track"])
     v = _venv(rx, golden, tracks, autoreset="disabled")
@@ -126,7 +137,7 @@ def test_single_trajectories_vs_golden(rx, golden):
     assert worst <= OBS_TOL
 
 
-def test_random_rollout_bit_exact_vs_oracle_dev(rx, golden, oracle_dev):
+def test_random_rollout_bit_exact_vs_oracle_dev(rx, golden, oracle_dev, dyn_path):
     """600 steps of random play on 2048 envs over all 21 golden tracks, next-step
     autoreset included: the kernels and the device-libm oracle must stay
     bit-identical at every step (long-horizon exactness)."""
@@ -215,7 +226,7 @@ def test_multi_reset_slots(rx, golden):
         del first
 
 
-def test_next_step_autoreset_semantics(rx, golden):
+def test_next_step_autoreset_semantics(rx, golden, dyn_path):
     """The step after a terminal one: reset obs, reward 0, terminated = truncated = False."""
     v = _venv(rx, golden, [0] * 64, autoreset="next_step")
     obs0 = v.reset_device().clone()
@@ -234,7 +245,7 @@ def test_next_step_autoreset_semantics(rx, golden):
     assert (v.state["steps"] == 0).all()
 
 
-def test_episode_statistics(rx, golden):
+def test_episode_statistics(rx, golden, dyn_path):
     v = _venv(rx, golden, list(range(8)) * 8, autoreset="next_step")
     v.reset_device()
     ret = torch.zeros(64, dtype=torch.float64, device="cuda")
@@ -256,7 +267,7 @@ def test_episode_statistics(rx, golden):
     assert abs(s[0] - sums[0]) < 1e-6 * max(1.0, abs(sums[0])) and s[1] == sums[1]
 
 
-def test_numpy_surface(rx, golden):
+def test_numpy_surface(rx, golden, dyn_path):
     v = _venv(rx, golden, [0, 1, 2, 3], autoreset="next_step")
     obs, infos = v.reset()
     assert obs.shape == (4, 15) and obs.dtype == np.float32
@@ -371,3 +382,32 @@ def test_dyn_lanes_per_env_paths_agree(rx, golden):
         assert torch.equal(ob[:n_small], os_) and torch.equal(rb[:n_small], rs) and torch.equal(db[:n_small], ds), t
     big.close()
     small.close()
+
+
+@pytest.mark.parametrize("autoreset", ["next_step", "disabled"])
+def test_split_step_equals_one_kernel_step(rx, golden, monkeypatch, autoreset):
+    """The split step (k_kin1 + fused REWARD/raycast k_step2) == the one-kernel
+    step bit for bit: obs, rewards (f32 and f64), masks, info, episode
+    statistics and the whole f64 state, over 300 steps of random play."""
+    monkeypatch.setenv("RX_DYN1_LPE", "1")
+    N = 2048
+    tracks = np.arange(N) % golden.n_tracks
+    monkeypatch.setenv("RX_SPLIT", "0")
+    va = _venv(rx, golden, tracks, autoreset=autoreset)
+    monkeypatch.setenv("RX_SPLIT", "1")
+    vb = _venv(rx, golden, tracks, autoreset=autoreset)
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(17)
+    for t in range(300):
+        a = torch.rand((N, 2), device="cuda", generator=g) * torch.tensor([2.4, 1.4], device="cuda") - torch.tensor(
+            [1.2, 0.2], device="cuda")
+        oa, ra, da = va.step_device(a, full_info=True)
+        ob, rb, db = vb.step_device(a, full_info=True)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        for k in ("reward64", "terminated", "truncated", "info", "ep_done"):
+            assert torch.equal(va.buf[k], vb.buf[k]), (t, k)
+    sa, sb = va.get_state(), vb.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    ea, eb = va.episode_stats(), vb.episode_stats()  # atomics: the f64 sum order is not fixed
+    assert ea[1:] == eb[1:] and ea[0] == pytest.approx(eb[0], rel=1e-12)

@@ -4,9 +4,9 @@
     python tools/dyn_stamps.py [N]        # on the GPU box: per-phase cycles per wave
 
 Phases (k_dyn1, stamps after a full s_waitcnt): 0->1 wave record, perm and
-state loads; 1->2 dynamics (sincos); 2->3 closest-waypoint argmins; 3->4
-wall collision; 4->5 reward / done / state stores; 5->6 outputs; 6->7 ray
-task sort.  Profiling variant only; the product library has no stamps.
+state loads; 1->2 dynamics (sincos); 2->3 argmin window scan; 3->4 waypoint
+super-chunk tests; 4->5 leaf visits; 5->6 wall collision; 6->7 reward / done /
+state stores; 7->8 outputs; 8->9 episode stats + ray task sort.  Profiling variant only; the product library has no stamps.
 """
 import json
 import os
@@ -40,19 +40,19 @@ for _ in range(40):
     env.step_device(torch.rand((N, 2), generator=g, device="cuda") * scale + shift)
 n_waves = (N + 63) // 64
 res = []
-env.counters = torch.zeros(16 + 8 * n_waves, dtype=torch.int64, device="cuda")
+env.counters = torch.zeros(16 + 12 * n_waves, dtype=torch.int64, device="cuda")
 env._io_cache.clear()  # the cached io structs hold the counters pointer
 for rep in range(5):
     env.counters.zero_()
     env.step_device(torch.rand((N, 2), generator=g, device="cuda") * scale + shift, phases=1)
     torch.cuda.synchronize()
-    st = env.counters[16:].view(n_waves, 8).cpu().numpy().astype(np.float64)
+    st = env.counters[16:].view(n_waves, 12)[:, :10].cpu().numpy().astype(np.float64)
     ok = (st > 0).all(axis=1)
     d = np.diff(st[ok], axis=1)
-    span = st[ok, 7].max() - st[ok, 0].min()
+    span = st[ok, 9].max() - st[ok, 0].min()
     res.append({"waves": int(ok.sum()), "phase_cycles_median": np.median(d, axis=0).round(0).tolist(),
                 "phase_cycles_mean": d.mean(axis=0).round(0).tolist(),
-                "wave_total_median": float(np.median(st[ok, 7] - st[ok, 0])),
+                "wave_total_median": float(np.median(st[ok, 9] - st[ok, 0])),
                 "launch_span_cycles": float(span),
                 "start_spread_cycles": float(np.percentile(st[ok, 0], 99) - st[ok, 0].min())})
 print(json.dumps(res[-1], indent=1))
