@@ -43,8 +43,12 @@ struct rx_track_view {
   const float* super_box_f;
 };
 
-#define RX_WP_CHUNK 8
+#ifndef RX_WP_CHUNK
+#define RX_WP_CHUNK 8  // waypoints per closest-waypoint culling leaf
+#endif
+#ifndef RX_WP_SUPER
 #define RX_WP_SUPER 4  // leaves per waypoint super-chunk
+#endif
 
 // lanes per env in k_dyn1 (a dynamics wave holds 64 / lpe envs): 4 when there
 // are few envs (latency-bound: more lanes per env shorten the chain), 1 when
