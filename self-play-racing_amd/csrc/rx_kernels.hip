@@ -1288,12 +1288,20 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 // stepped positions k_kin1 wrote; the raycast reads them and, as an ordering
 // hint only, progress), so they run side by side: the latency-bound argmin
 // hides under the VALU-bound raycast.
+#ifndef RX_REWARD_PRIO
+#define RX_REWARD_PRIO 0
+#endif
 #ifndef RX_STEP2_MINW
 #define RX_STEP2_MINW 8  // min waves per SIMD: caps VGPRs at 64 so the raycast half keeps full occupancy (some spills in the REWARD half)
 #endif
 __global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
   if (b < n_rw) {
+#if RX_REWARD_PRIO > 0
+    // issue priority over the raycast waves sharing the SIMD: the REWARD
+    // waves are long latency chains that would otherwise finish last
+    __builtin_amdgcn_s_setprio(RX_REWARD_PRIO);
+#endif
     double ang[1], ep[3] = {0.0, 0.0, 0.0};
     int e = -1;
     dyn1_env<1, RX_PART_REWARD>(a, b, ang, e, ep);
