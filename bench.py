@@ -21,8 +21,8 @@ optimizer step over RCCL).  With N GPUs
 N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
 
 Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel
-(k_rays, the raycast), timed live with HIP events on the stream the kernels
-run on; ``cpu_baseline`` times oracle/np_env.py -- the reference's NumPy step
+(k_rays, the raycast), timed live from per-wave device wall-clock stamps
+(rx_profile: first wave start to last wave end, the span rocprofv3 reports); ``cpu_baseline`` times oracle/np_env.py -- the reference's NumPy step
 restated (bit-exact vs the reference's golden vectors) -- on this host.
 """
 import argparse
@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--async-probe-groups", type=int, default=4,
                     help="after the timed region, also time the same workload as this many stream groups "
                          "(reported as 'async_stream_groups'; 0 = skip)")
+    ap.add_argument("--no-kernel-profile", action="store_true",
+                    help="time without per-launch timestamp events (no per-kernel durations)")
     ap.add_argument("--sample-every", type=int, default=8,
                     help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
     ap.add_argument("--ppo-updates", type=int, default=2,
@@ -250,12 +252,15 @@ def main():
                 with torch.cuda.stream(streams[g]):
                     if ev is None or g:  # the production call: one rx_step
                         envs[g].step_device(acts[g][k])
-                    else:  # instrumented (group 0): the two phases around HIP events on its stream
-                        ev[0].record()
+                    elif ev == "step":  # recorded production step (group 0)
+                        envs[g].profile(2)
+                        envs[g].step_device(acts[g][k])
+                        envs[g].profile(0)
+                    else:  # recorded split step (group 0): dynamics phase, then the raycast on its own
+                        envs[g].profile(2)
                         envs[g].step_device(acts[g][k], phases=1)
-                        ev[1].record()
                         envs[g].step_device(acts[g][k], phases=2)
-                        ev[2].record()
+                        envs[g].profile(0)
         return envs, one_step, n
 
     def timed(one_step, steps, events=None):
@@ -284,13 +289,17 @@ def main():
     ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))  # one launch = group 0's envs
     for _ in range(args.warmup):
         one_step()
-    # every --sample-every'th timed step is instrumented (event records between the
-    # kernels cost ~10 us of GPU idle per step, so not every step carries them)
-    events = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-              for k in range(args.steps) if k % args.sample_every == 0}
+    # kernel durations from the dispatch packets' own timestamps (rx_profile, what rocprofv3
+    # reports) over the whole timed region; every --sample-every'th step launches the raycast
+    # on its own (dynamics phase first), so the dominant kernel has its own duration
+    half = max(1, args.sample_every // 2)
+    events = {} if args.no_kernel_profile else \
+        {k: ("split" if k % args.sample_every == 0 else "step") for k in range(args.steps) if k % half == 0}
+    env0.profile(1)
+    env0.profile(0)
     elapsed = timed(one_step, args.steps, events)
-    dyn_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events.values()]))
-    ray_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events.values()]))
+    prof = env0.profile_read()
+    ray_ms = prof["k_rays"][0] if "k_rays" in prof else float("nan")
     ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     for e in envs:
         e.close()
@@ -345,8 +354,10 @@ def main():
                        "stream_groups": G, "envs_per_launch": n,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
-                       "kernel_timing": f"HIP events around group 0's dynamics phase / k_rays (on its stream) on every "
-                                        f"{args.sample_every}th timed step",
+                       "kernel_timing": "per-wave device wall-clock stamps (rx_profile: first wave start .. last "
+                                        "wave end) of group 0's kernels on every "
+                                        f"{max(1, args.sample_every // 2)}th timed step; every "
+                                        f"{args.sample_every}th step launches the raycast on its own",
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
@@ -364,10 +375,10 @@ def main():
                                  "valu_insts_per_launch": valu_insts,
                                  "brute_force_equiv_tflops": round(achieved_tf, 3),
                                  "brute_force_flops_per_launch": ray_flops_per_launch},
-            # sampled steps split the step for timing: dynamics phase (k_kin1 + the REWARD half of k_step2
-            # launched alone) and the raycast alone; the production step runs REWARD and the raycast in ONE
-            # k_step2 launch, side by side
-            "kernels_ms": {"dynamics": round(dyn_ms, 5), "k_rays": round(ray_ms, 5)},
+            # production step = k_kin1 + k_step2 (REWARD half beside the raycast); sampled steps run
+            # k_kin1 + k_step2_reward (REWARD half alone) + k_rays (raycast alone)
+            "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
+            "kernel_launches": {k: v[1] for k, v in prof.items()},
             "gae": gae,
             "episodes_ended": ep[2],
             "async_stream_groups": async_probe,

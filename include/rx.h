@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 9
+#define RX_ABI_VERSION 10
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -182,6 +182,26 @@ int rx_step(rx_env* h, const rx_io* io, void* stream);
 #define RX_PHASE_DYNAMICS 1
 #define RX_PHASE_RAYS 2
 int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
+
+/* Kernel timing for benchmarks.  While profiling, every wave of a recorded
+ * launch stamps the device wall clock (s_memrealtime, 100 MHz, one chip-wide
+ * counter) at its start and end; a launch's duration is last end - first
+ * start: its execution span, as rocprofv3 --kernel-trace measures it, without
+ * the dispatch and end-of-kernel cache-flush time that stream events around a
+ * launch include.  rx_profile(h, 1) starts a fresh record of the kernels that
+ * rx_step / rx_reset / rx_step_phases launch (up to 256 launches; the call
+ * synchronises the device), rx_profile(h, 0) pauses recording and
+ * rx_profile(h, 2) resumes it (record selected steps only), rx_profile_read
+ * synchronises and returns per kernel kind the mean duration (ms) and the
+ * launch count.  No counterpart in the reference (it has no benchmarks). */
+#define RX_KERNEL_DYN 0    /* k_dyn1 / k_dyn2: one-kernel dynamics (reset, small N, two-car) */
+#define RX_KERNEL_RAYS 1   /* k_rays launched on its own (rx_step_phases, one-kernel step) */
+#define RX_KERNEL_KIN 2    /* k_kin1: first kernel of the split step */
+#define RX_KERNEL_STEP2 3  /* k_step2: REWARD half + raycast in one launch (split step) */
+#define RX_KERNEL_REWARD 4 /* k_step2 with the REWARD half only (rx_step_phases dynamics) */
+#define RX_KERNEL_KINDS 5
+int rx_profile(rx_env* h, int32_t enable);
+int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count);
 
 /* GAE (agent/ppo.py:134-154), float32, bit-exact lane-per-env recurrence.
  * rewards/values/dones [T][N]; next_value/next_done [N]; adv/returns [T][N]. */

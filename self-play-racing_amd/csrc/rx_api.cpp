@@ -107,6 +107,10 @@ struct rx_env {
   // split step (k_kin1 + k_step2): cos / sin of the stepped angles; RX_SPLIT=0 disables
   DevBuf<double> cs_scratch;
   bool split = true;
+  // rx_profile: per recorded launch, [RX_PROF_SLOTS] wave start + [RX_PROF_SLOTS] wave end stamps
+  bool prof = false;
+  DevBuf<unsigned long long> prof_buf;
+  std::vector<int> prof_kinds;
   // state
   bool bound = false;
   rx_state st{};
@@ -308,6 +312,7 @@ int rx_destroy(rx_env* h) {
                   &h->vals_in, &h->slot_n, &h->tasks})
     b->release();
   h->cs_scratch.release();
+  h->prof_buf.release();
   h->resets.release();
   h->chunk_box_f.release();
   h->super_box_f.release();
@@ -483,6 +488,18 @@ int rx_set_speed_weight(rx_env* h, double w) {
   return RX_OK;
 }
 
+// rx_profile: give the next launch its stamp record (nullptr when not
+// profiling or the record is full).
+static constexpr int kProfMax = 256;  // launches per record
+static int prof_stride(const rx_env* h) { return (h->n_dyn_waves + 7) / 8 * 8 + h->n_ray_waves + 8; }
+static void prof_arm(rx_env* h, rx_kargs& a, int kind) {
+  a.prof_ts = nullptr;
+  if (!h->prof || !h->prof_buf.p || (int)h->prof_kinds.size() >= kProfMax) return;
+  a.prof_stride = prof_stride(h);
+  a.prof_ts = h->prof_buf.p + (size_t)h->prof_kinds.size() * 2 * a.prof_stride;
+  h->prof_kinds.push_back(kind);
+}
+
 static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
   if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
   if (!h) return fail(RX_EINVAL, "null handle");
@@ -535,19 +552,26 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (split) {
     const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
     const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
-    if (dyn && (rc = rx_launch_split(&a, RX_SPLIT_KIN, s)) != 0)
-      return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
+    if (dyn) {
+      prof_arm(h, a, RX_KERNEL_KIN);
+      if ((rc = rx_launch_split(&a, RX_SPLIT_KIN, s)) != 0)
+        return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
+    }
     a.tasks_out = nullptr;
     if (sort) {
       a.sort_keys = h->keys_in.p;
       a.sort_vals = h->vals_in.p;
     }
     if (dyn) {
+      prof_arm(h, a, phases == 3 ? RX_KERNEL_STEP2 : RX_KERNEL_REWARD);
       if ((rc = rx_launch_split(&a, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
         return fail(RX_EHIP, "k_step2 launch failed: %s", hipGetErrorString((hipError_t)rc));
-    } else if ((rc = rx_launch_step(&a, 1, RX_PHASE_RAYS, s)) != 0) {
-      return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
+    } else {
+      prof_arm(h, a, RX_KERNEL_RAYS);
+      if ((rc = rx_launch_step(&a, 1, RX_PHASE_RAYS, s)) != 0)
+        return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
+    a.prof_ts = nullptr;
     if (sort) {  // keys written by k_step2: the new env order applies from the next step
       size_t tmp = h->sort_tmp_bytes;
       const int nxt = 1 - h->cur;
@@ -565,8 +589,10 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
       a.sort_keys = h->keys_in.p;
       a.sort_vals = h->vals_in.p;
     }
+    prof_arm(h, a, RX_KERNEL_DYN);
     if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_DYNAMICS, s)) != 0)
       return fail(RX_EHIP, "k_dyn launch failed: %s", hipGetErrorString((hipError_t)rc));
+    a.prof_ts = nullptr;
     if (sort) {
       size_t tmp = h->sort_tmp_bytes;
       const int nxt = 1 - h->cur;
@@ -581,8 +607,62 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     a.sort_keys = nullptr;
     a.sort_vals = nullptr;
     a.tasks_out = nullptr;
+    prof_arm(h, a, RX_KERNEL_RAYS);
     if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_RAYS, s)) != 0)
       return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
+  }
+  return RX_OK;
+}
+
+int rx_profile(rx_env* h, int32_t enable) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (enable == 1) {  // a fresh record, all stamps 0 (= no wave)
+    if (!h->assigned) return fail(RX_ESTATE, "rx_profile before rx_assign");
+    RX_HIP(hipSetDevice(h->cfg.device));
+    RX_HIP(hipDeviceSynchronize());  // no launch of the previous record may still write
+    const size_t n = (size_t)kProfMax * 2 * prof_stride(h);
+    if (h->prof_buf.n < n) {
+      h->prof_buf.release();
+      if (hipMalloc(&h->prof_buf.p, n * sizeof(unsigned long long)) != hipSuccess)
+        return fail(RX_ENOMEM, "rx_profile: stamp buffer alloc");
+      h->prof_buf.n = n;
+    }
+    RX_HIP(hipMemset(h->prof_buf.p, 0, n * sizeof(unsigned long long)));
+    h->prof_kinds.clear();
+  }
+  h->prof = enable != 0;  // 2 = resume the current record
+  return RX_OK;
+}
+
+int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count) {
+  if (!h || !mean_ms || !count) return fail(RX_EINVAL, "rx_profile_read: null argument");
+  double sum[RX_KERNEL_KINDS] = {0};
+  int32_t n[RX_KERNEL_KINDS] = {0};
+  const size_t nl = h->prof_kinds.size();
+  if (nl) {
+    RX_HIP(hipSetDevice(h->cfg.device));
+    int khz = 0;
+    RX_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device));
+    if (khz <= 0) return fail(RX_EHIP, "rx_profile_read: no wall-clock rate");
+    RX_HIP(hipDeviceSynchronize());
+    const int stride = prof_stride(h);
+    std::vector<unsigned long long> st(nl * 2 * stride);
+    RX_HIP(hipMemcpy(st.data(), h->prof_buf.p, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (size_t l = 0; l < nl; ++l) {
+      const unsigned long long* r = st.data() + l * 2 * stride;
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int i = 0; i < stride; ++i) {
+        if (r[i]) t0 = std::min(t0, r[i]);
+        t1 = std::max(t1, r[stride + i]);
+      }
+      if (t1 == 0 || t0 == ~0ull || t1 < t0) continue;  // launch with no waves
+      sum[h->prof_kinds[l]] += (double)(t1 - t0) / (double)khz;  // ticks / kHz = ms
+      ++n[h->prof_kinds[l]];
+    }
+  }
+  for (int k = 0; k < RX_KERNEL_KINDS; ++k) {
+    mean_ms[k] = n[k] ? sum[k] / n[k] : 0.0;
+    count[k] = n[k];
   }
   return RX_OK;
 }

@@ -85,6 +85,8 @@ struct rx_kargs {
   int32_t dyn_lpe;            // k_dyn1 lanes per env (1 or RX_DYN1_LPE_SMALL)
   int32_t argmin_window;      // half-width of the closest-waypoint scan around the previous one
   double* cs_scratch;         // split step: [N][2] cos / sin of the stepped angle, k_kin1 -> k_step2
+  unsigned long long* prof_ts;  // rx_profile: [2][prof_stride] per-wave start / end wall-clock stamps, or nullptr
+  int32_t prof_stride;          // waves per stamp array (>= waves of any launch)
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
   double speed_weight;
   uint64_t seed;

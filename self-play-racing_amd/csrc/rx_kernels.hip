@@ -689,6 +689,17 @@ __device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const doubl
   }
 }
 
+// rx_profile: each wave stores the 100 MHz device wall clock (s_memrealtime,
+// one chip-wide counter) when it starts and ends, at its wave index (plain
+// stores: no contention).  The host takes min(start) .. max(end) as the
+// launch's duration -- the kernel's execution span, as rocprofv3 measures it,
+// without the dispatch / cache-flush time that stream events around a launch
+// include.
+__device__ __forceinline__ void prof_mark(const rx_kargs& a, int wave, bool end) {
+  if (!a.prof_ts || (threadIdx.x & 63) != 0 || wave >= a.prof_stride) return;
+  a.prof_ts[(end ? a.prof_stride : 0) + wave] = wall_clock64();
+}
+
 // k_dyn1 (PART = FULL) and k_kin1 (PART = KIN): 4 waves per workgroup.
 template <int LPE, int PART>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
@@ -698,11 +709,13 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
+  prof_mark(a, wave, false);
   double ang[1], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;  // set on the lane that finishes an env (sub 0)
   dyn1_env<LPE, PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
+  prof_mark(a, wave, true);
 #ifdef RX_DYN_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t7 = __builtin_amdgcn_s_memtime();
@@ -1032,11 +1045,13 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
+  prof_mark(a, wave, false);
   double ang[2], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;
   dyn2_env(a, ang, e, ep);
   add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
+  prof_mark(a, wave, true);
 }
 
 // ============================================================ k_rays
@@ -1277,7 +1292,10 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
 
 template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
-  rays_body<A>(a, uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  prof_mark(a, wave, false);
+  rays_body<A>(a, wave);
+  prof_mark(a, wave, true);
 }
 
 // Second kernel of the split step (A = 1, rx_api.cpp): one wave per
@@ -1296,6 +1314,7 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 #endif
 __global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
+  prof_mark(a, b, false);
   if (b < n_rw) {
 #if RX_REWARD_PRIO > 0
     // issue priority over the raycast waves sharing the SIMD: the REWARD
@@ -1306,9 +1325,10 @@ __global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_r
     int e = -1;
     dyn1_env<1, RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
-    return;
+  } else {
+    rays_body<1>(a, b - n_rw);
   }
-  rays_body<1>(a, b - n_rw);
+  prof_mark(a, b, true);
 }
 
 // ============================================================ GAE

@@ -172,6 +172,19 @@ class RacingVectorEnv:
             _lib.ptr(self.counters) if self.counters is not None else None,
         )
 
+    def profile(self, mode=1):
+        """rx_profile: 1 = start a fresh record of kernel durations (per-wave wall-clock
+        stamps), 2 = resume recording, 0 = pause (benchmarks)."""
+        _lib.check(self.L.rx_profile(self._h, int(mode)), "rx_profile")
+
+    def profile_read(self):
+        """{kernel: (mean ms, launches)} of the launches recorded since profile(True)."""
+        import ctypes
+        ms = (ctypes.c_double * len(_lib.RX_KERNEL_NAMES))()
+        n = (ctypes.c_int32 * len(_lib.RX_KERNEL_NAMES))()
+        _lib.check(self.L.rx_profile_read(self._h, ms, n), "rx_profile_read")
+        return {k: (ms[i], n[i]) for i, k in enumerate(_lib.RX_KERNEL_NAMES) if n[i]}
+
     def enable_counters(self, on=True):
         """Per-wave culling counters (rx_io.counters): chunk tests / scans."""
         self.counters = torch.zeros(4, dtype=torch.int64, device=self.device) if on else None
