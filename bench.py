@@ -167,8 +167,8 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
@@ -184,7 +184,7 @@ def main():
                          "(reported as 'async_stream_groups'; 0 = skip)")
     ap.add_argument("--no-kernel-profile", action="store_true",
                     help="time without per-launch timestamp events (no per-kernel durations)")
-    ap.add_argument("--sample-every", type=int, default=8,
+    ap.add_argument("--sample-every", type=int, default=16,
                     help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
     ap.add_argument("--ppo-updates", type=int, default=2,
                     help="also time this many PPO updates (configs[1] per GPU; 0 = skip), reported as 'ppo_train'")

@@ -189,7 +189,7 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
  * start: its execution span, as rocprofv3 --kernel-trace measures it, without
  * the dispatch and end-of-kernel cache-flush time that stream events around a
  * launch include.  rx_profile(h, 1) starts a fresh record of the kernels that
- * rx_step / rx_reset / rx_step_phases launch (up to 256 launches; the call
+ * rx_step / rx_reset / rx_step_phases launch (up to 512 launches; the call
  * synchronises the device), rx_profile(h, 0) pauses recording and
  * rx_profile(h, 2) resumes it (record selected steps only), rx_profile_read
  * synchronises and returns per kernel kind the mean duration (ms) and the

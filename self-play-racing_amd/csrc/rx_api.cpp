@@ -490,7 +490,7 @@ int rx_set_speed_weight(rx_env* h, double w) {
 
 // rx_profile: give the next launch its stamp record (nullptr when not
 // profiling or the record is full).
-static constexpr int kProfMax = 256;  // launches per record
+static constexpr int kProfMax = 512;  // launches per record
 static int prof_stride(const rx_env* h) { return (h->n_dyn_waves + 7) / 8 * 8 + h->n_ray_waves + 8; }
 static void prof_arm(rx_env* h, rx_kargs& a, int kind) {
   a.prof_ts = nullptr;

@@ -24,7 +24,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --steps 50 --warmup 5 --no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 > "$OUT/prof.log" 2>&1; rc=$?
+    python bench.py --steps 400 --warmup 100 --no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 > "$OUT/prof.log" 2>&1; rc=$?
   echo "rocprof rc=$rc"; tail -2 "$OUT/prof.log"
   find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \; | head -20
   [ $rc -eq 0 ] || exit $rc
