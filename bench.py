@@ -26,6 +26,7 @@ Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel
 restated (bit-exact vs the reference's golden vectors) -- on this host.
 """
 import argparse
+import gc
 import json
 import os
 import random
@@ -142,10 +143,13 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
             dist.barrier()
         torch.cuda.synchronize()
     sync()
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     for _ in range(updates):
         next(it)
     sync()
+    gc.enable()
     el = time.perf_counter() - t0
     if dist:
         x = torch.tensor([el], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
@@ -268,10 +272,13 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+        gc.collect()
+        gc.disable()  # a full collection over the 65,536-track pool stalls the host for tens of ms
         t0 = time.perf_counter()
         for k in range(steps):
             one_step(events.get(k) if events else None)
         torch.cuda.synchronize()  # all streams
+        gc.enable()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()

@@ -703,7 +703,7 @@ __device__ __forceinline__ void prof_mark(const rx_kargs& a, int wave, bool end)
 // k_dyn1 (PART = FULL) and k_kin1 (PART = KIN): 4 waves per workgroup.
 template <int LPE, int PART>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
-  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   __shared__ int32_t tcnt[4][kTaskSectors];
   int32_t* cnt = tcnt[threadIdx.x >> 6];
@@ -1413,7 +1413,14 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s) {
   const int n_rw = (a->n_dyn_waves + 7) / 8 * 8;
   if (part == RX_SPLIT_KIN) {
-    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3((a->n_dyn_waves + 3) / 4), dim3(256), 0, s, *a);
+    // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
+    // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
+    static const int kin_wpb = [] {
+      const char* e = getenv("RX_KIN_WPB");  // A/B knob: waves per k_kin1 workgroup (1 or 4)
+      return e && atoi(e) == 4 ? 4 : 1;
+    }();
+    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3((a->n_dyn_waves + kin_wpb - 1) / kin_wpb), dim3(64 * kin_wpb),
+                       0, s, *a);
   } else if (part == RX_SPLIT_REWARD) {
     hipLaunchKernelGGL(k_step2, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
   } else {  // RX_SPLIT_REWARD_RAYS: both halves in one launch
