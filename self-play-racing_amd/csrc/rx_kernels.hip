@@ -129,7 +129,7 @@ __device__ __forceinline__ bool box_may_hold_c(const double* __restrict__ b, con
 }
 
 template <int NP, int NC>
-__device__ __forceinline__ void car_thresholds(const double best[NP], double T[NC]) {
+__device__ __forceinline__ void car_thresholds(const double best[NP], double T[NC], bool active = true) {
   constexpr int PPC = NP / NC;
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
@@ -137,7 +137,7 @@ __device__ __forceinline__ void car_thresholds(const double best[NP], double T[N
 #pragma unroll
     for (int p = q * PPC + 1; p < (q + 1) * PPC; ++p) m = __builtin_fmax(m, best[p]);
     const double r = RX_CAR_RADIUS + __builtin_sqrt(m);
-    T[q] = (r * r) * (1.0 + 0x1p-40) + 1e-12;
+    T[q] = active ? (r * r) * (1.0 + 0x1p-40) + 1e-12 : -1.0;  // -1: needs no box (result unused)
   }
 }
 
@@ -155,7 +155,8 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
                                               const double* __restrict__ wsbox, int W,
                                               const double px[NP], const double py[NP], const int prev[NC],
                                               const double cxs[NC], const double cys[NC], int H, int idx[NP],
-                                              unsigned long long* counters, unsigned long long* stamps = nullptr) {
+                                              unsigned long long* counters, unsigned long long* stamps = nullptr,
+                                              bool active = true) {
   constexpr int PPC = NP / NC;  // points per car (the lane's points of each car)
   double best[NP];
 #pragma unroll
@@ -192,7 +193,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   const int nws = (nwc + RX_WP_SUPER - 1) / RX_WP_SUPER;  // <= 64 (W <= 64 * RX_WP_CHUNK * RX_WP_SUPER)
   unsigned long long smask = 0;
   double T[NC];
-  car_thresholds<NP, NC>(best, T);
+  car_thresholds<NP, NC>(best, T, active);
 #pragma unroll 4
   for (int u = 0; u < nws; ++u)
     smask |= (unsigned long long)(__any(box_may_hold_c<NC>(wsbox + 4 * u, cxs, cys, T)) ? 1 : 0) << u;
@@ -215,7 +216,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     for (int q = 0; q < nl; ++q) {
       const int c = l0 + (back ? nl - 1 - q : q);
       ++tested;
-      car_thresholds<NP, NC>(best, T);
+      car_thresholds<NP, NC>(best, T, active);
       if (!__any(box_may_hold_c<NC>(wbox + 4 * c, cxs, cys, T))) continue;
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
@@ -404,7 +405,8 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
 #define RX_EF_RESET_NOW 2u
 
 template <int LPE, int PART>
-__device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3]) {
+__device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
+                                         int sub_block = 0) {
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
 #ifdef RX_DYN_STAMPS
   unsigned long long stamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -413,7 +415,10 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   constexpr int NPL = (5 + LPE - 1) / LPE;  // argmin points per lane
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
-  const int lane = (threadIdx.x & 63) / LPE;  // env slot in the wave
+  // env slot in the dynamics wave's 64-env group (a wave at LPE lanes per env
+  // covers 64 / LPE of them; sub_block picks which when the group's dynamics
+  // wave was built for one lane per env: the REWARD half at LPE = 2)
+  const int lane = (threadIdx.x & 63) / LPE + sub_block * (64 / LPE);
   const int sub = threadIdx.x & (LPE - 1);
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
@@ -859,11 +864,20 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       }
       int idx[10];
       if (a.cull_chunk > 0) {
-        const int prev[2] = {prev_waypoint(c[0].progress, W), prev_waypoint(c[1].progress, W)};
-        const double ccx[2] = {c[0].x, c[1].x}, ccy[2] = {c[0].y, c[1].y};
-        argmin_culled<10, 2>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
-                             a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, ccx, ccy,
-                             a.argmin_window, idx, a.io.counters);
+        // one culled pass per car: the envs of a wave are sorted by car 0's
+        // position, so car 1s are scattered once the cars separate -- a joint
+        // pass scanned the union of both (nearly every leaf), and every scanned
+        // leaf evaluated all 10 points.  A car that does not move (crashed) is
+        // left out of its pass (its result is not used).
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (!__any(mv[q])) continue;
+          const int prev[1] = {prev_waypoint(c[q].progress, W)};
+          const double ccx[1] = {c[q].x}, ccy[1] = {c[q].y};
+          argmin_culled<5, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
+                              a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px + 5 * q, py + 5 * q,
+                              prev, ccx, ccy, a.argmin_window, idx + 5 * q, a.io.counters, nullptr, mv[q]);
+        }
       } else {
         argmin_pts<10>(wp, W, px, py, idx);
       }
@@ -1306,6 +1320,9 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 // stepped positions k_kin1 wrote; the raycast reads them and, as an ordering
 // hint only, progress), so they run side by side: the latency-bound argmin
 // hides under the VALU-bound raycast.
+#ifndef RX_REWARD_LPE
+#define RX_REWARD_LPE 1  // lanes per env in the REWARD half (1 or 2: fewer argmin points per lane)
+#endif
 #ifndef RX_REWARD_PRIO
 #define RX_REWARD_PRIO 0
 #endif
@@ -1323,7 +1340,7 @@ __global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_r
 #endif
     double ang[1], ep[3] = {0.0, 0.0, 0.0};
     int e = -1;
-    dyn1_env<1, RX_PART_REWARD>(a, b, ang, e, ep);
+    dyn1_env<RX_REWARD_LPE, RX_PART_REWARD>(a, b / RX_REWARD_LPE, ang, e, ep, b % RX_REWARD_LPE);
     add_episode_stats(a, ep);
   } else {
     rays_body<1>(a, b - n_rw);
@@ -1411,7 +1428,7 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 
 // ------------------------------------------------------------ launchers
 extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s) {
-  const int n_rw = (a->n_dyn_waves + 7) / 8 * 8;
+  const int n_rw = (a->n_dyn_waves * RX_REWARD_LPE + 7) / 8 * 8;
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
