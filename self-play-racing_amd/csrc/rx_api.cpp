@@ -370,10 +370,13 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if (h->cfg.ray_order == 2 && A * R > 16 * A)
     return fail(RX_EINVAL, "ray_order 2 supports at most 16 sensors (got %d)", R);
   h->dyn_lpe = (A == 1 && N <= RX_DYN1_SMALL_N) ? RX_DYN1_LPE_SMALL : 1;
+  int wide_n = RX_WIDE_N;
+  if (const char* ev = getenv("RX_WIDE_N")) wide_n = atoi(ev);  // A/B knob
+  if (A == 1 && N <= wide_n) h->dyn_lpe = 64;
   if (const char* ev = getenv("RX_ARGMIN_WINDOW")) h->argmin_window = std::max(0, std::min(32, atoi(ev)));  // A/B knob
   if (const char* ev = getenv("RX_DYN1_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
     const int v = atoi(ev);
-    if (A == 1 && (v == 1 || v == 2 || v == 4)) h->dyn_lpe = v;
+    if (A == 1 && (v == 1 || v == 2 || v == 4 || v == 64)) h->dyn_lpe = v;
   }
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
@@ -491,7 +494,10 @@ int rx_set_speed_weight(rx_env* h, double w) {
 // rx_profile: give the next launch its stamp record (nullptr when not
 // profiling or the record is full).
 static constexpr int kProfMax = 512;  // launches per record
-static int prof_stride(const rx_env* h) { return (h->n_dyn_waves + 7) / 8 * 8 + h->n_ray_waves + 8; }
+static int prof_stride(const rx_env* h) {
+  const int wide = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;  // k_rays_wide: one wave per ray
+  return std::max((h->n_dyn_waves + 7) / 8 * 8 + h->n_ray_waves, wide) + 8;
+}
 static void prof_arm(rx_env* h, rx_kargs& a, int kind) {
   a.prof_ts = nullptr;
   if (!h->prof || !h->prof_buf.p || (int)h->prof_kinds.size() >= kProfMax) return;
@@ -537,8 +543,10 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.dyn_lpe = h->dyn_lpe;
   a.argmin_window = h->argmin_window;
   a.slot_nenv = h->slot_n.p;
+  a.wide = h->dyn_lpe == 64;
+  a.n_wide_tasks = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;
   a.tasks = h->tasks.p;
-  a.tasks_out = h->cfg.ray_order == 2 ? h->tasks.p : nullptr;
+  a.tasks_out = (h->cfg.ray_order == 2 && !a.wide) ? h->tasks.p : nullptr;
   a.cs_scratch = h->cs_scratch.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;

@@ -55,6 +55,10 @@ struct rx_track_view {
 // the chip is full (issue-bound: the replicated dynamics would cost more)
 #define RX_DYN1_LPE_SMALL 4
 #define RX_DYN1_SMALL_N 8192
+// at most this many single-agent envs: one env per dynamics wave and one ray
+// per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
+// are latency chains there, and 64 lanes shorten them
+#define RX_WIDE_N 2048
 
 struct rx_kargs {
   rx_track_view tr;
@@ -84,6 +88,8 @@ struct rx_kargs {
   int32_t cull_super;         // leaves per super-chunk (0 = one-level culling)
   int32_t dyn_lpe;            // k_dyn1 lanes per env (1 or RX_DYN1_LPE_SMALL)
   int32_t argmin_window;      // half-width of the closest-waypoint scan around the previous one
+  int32_t wide;               // small N: k_dyn1 one env per wave (dyn_lpe 64), k_rays_wide one ray per wave
+  int32_t n_wide_tasks;       // N * A * R ray tasks of k_rays_wide
   double* cs_scratch;         // split step: [N][2] cos / sin of the stepped angle, k_kin1 -> k_step2
   unsigned long long* prof_ts;  // rx_profile: [2][prof_stride] per-wave start / end wall-clock stamps, or nullptr
   int32_t prof_stride;          // waves per stamp array (>= waves of any launch)

@@ -248,6 +248,42 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   }
 }
 
+// Wide closest-waypoint argmin (one env per wave, dyn_lpe 64, small N): for
+// each of the car's 5 points the 64 lanes split the slot's waypoints (lane l
+// takes i = l, l + 64, ...; coalesced gathers) and combine (distance, index)
+// in a lexicographic wave minimum: the reference's first-index argmin
+// (track.py:150-152) whatever the split.  All 64 lanes must be active; lane
+// P < 5 keeps point P's index.
+__device__ __forceinline__ int argmin_wave(const double2* __restrict__ wp, int W, const double px[5],
+                                           const double py[5], int P) {
+  const int l = threadIdx.x & 63;
+  int mine = 0;
+#pragma unroll
+  for (int p = 0; p < 5; ++p) {
+    double best = __builtin_inf();
+    int bi = 0x7fffffff;
+    for (int i = l; i < W; i += 64) {  // ascending per lane: strict < keeps the first index
+      const double2 w = wp[i];
+      const double dx = w.x - px[p], dy = w.y - py[p];
+      const double d = dx * dx + dy * dy;
+      if (d < best) {
+        best = d;
+        bi = i;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      const bool take = (ob < best) | ((ob == best) & (oi < bi));
+      best = take ? ob : best;
+      bi = take ? oi : bi;
+    }
+    if (p == P) mine = bi;
+  }
+  return mine;
+}
+
 // Car.update -- environment/car.py:45-80, minus the argmins (done by the
 // caller for all cars of the lane in one pass).  Returns cos/sin of the new
 // angle and the 4 corners.
@@ -487,7 +523,9 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
       qx[j] = pick5(px, P);
       qy[j] = pick5(py, P);
     }
-    if (a.cull_chunk > 0) {
+    if constexpr (LPE == 64) {
+      idx[0] = argmin_wave(wp, W, px, py, sub < 5 ? sub : -1);
+    } else if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
       const double ccx[1] = {c.x}, ccy[1] = {c.y};
       argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
@@ -1159,6 +1197,10 @@ __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx
 }
 
 template <int A>
+__device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int q, int ray, double ox, double oy,
+                                           double v3x, double v3y, double best);
+
+template <int A>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
   const rx_wave we = a.ray_waves[wave];
@@ -1276,6 +1318,16 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
   }
+  ray_finish<A>(a, i, e, q, ray, ox, oy, v3x, v3y, best);
+}
+
+// The observation of one ray from the wall minimum `best` (inf = no hit):
+// Track.raycast's max_dist for no hit (track.py:199, uncapped otherwise),
+// the other car's edges for A = 2 (MultiTrack.raycast_with_cars,
+// multi_track.py:5-44), float32 division by 50 (racing_env.py:46,51,53).
+template <int A>
+__device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int q, int ray, double ox, double oy,
+                                           double v3x, double v3y, double best) {
   double dist = (best == __builtin_inf()) ? RX_MAX_RANGE : best;
   if (A == 2) {
     const int o = A * e + (1 - q);
@@ -1309,6 +1361,36 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   prof_mark(a, wave, false);
   rays_body<A>(a, wave);
+  prof_mark(a, wave, true);
+}
+
+// Small-N raycast (a.wide: few envs, latency-bound): one WAVE per (env,
+// agent, ray) task in env order; the 64 lanes split the slot's 2W boundary
+// segments (lane l tests j = l, l + 64, ...; coalesced loads), then a wave
+// minimum.  Brute force, so no culling argument is involved; the min over the
+// exact t of hits is order-independent, hence bit-identical to k_rays.
+template <int A>
+__global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
+  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  prof_mark(a, wave, false);
+  const int R = a.n_sensors;
+  if (wave < a.n_wide_tasks) {
+    const int iq = wave / R, ray = wave - iq * R, e = iq / A, q = iq - e * A;
+    const int k = uniform(a.st.track[e]);
+    const int wp0 = uniform(a.tr.wp_off[k]);
+    const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
+    const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+    const double ox = a.st.x[iq], oy = a.st.y[iq];
+    double sn, cs;
+    rx_sincos(a.st.angle[iq] + a.rel_angles[ray], &sn, &cs);  // racing_env.py:50
+    const double v3x = -sn, v3y = cs;
+    double best = __builtin_inf();
+    float bestf = __builtin_inff();
+    for (int j = threadIdx.x & 63; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
+    if ((threadIdx.x & 63) == 0) ray_finish<A>(a, iq, e, q, ray, ox, oy, v3x, v3y, best);
+  }
   prof_mark(a, wave, true);
 }
 
@@ -1450,7 +1532,9 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   const dim3 blk(256);
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
-    if (n_agents == 1 && a->dyn_lpe == 4)
+    if (n_agents == 1 && a->dyn_lpe == 64)
+      hipLaunchKernelGGL((k_dyn1<64, RX_PART_FULL>), grd, blk, 0, s, *a);
+    else if (n_agents == 1 && a->dyn_lpe == 4)
       hipLaunchKernelGGL((k_dyn1<4, RX_PART_FULL>), grd, blk, 0, s, *a);
     else if (n_agents == 1 && a->dyn_lpe == 2)
       hipLaunchKernelGGL((k_dyn1<2, RX_PART_FULL>), grd, blk, 0, s, *a);
@@ -1459,7 +1543,13 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else
       hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
   }
-  if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
+  if ((phases & RX_PHASE_RAYS) && a->wide) {
+    const dim3 wg((a->n_wide_tasks + 3) / 4);
+    if (n_agents == 1)
+      hipLaunchKernelGGL(k_rays_wide<1>, wg, blk, 0, s, *a);
+    else
+      hipLaunchKernelGGL(k_rays_wide<2>, wg, blk, 0, s, *a);
+  } else if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
     // waves per workgroup for the raycast (RX_RAYS_WPB: 1, 2 or 4; A/B knob)
     static const int wpb = [] {
       const char* e = getenv("RX_RAYS_WPB");

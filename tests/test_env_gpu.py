@@ -29,14 +29,21 @@ def rx():
     return ve
 
 
-@pytest.fixture(params=["default", "split"])
+@pytest.fixture(params=["default", "split", "wide"])
 def dyn_path(request, monkeypatch):
-    """Run a test on the default kernel choice (one k_dyn1 at <= 8,192 envs)
-    and on the split step (k_kin1 + k_step2: REWARD half beside the raycast),
-    which librx uses at one lane per env -- forced here via RX_DYN1_LPE=1."""
+    """Run a test on the default kernel choice for its env count, on the split
+    step (k_kin1 + k_step2: REWARD half beside the raycast), which librx uses
+    at one lane per env -- forced here via RX_DYN1_LPE=1 -- and on the small-N
+    wide kernels (one env per dynamics wave, one ray per raycast wave, brute
+    force over the lanes; librx uses them up to 2,048 envs) forced for any N."""
     if request.param == "split":
         monkeypatch.setenv("RX_DYN1_LPE", "1")
         monkeypatch.setenv("RX_SPLIT", "1")
+        monkeypatch.setenv("RX_WIDE_N", "0")
+    elif request.param == "wide":
+        monkeypatch.setenv("RX_WIDE_N", "1000000")
+    else:
+        monkeypatch.setenv("RX_WIDE_N", "0")
     return request.param
 
 
