@@ -458,8 +458,8 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       for (int qr = 0; qr < A * R; ++qr) t0[o++] = perm[i] * A * R + qr;
     if ((rc = upload(h->tasks, t0.data(), nt))) return rc;
   }
-  if (A == 1) {
-    std::vector<double> z(2 * (size_t)N, 0.0);
+  {
+    std::vector<double> z(2 * (size_t)N * A, 0.0);
     if ((rc = upload(h->cs_scratch, z.data(), z.size()))) return rc;
   }
   if (const char* ev = getenv("RX_SPLIT")) h->split = atoi(ev) != 0;  // A/B knob
@@ -550,19 +550,21 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.cs_scratch = h->cs_scratch.p;
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  // Split step: k_kin1 (resets, kinematics, non-ray obs, ray-task sort), then
-  // k_step2 = the REWARD part (argmins, collision, reward, done) side by side
-  // with the raycast in ONE launch.  Single-agent STEP with next-step or no
-  // autoreset at one lane per env (same-step autoreset needs done before the
-  // observation; explicit resets and small N use the one-kernel path).
-  const bool split = h->split && mode == RX_MODE_STEP && h->cfg.n_agents == 1 && h->dyn_lpe == 1 &&
+  // Split step: k_kin1 / k_kin2 (resets, kinematics, [car-car contact,]
+  // non-ray obs, ray-task sort), then k_step2<A> = the REWARD part (argmins,
+  // collision, reward, done) side by side with the raycast in ONE launch.  STEP
+  // with next-step or no autoreset; single-agent envs at one lane per env
+  // (same-step autoreset needs done before the observation; explicit resets
+  // and small single-agent N use the one-kernel path).
+  const int A = h->cfg.n_agents;
+  const bool split = h->split && mode == RX_MODE_STEP && (A == 2 || h->dyn_lpe == 1) &&
                      h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
   if (split) {
     const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
     const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
     if (dyn) {
       prof_arm(h, a, RX_KERNEL_KIN);
-      if ((rc = rx_launch_split(&a, RX_SPLIT_KIN, s)) != 0)
+      if ((rc = rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
         return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
     a.tasks_out = nullptr;
@@ -572,11 +574,11 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     }
     if (dyn) {
       prof_arm(h, a, phases == 3 ? RX_KERNEL_STEP2 : RX_KERNEL_REWARD);
-      if ((rc = rx_launch_split(&a, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
+      if ((rc = rx_launch_split(&a, A, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
         return fail(RX_EHIP, "k_step2 launch failed: %s", hipGetErrorString((hipError_t)rc));
     } else {
       prof_arm(h, a, RX_KERNEL_RAYS);
-      if ((rc = rx_launch_step(&a, 1, RX_PHASE_RAYS, s)) != 0)
+      if ((rc = rx_launch_step(&a, A, RX_PHASE_RAYS, s)) != 0)
         return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
     a.prof_ts = nullptr;

@@ -90,7 +90,7 @@ struct rx_kargs {
   int32_t argmin_window;      // half-width of the closest-waypoint scan around the previous one
   int32_t wide;               // small N: k_dyn1 one env per wave (dyn_lpe 64), k_rays_wide one ray per wave
   int32_t n_wide_tasks;       // N * A * R ray tasks of k_rays_wide
-  double* cs_scratch;         // split step: [N][2] cos / sin of the stepped angle, k_kin1 -> k_step2
+  double* cs_scratch;         // split step: [N*A][2] cos / sin of the stepped angle, k_kin -> k_step2
   unsigned long long* prof_ts;  // rx_profile: [2][prof_stride] per-wave start / end wall-clock stamps, or nullptr
   int32_t prof_stride;          // waves per stamp array (>= waves of any launch)
   const int32_t* slot_nenv;   // [n_tracks] envs assigned to each slot (ray-major task decode)
@@ -100,11 +100,11 @@ struct rx_kargs {
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);
-// split step (A = 1, STEP mode, next-step / no autoreset): k_kin1, then k_step2
+// split step (STEP mode, next-step / no autoreset): k_kin1 / k_kin2, then k_step2<A>
 #define RX_SPLIT_KIN 0
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
-extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s);
+extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,

@@ -829,8 +829,17 @@ __device__ __forceinline__ bool rect_intersect(const double ax[4], const double 
   return !sep;
 }
 
-__device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int& e_out, double ep_out[3]) {
-  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+// PART as for dyn1_env: FULL = the whole step (k_dyn2); the split two-car step
+// runs KIN (resets, kinematics, car-car contact, non-ray obs, ray-task sort:
+// everything the raycast reads) in k_kin2, then REWARD (argmins, wall
+// collision, rewards, placement, done, episode statistics) beside the raycast
+// in k_step2<2>.  Contact only needs the kinematic poses, so it moves to KIN;
+// KIN passes "the cars touched" to REWARD in env_flags (RX_EF_TOUCH) and the
+// stepped cos / sin of each moving car in cs_scratch[2e + q].
+#define RX_EF_TOUCH 4u
+template <int PART>
+__device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3]) {
+  constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
   const int lane = threadIdx.x & 63;
@@ -850,20 +859,28 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
   Car c[2];
   uint8_t fl[2];
   double last_steering[2];
+  double csr[2][2];  // REWARD: cos / sin of each stepped car's angle (KIN's cs_scratch)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int i = 2 * e + q;
     fl[q] = S.flags[i];
     c[q] = Car{S.x[i], S.y[i], S.angle[i], S.vx[i], S.vy[i], S.progress[i], (fl[q] & RX_F_CRASHED) != 0};
-    last_steering[q] = S.last_steering[i];
+    last_steering[q] = REW ? 0.0 : S.last_steering[i];
+    if (REW) {
+      const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[i];
+      csr[q][0] = sc.x;
+      csr[q][1] = sc.y;
+    }
   }
   bool do_reset;
-  if (a.mode == RX_MODE_RESET)
+  if (REW)
+    do_reset = (ef & RX_EF_RESET_NOW) != 0;
+  else if (a.mode == RX_MODE_RESET)
     do_reset = (a.reset_mask == nullptr) || a.reset_mask[e];
   else
     do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
   const bool stepping = (a.mode == RX_MODE_STEP) && !do_reset;
-  int steps = S.steps[e];
+  int steps = S.steps[e];  // REWARD: already advanced by KIN
   double rw[2] = {0.0, 0.0};
   int place[2] = {0, 0};
   bool term = false, trunc = false;
@@ -872,23 +889,34 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
   double sn[2], cn[2];
   bool have_sc[2] = {false, false};
   if (stepping) {
-    const float4 act = reinterpret_cast<const float4*>(a.io.actions)[e];
-    const float av[4] = {act.x, act.y, act.z, act.w};
+    float av[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (!REW) {
+      const float4 act = reinterpret_cast<const float4*>(a.io.actions)[e];
+      av[0] = act.x;
+      av[1] = act.y;
+      av[2] = act.z;
+      av[3] = act.w;
+    }
     double cx[2][4], cy[2][4], cs[2][2];
     bool mv[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // multi_racing_env.py:215-220
-      last_steering[q] = (double)clipf(av[2 * q], -1.0f, 1.0f);
-      const float thr = clipf((av[2 * q + 1] + 1.0f) / 2.0f, 0.0f, 1.0f);
       mv[q] = !c[q].crashed;
-      if (mv[q]) {
-        car_kinematics(c[q], last_steering[q], (double)thr, cs[q], cx[q], cy[q]);
-        cn[q] = cs[q][0];
-        sn[q] = cs[q][1];
-        have_sc[q] = true;
+      if (!REW) {
+        last_steering[q] = (double)clipf(av[2 * q], -1.0f, 1.0f);
+        const float thr = clipf((av[2 * q + 1] + 1.0f) / 2.0f, 0.0f, 1.0f);
+        if (mv[q]) {
+          car_kinematics(c[q], last_steering[q], (double)thr, cs[q], cx[q], cy[q]);
+          cn[q] = cs[q][0];
+          sn[q] = cs[q][1];
+          have_sc[q] = true;
+          if (KIN) reinterpret_cast<double2*>(a.cs_scratch)[2 * e + q] = make_double2(cs[q][0], cs[q][1]);
+        }
+      } else if (mv[q]) {  // car.py:26-43 of the stepped pose
+        corners(c[q].x, c[q].y, csr[q][0], csr[q][1], cx[q], cy[q]);
       }
     }
-    if (mv[0] || mv[1]) {
+    if (!KIN && (mv[0] || mv[1])) {
       double px[10], py[10];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -930,7 +958,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       }
     }
     // car-car contact, multi_racing_env.py:222-231 (corners of the current state)
-    {
+    if (!REW) {
       double ax[4], ay[4], bx[4], by[4];
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -940,6 +968,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
         }
       corners(c[0].x, c[0].y, cn[0], sn[0], ax, ay);
       corners(c[1].x, c[1].y, cn[1], sn[1], bx, by);
+      ef &= (uint8_t)~RX_EF_TOUCH;
       if (rect_intersect(ax, ay, bx, by)) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -947,9 +976,15 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
           c[q].vy *= 0.92;
           rw[q] = -5.0;
         }
+        if (KIN) ef |= RX_EF_TOUCH;
       }
+    } else if (ef & RX_EF_TOUCH) {  // touching_penalties from KIN's contact test
+      rw[0] = rw[1] = -5.0;
+      ef &= (uint8_t)~RX_EF_TOUCH;
     }
-    steps += 1;
+    if (!REW) steps += 1;
+  }
+  if (!KIN && stepping) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = 2 * e + q;
@@ -990,11 +1025,12 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       ep_out[2] = 1.0;
     }
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
-    if (ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;
-  } else if (a.io.ep_done) {
+    if (FULL && ended && a.autoreset == RX_AUTORESET_SAME_STEP) do_reset = true;
+  } else if (!REW && !stepping && a.io.ep_done) {
     a.io.ep_done[e] = 0;
   }
-  if (a.io.info) {
+  // split: KIN writes the zero info of the envs it resets, REWARD that of the stepped ones
+  if (a.io.info && (FULL || (REW && stepping) || (KIN && !stepping))) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       double* inf = a.io.info + (size_t)(2 * e + q) * RX_INFO_W;
@@ -1005,7 +1041,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       inf[RX_INFO_PLACEMENT] = keep ? (double)place[q] : 0.0;
     }
   }
-  if (do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
+  if (!REW && do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
     have_sc[0] = have_sc[1] = false;  // angles are reset below
     const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.reset_count[e]++ << 32) ^ (uint64_t)e));
     const int first = (int)(h & 1ull);  // agent_order[0] after np.random.shuffle([0, 1])
@@ -1023,11 +1059,13 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
       S.finished_step[2 * e + q] = -1;
     }
     steps = 0;
-    ef &= (uint8_t)~RX_EF_PENDING_RESET;
+    ef &= (uint8_t)~(RX_EF_PENDING_RESET | RX_EF_TOUCH);
+    if (KIN) ef |= RX_EF_RESET_NOW;
     S.ep_return[e] = 0.0;
     S.ep_length[e] = 0;
   }
-  if (stepping || do_reset) {
+  if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
+  if (FULL && (stepping || do_reset)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = 2 * e + q;
@@ -1044,19 +1082,53 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
     S.steps[e] = steps;
     S.env_flags[e] = ef;
   }
-  const bool wrote_step = stepping;
+  if (KIN && (stepping || do_reset)) {  // the pose the raycast and REWARD read
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (a.io.reward) a.io.reward[2 * e + q] = wrote_step ? (float)rw[q] : 0.0f;
-    if (a.io.reward64) a.io.reward64[2 * e + q] = wrote_step ? rw[q] : 0.0;
+    for (int q = 0; q < 2; ++q) {
+      const int i = 2 * e + q;
+      S.x[i] = c[q].x;
+      S.y[i] = c[q].y;
+      S.angle[i] = c[q].angle;
+      S.vx[i] = c[q].vx;
+      S.vy[i] = c[q].vy;
+      S.last_steering[i] = last_steering[q];
+      if (do_reset) {
+        S.progress[i] = 0.0;
+        S.last_progress[i] = 0.0;
+        S.flags[i] = fl[q];
+      }
+    }
+    S.steps[e] = steps;
+    S.env_flags[e] = ef;
   }
-  const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
-  if (a.io.terminated) a.io.terminated[e] = t_out;
-  if (a.io.truncated) a.io.truncated[e] = u_out;
-  if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  if (REW && (stepping || do_reset)) {
+    if (stepping) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 2 * e + q;
+        S.progress[i] = c[q].progress;
+        S.last_progress[i] = c[q].progress;
+        S.flags[i] = fl[q];
+      }
+    }
+    S.env_flags[e] = ef;
+  }
+  // outputs: reset-by-NEXT_STEP / explicit reset gives reward 0, term = trunc = False
+  if (FULL || (REW && stepping) || (KIN && !stepping)) {
+    const bool wrote_step = stepping;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (a.io.reward) a.io.reward[2 * e + q] = wrote_step ? (float)rw[q] : 0.0f;
+      if (a.io.reward64) a.io.reward64[2 * e + q] = wrote_step ? rw[q] : 0.0;
+    }
+    const bool t_out = wrote_step && term, u_out = wrote_step && trunc;
+    if (a.io.terminated) a.io.terminated[e] = t_out;
+    if (a.io.truncated) a.io.truncated[e] = u_out;
+    if (a.io.done_f32) a.io.done_f32[e] = (t_out || u_out) ? 1.0f : 0.0f;
+  }
   // non-ray observation columns, multi_racing_env.py:226-271
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < 2 && !REW; ++q) {
     const Car& me = c[q];
     const Car& o = c[1 - q];
     double s, co;
@@ -1084,14 +1156,19 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, double* ang_out, int
     ob[6] = (float)rx_clip(lvx / RX_MAX_SPEED, -1.0, 1.0);
     ob[7] = (float)rx_clip(lvy / RX_MAX_SPEED, -1.0, 1.0);
   }
-  write_sort_key(a, we.perm_start + lane, k, e, c[0].progress, W);
-  ang_out[0] = c[0].angle;
-  ang_out[1] = c[1].angle;
-  e_out = e;
+  if (!KIN) write_sort_key(a, we.perm_start + lane, k, e, c[0].progress, W);
+  if (!REW) {
+    ang_out[0] = c[0].angle;
+    ang_out[1] = c[1].angle;
+    e_out = e;
+  }
 }
 
+// k_dyn2 (PART = FULL) and k_kin2 (PART = KIN, one wave per workgroup so that
+// block b's wave lands on the XCD of block b's REWARD and raycast waves).
+template <int PART>
 __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
-  const int wave = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   __shared__ int32_t tcnt[4][kTaskSectors];
   int32_t* cnt = tcnt[threadIdx.x >> 6];
@@ -1100,8 +1177,8 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   prof_mark(a, wave, false);
   double ang[2], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;
-  dyn2_env(a, ang, e, ep);
-  add_episode_stats(a, ep);
+  dyn2_env<PART>(a, wave, ang, e, ep);
+  if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
   prof_mark(a, wave, true);
 }
@@ -1411,7 +1488,11 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 #ifndef RX_STEP2_MINW
 #define RX_STEP2_MINW 8  // min waves per SIMD: caps VGPRs at 64 so the raycast half keeps full occupancy (some spills in the REWARD half)
 #endif
-__global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_rw) {
+#ifndef RX_STEP2_MINW_2
+#define RX_STEP2_MINW_2 6  // two-car k_step2<2>: 80 VGPRs (fewer REWARD spills; 8 -> 6 waves: +9 % at 8,192 envs, +1 % at 65,536)
+#endif
+template <int A>
+__global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
   prof_mark(a, b, false);
   if (b < n_rw) {
@@ -1420,12 +1501,15 @@ __global__ __launch_bounds__(64, RX_STEP2_MINW) void k_step2(rx_kargs a, int n_r
     // waves are long latency chains that would otherwise finish last
     __builtin_amdgcn_s_setprio(RX_REWARD_PRIO);
 #endif
-    double ang[1], ep[3] = {0.0, 0.0, 0.0};
+    double ang[A], ep[3] = {0.0, 0.0, 0.0};
     int e = -1;
-    dyn1_env<RX_REWARD_LPE, RX_PART_REWARD>(a, b / RX_REWARD_LPE, ang, e, ep, b % RX_REWARD_LPE);
+    if constexpr (A == 1)
+      dyn1_env<RX_REWARD_LPE, RX_PART_REWARD>(a, b / RX_REWARD_LPE, ang, e, ep, b % RX_REWARD_LPE);
+    else
+      dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
   } else {
-    rays_body<1>(a, b - n_rw);
+    rays_body<A>(a, b - n_rw);
   }
   prof_mark(a, b, true);
 }
@@ -1509,7 +1593,16 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 }  // namespace
 
 // ------------------------------------------------------------ launchers
-extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s) {
+extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s) {
+  if (n_agents == 2) {  // k_kin2, then k_step2<2> (REWARD waves padded to 8, as below)
+    const int n_rw2 = (a->n_dyn_waves + 7) / 8 * 8;
+    if (part == RX_SPLIT_KIN)
+      hipLaunchKernelGGL((k_dyn2<RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
+    else
+      hipLaunchKernelGGL(k_step2<2>, dim3(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves)), dim3(64), 0, s,
+                         *a, n_rw2);
+    return (int)hipGetLastError();
+  }
   const int n_rw = (a->n_dyn_waves * RX_REWARD_LPE + 7) / 8 * 8;
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
@@ -1521,9 +1614,9 @@ extern "C" int rx_launch_split(const rx_kargs* a, int part, hipStream_t s) {
     hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3((a->n_dyn_waves + kin_wpb - 1) / kin_wpb), dim3(64 * kin_wpb),
                        0, s, *a);
   } else if (part == RX_SPLIT_REWARD) {
-    hipLaunchKernelGGL(k_step2, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
+    hipLaunchKernelGGL(k_step2<1>, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
   } else {  // RX_SPLIT_REWARD_RAYS: both halves in one launch
-    hipLaunchKernelGGL(k_step2, dim3(n_rw + a->n_ray_waves), dim3(64), 0, s, *a, n_rw);
+    hipLaunchKernelGGL(k_step2<1>, dim3(n_rw + a->n_ray_waves), dim3(64), 0, s, *a, n_rw);
   }
   return (int)hipGetLastError();
 }
@@ -1541,7 +1634,7 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else if (n_agents == 1)
       hipLaunchKernelGGL((k_dyn1<1, RX_PART_FULL>), grd, blk, 0, s, *a);
     else
-      hipLaunchKernelGGL(k_dyn2, grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn2<RX_PART_FULL>), grd, blk, 0, s, *a);
   }
   if ((phases & RX_PHASE_RAYS) && a->wide) {
     const dim3 wg((a->n_wide_tasks + 3) / 4);

@@ -183,7 +183,11 @@ def test_random_rollout_bit_exact_vs_oracle_dev(rx, golden, oracle_dev, dyn_path
         assert np.array_equal(g[k], st[k]), k
 
 
-def test_multi_step_vs_golden_and_oracle(rx, golden, oracle_dev):
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_multi_step_vs_golden_and_oracle(rx, golden, oracle_dev, monkeypatch, split):
+    """Two-car KATs on the one-kernel step (k_dyn2 + k_rays<2>) and on the split
+    step (k_kin2 + k_step2<2>)."""
+    monkeypatch.setenv("RX_SPLIT", split)
     step = golden["step_multi"]
     v = _venv(rx, golden, step["track"], n_agents=2, autoreset="disabled")
     st = multi_state_from(step)
@@ -391,23 +395,31 @@ def test_dyn_lanes_per_env_paths_agree(rx, golden):
     small.close()
 
 
+@pytest.mark.parametrize("n_agents", [1, 2])
 @pytest.mark.parametrize("autoreset", ["next_step", "disabled"])
-def test_split_step_equals_one_kernel_step(rx, golden, monkeypatch, autoreset):
-    """The split step (k_kin1 + fused REWARD/raycast k_step2) == the one-kernel
-    step bit for bit: obs, rewards (f32 and f64), masks, info, episode
-    statistics and the whole f64 state, over 300 steps of random play."""
+def test_split_step_equals_one_kernel_step(rx, golden, monkeypatch, autoreset, n_agents):
+    """The split step (k_kin1 / k_kin2 + fused REWARD/raycast k_step2<A>) == the
+    one-kernel step bit for bit: obs, rewards (f32 and f64), masks, placement,
+    info, episode statistics and the whole f64 state, over 300 steps of random
+    play (two cars: start-slot draws, car-car contact and placement included)."""
     monkeypatch.setenv("RX_DYN1_LPE", "1")
     N = 2048
     tracks = np.arange(N) % golden.n_tracks
+    kw = dict(autoreset=autoreset, n_agents=n_agents)
+    if n_agents == 2:
+        kw["seed"] = 5
     monkeypatch.setenv("RX_SPLIT", "0")
-    va = _venv(rx, golden, tracks, autoreset=autoreset)
+    va = _venv(rx, golden, tracks, **kw)
     monkeypatch.setenv("RX_SPLIT", "1")
-    vb = _venv(rx, golden, tracks, autoreset=autoreset)
+    vb = _venv(rx, golden, tracks, **kw)
     assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(17)
     for t in range(300):
-        a = torch.rand((N, 2), device="cuda", generator=g) * torch.tensor([2.4, 1.4], device="cuda") - torch.tensor(
-            [1.2, 0.2], device="cuda")
+        if n_agents == 1:
+            a = torch.rand((N, 2), device="cuda", generator=g) * torch.tensor([2.4, 1.4], device="cuda") - torch.tensor(
+                [1.2, 0.2], device="cuda")
+        else:  # both cars often steer into each other: start slots are 3.5 apart
+            a = torch.rand((N, 2, 2), device="cuda", generator=g) * 2.4 - 1.2
         oa, ra, da = va.step_device(a, full_info=True)
         ob, rb, db = vb.step_device(a, full_info=True)
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
