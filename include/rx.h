@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 10
+#define RX_ABI_VERSION 11
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -334,6 +334,35 @@ typedef struct rx_policy_io {
   int64_t act_stride;     /* e.g. 4 for one car's actions in [n][2][2] */
 } rx_policy_io;
 int rx_policy_act(const rx_policy_io* io, void* stream);
+
+/* A whole rollout of few single-agent envs in ONE persistent launch.
+ * Replaces PPO.collect_rollout's step loop (agent/ppo.py:97-132: per step
+ * agent.get_action_and_value(next_obs) at :105-110, envs.step(action) at
+ * :112-120) for handles in the small-N configuration (one env per dynamics
+ * wave: rx_rollout_supported).  Per step t the env's workgroup evaluates the
+ * policy on obs[t] exactly as rx_policy_act does with eps[t] (actions,
+ * log-probs, values), then steps the env exactly as rx_step does, writing
+ * obs[t+1] (next_obs after the last step), rewards[t], dones[t+1] (next_done
+ * after the last step).  obs[0] and dones[0] are the caller's.  io supplies the
+ * env's terminated / truncated / ep_done / ep_stats buffers (its obs, reward,
+ * done and actions pointers are ignored).  Same stream semantics as rx_step. */
+typedef struct rx_rollout_io {
+  int32_t T;              /* steps */
+  int32_t obs_dim;        /* 15 or 19 (= the handle's observation width) */
+  const float* params;    /* flat policy parameters (rx_policy_act layout) */
+  const float* log_std;   /* [2] */
+  const float* eps;       /* [T][N][2] N(0,1) noise */
+  float* obs;             /* [T][N][D] */
+  float* actions;         /* [T][N][2] out */
+  float* logprobs;        /* [T][N] out */
+  float* values;          /* [T][N] out */
+  float* rewards;         /* [T][N] out */
+  float* dones;           /* [T][N] out (rows 1..T-1) */
+  float* next_obs;        /* [N][D] out */
+  float* next_done;       /* [N] out */
+} rx_rollout_io;
+int rx_rollout_supported(const rx_env* h);
+int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream);
 
 #ifdef __cplusplus
 }

@@ -506,16 +506,7 @@ static void prof_arm(rx_env* h, rx_kargs& a, int kind) {
   h->prof_kinds.push_back(kind);
 }
 
-static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
-  if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
-  if (!h) return fail(RX_EINVAL, "null handle");
-  if (!io) return fail(RX_EINVAL, "io is null");
-  if (h->n_tracks <= 0) return fail(RX_ESTATE, "no track table (rx_upload_tracks)");
-  if (!h->assigned) return fail(RX_ESTATE, "no env assignment (rx_assign)");
-  if (!h->bound) return fail(RX_ESTATE, "no state bound (rx_bind_state)");
-  if (!io->obs) return fail(RX_EINVAL, "io->obs is required");
-  if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
-  rx_kargs a{};
+static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, rx_kargs& a) {
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
                        h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
@@ -548,6 +539,19 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   a.tasks = h->tasks.p;
   a.tasks_out = (h->cfg.ray_order == 2 && !a.wide) ? h->tasks.p : nullptr;
   a.cs_scratch = h->cs_scratch.p;
+}
+
+static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
+  if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (!io) return fail(RX_EINVAL, "io is null");
+  if (h->n_tracks <= 0) return fail(RX_ESTATE, "no track table (rx_upload_tracks)");
+  if (!h->assigned) return fail(RX_ESTATE, "no env assignment (rx_assign)");
+  if (!h->bound) return fail(RX_ESTATE, "no state bound (rx_bind_state)");
+  if (!io->obs) return fail(RX_EINVAL, "io->obs is required");
+  if (mode == RX_MODE_STEP && !io->actions) return fail(RX_EINVAL, "io->actions is required");
+  rx_kargs a{};
+  make_kargs(h, io, mode, mask, a);
   hipStream_t s = (hipStream_t)stream;
   int rc;
   // Split step: k_kin1 / k_kin2 (resets, kinematics, [car-car contact,]
@@ -685,6 +689,35 @@ int rx_step(rx_env* h, const rx_io* io, void* stream) { return launch(h, io, RX_
 
 int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream) {
   return launch(h, io, RX_MODE_STEP, nullptr, stream, phases);
+}
+
+// rx_rollout: the persistent small-N rollout (k_rollout) on a handle in the
+// one-env-per-wave configuration; the per-step io pointers are set in-kernel.
+int rx_rollout_supported(const rx_env* h) {
+  return h && h->assigned && h->bound && h->cfg.n_agents == 1 && h->dyn_lpe == 64 && (h->D == 15 || h->D == 19);
+}
+
+int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream) {
+  if (!h || !io || !r) return fail(RX_EINVAL, "rx_rollout: null argument");
+  if (!rx_rollout_supported(h))
+    return fail(RX_ESTATE, "rx_rollout: needs an assigned, bound single-agent handle in the small-N (one env per "
+                           "wave) configuration with 15 or 19 observation columns");
+  if (r->T <= 0) return fail(RX_EINVAL, "rx_rollout: T=%d must be > 0", r->T);
+  if (r->obs_dim != h->D) return fail(RX_EINVAL, "rx_rollout: obs_dim %d != the handle's %d", r->obs_dim, h->D);
+  if (!r->params || !r->log_std || !r->eps || !r->obs || !r->actions || !r->logprobs || !r->values || !r->rewards ||
+      !r->dones || !r->next_obs || !r->next_done)
+    return fail(RX_EINVAL, "rx_rollout: null rollout buffer");
+  if (h->n_dyn_waves != h->cfg.n_envs) return fail(RX_ESTATE, "rx_rollout: expected one env per dynamics wave");
+  rx_kargs a{};
+  make_kargs(h, io, RX_MODE_STEP, nullptr, a);
+  a.sort_keys = nullptr;
+  a.sort_vals = nullptr;
+  a.tasks_out = nullptr;
+  a.prof_ts = nullptr;
+  int rc;
+  if ((rc = rx_launch_rollout(&a, r, (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "k_rollout launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
 }
 
 static int gae(int32_t T, int32_t N, const float* r, const float* v, const float* d, const float* nv, const float* nd,

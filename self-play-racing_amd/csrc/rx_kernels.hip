@@ -26,6 +26,7 @@
 #include "rx.h"
 #include "rx_internal.h"
 #include "rx_math.h"
+#include "rx_policy.h"
 
 #define RX_TWO_PI 6.283185307179586  // 2*np.pi, environment/car.py:54
 #define RX_MAX_SPEED 30.0
@@ -1447,26 +1448,32 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 // minimum.  Brute force, so no culling argument is involved; the min over the
 // exact t of hits is order-independent, hence bit-identical to k_rays.
 template <int A>
+__device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray) {
+  const int e = iq / A, q = iq - e * A;
+  const int k = uniform(a.st.track[e]);
+  const int wp0 = uniform(a.tr.wp_off[k]);
+  const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
+  const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+  const double ox = a.st.x[iq], oy = a.st.y[iq];
+  double sn, cs;
+  rx_sincos(a.st.angle[iq] + a.rel_angles[ray], &sn, &cs);  // racing_env.py:50
+  const double v3x = -sn, v3y = cs;
+  double best = __builtin_inf();
+  float bestf = __builtin_inff();
+  for (int j = threadIdx.x & 63; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
+  if ((threadIdx.x & 63) == 0) ray_finish<A>(a, iq, e, q, ray, ox, oy, v3x, v3y, best);
+}
+
+template <int A>
 __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   prof_mark(a, wave, false);
   const int R = a.n_sensors;
   if (wave < a.n_wide_tasks) {
-    const int iq = wave / R, ray = wave - iq * R, e = iq / A, q = iq - e * A;
-    const int k = uniform(a.st.track[e]);
-    const int wp0 = uniform(a.tr.wp_off[k]);
-    const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
-    const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
-    const double ox = a.st.x[iq], oy = a.st.y[iq];
-    double sn, cs;
-    rx_sincos(a.st.angle[iq] + a.rel_angles[ray], &sn, &cs);  // racing_env.py:50
-    const double v3x = -sn, v3y = cs;
-    double best = __builtin_inf();
-    float bestf = __builtin_inff();
-    for (int j = threadIdx.x & 63; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
-    if ((threadIdx.x & 63) == 0) ray_finish<A>(a, iq, e, q, ray, ox, oy, v3x, v3y, best);
+    const int iq = wave / R;
+    ray_wide<A>(a, iq, wave - iq * R);
   }
   prof_mark(a, wave, true);
 }
@@ -1512,6 +1519,112 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     rays_body<A>(a, b - n_rw);
   }
   prof_mark(a, b, true);
+}
+
+// ============================================================ k_rollout
+// PPO.collect_rollout (agent/ppo.py:97-132) for few single-agent envs as ONE
+// persistent launch (rx_rollout): workgroup b = the env of dynamics wave b
+// (small N: one env per wave), and per step t
+//   policy   : waves 0 / 1 = actor / critic trunk on obs[t], lane = hidden
+//              unit, weights staged once in LDS (transposed: lane reads are
+//              conflict-free).  Every output is the same fmaf chain in the same
+//              order as k_policy_act (rx_ppo.hip), so actions, log-probs and
+//              values equal rx_policy_act's with the same eps bit for bit;
+//   dynamics : wave 0 runs RacingEnv.step (dyn1_env<64, FULL>, as k_dyn1<64>);
+//   raycast  : wave w casts rays w, w + kRollWaves, ... (ray_wide, as
+//              k_rays_wide) into obs[t+1].
+// An env's actions depend only on its own observations, so workgroups never
+// wait for each other: the T steps run back to back inside the workgroup with
+// three barriers per step and no kernel launch between them.
+#ifndef RX_ROLL_WAVES
+#define RX_ROLL_WAVES 12
+#endif
+constexpr int kRollWaves = RX_ROLL_WAVES;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int D>
+__global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_rollout_io r) {
+  using L = rx_policy::Lay<D>;
+  constexpr int H = rx_policy::kH, NA = rx_policy::kNA;
+  __shared__ float sW1[2][D * H];  // [trunk][d][j] = W1[j][d]
+  __shared__ float sW2[2][H * H];  // [trunk][k][j] = W2[j][k]
+  __shared__ float sX[2][D], sH1[2][H], sH2[2][H];
+  const int b = blockIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t n = a.n_dyn_waves;  // = envs (one per dynamics wave)
+  const int e = a.perm[a.dyn_waves[b].perm_start];
+  const float* __restrict__ P = r.params;
+  for (int i = threadIdx.x; i < D * H; i += blockDim.x) {
+    const int j = i / D, d = i - j * D;
+    sW1[0][d * H + j] = P[L::aW1 + i];
+    sW1[1][d * H + j] = P[L::cW1 + i];
+  }
+  for (int i = threadIdx.x; i < H * H; i += blockDim.x) {
+    const int j = i / H, k = i - j * H;
+    sW2[0][k * H + j] = P[L::aW2 + i];
+    sW2[1][k * H + j] = P[L::cW2 + i];
+  }
+  __syncthreads();
+  rx_kargs at = a;
+  for (int t = 0; t < r.T; ++t) {
+    const bool last = t + 1 == r.T;
+    const int64_t row = (int64_t)t * n + e;
+    if (w < 2) {  // ---- policy (k_policy_act's operations, one row)
+      const int tr = w;  // 0 = actor, 1 = critic
+      if (lane < D) sX[tr][lane] = r.obs[row * D + lane];
+      wave_sync();
+      float z = 0.0f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) z = fmaf(sW1[tr][d * H + lane], sX[tr][d], z);
+      sH1[tr][lane] = tanhf(z + P[(tr ? L::cb1 : L::ab1) + lane]);
+      wave_sync();
+      z = 0.0f;
+#pragma unroll 16
+      for (int k = 0; k < H; ++k) z = fmaf(sW2[tr][k * H + lane], sH1[tr][k], z);
+      sH2[tr][lane] = tanhf(z + P[(tr ? L::cb2 : L::ab2) + lane]);
+      wave_sync();
+      if (tr == 0) {
+        float lp = 0.0f;
+        if (lane < NA) {
+          const int j = lane;
+          float zz = 0.0f;
+#pragma unroll 16
+          for (int k = 0; k < H; ++k) zz = fmaf(P[L::aW3 + j * H + k], sH2[0][k], zz);
+          const float mu = tanhf(zz + P[L::ab3 + j]);
+          const float scale = expf(r.log_std[j]);
+          const float var = scale * scale;
+          const float smp = r.eps[row * NA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
+          const float act = fminf(fmaxf(smp, -1.0f), 1.0f);
+          r.actions[row * NA + j] = act;
+          lp = rx_policy::normal_logp(act - mu, var, logf(scale));
+        }
+        const float lp1 = __shfl(lp, 1, 64);
+        if (lane == 0) r.logprobs[row] = (0.0f + lp) + lp1;  // logp = 0; logp += lp_j in j order
+      } else if (lane == 0) {
+        float v = 0.0f;
+        for (int k = 0; k < H; ++k) v = fmaf(P[L::cW3 + k], sH2[1][k], v);
+        r.values[row] = v + P[L::cb3];
+      }
+    }
+    __syncthreads();  // actions[t] -> the dynamics wave
+    at.io.actions = r.actions + (size_t)t * n * NA;
+    at.io.obs = last ? r.next_obs : r.obs + (size_t)(t + 1) * n * D;
+    at.io.reward = r.rewards + (size_t)t * n;
+    at.io.done_f32 = last ? r.next_done : r.dones + (size_t)(t + 1) * n;
+    if (w == 0) {  // ---- RacingEnv.step
+      double ang[1], ep[3] = {0.0, 0.0, 0.0};
+      int ee = -1;
+      dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep);
+      add_episode_stats(at, ep);
+    }
+    __syncthreads();  // stepped pose -> the raycast waves
+    for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray);
+    __syncthreads();  // obs[t+1] complete before the next policy step
+  }
 }
 
 // ============================================================ GAE
@@ -1660,6 +1773,14 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else
       hipLaunchKernelGGL(k_rays<2>, rgrd, rblk, lds, s, *a);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, hipStream_t s) {
+  if (r->obs_dim == 15)
+    hipLaunchKernelGGL(k_rollout<15>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), 0, s, *a, *r);
+  else
+    hipLaunchKernelGGL(k_rollout<19>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), 0, s, *a, *r);
   return (int)hipGetLastError();
 }
 

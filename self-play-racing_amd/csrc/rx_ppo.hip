@@ -15,11 +15,12 @@
 #include <hip/hip_runtime.h>
 
 #include "rx.h"
+#include "rx_policy.h"
 
 namespace {
 
-constexpr int kH = 64;   // hidden width (agent/ppo.py:20-29)
-constexpr int kNA = 2;   // action dims
+using rx_policy::kH;   // hidden width (agent/ppo.py:20-29)
+using rx_policy::kNA;  // action dims
 constexpr int kT = 256;  // threads per workgroup (4 waves)
 constexpr int kRP = 64;  // rows per pass (lane = row)
 constexpr int kS = 65;   // LDS row stride of the [64][64] tiles (lane-per-row reads hit distinct banks)
@@ -29,12 +30,8 @@ constexpr int kMaxWG = 512;  // partials per minibatch (rows per workgroup grow 
 #endif
 constexpr int kQ = RX_PPO_KQ;  // hidden columns per weight-load group (SGPR budget vs load batching)
 
-template <int D>
-struct Lay {  // flat parameter offsets, module.parameters() order; Pp = partial row stride
-  static constexpr int aW1 = 0, ab1 = aW1 + kH * D, aW2 = ab1 + kH, ab2 = aW2 + kH * kH, aW3 = ab2 + kH,
-                       ab3 = aW3 + kNA * kH, cW1 = ab3 + kNA, cb1 = cW1 + kH * D, cW2 = cb1 + kH,
-                       cb2 = cW2 + kH * kH, cW3 = cb2 + kH, cb3 = cW3 + kH, P = cb3 + 1, Pp = (P + 63) / 64 * 64;
-};
+using rx_policy::Lay;
+using rx_policy::normal_logp;
 
 struct ppo_args {
   rx_ppo_batch b;
@@ -88,12 +85,6 @@ __device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int o
     }
   }
   __syncthreads();
-}
-
-// Normal(mu, exp(log_std)).log_prob(a) for one action dim, in torch's operation
-// order (torch/distributions/normal.py: -((a-mu)**2)/(2*var) - log(scale) - log(sqrt(2*pi))).
-__device__ __forceinline__ float normal_logp(float diff, float var, float log_scale) {
-  return -(diff * diff) / (2.0f * var) - log_scale - 0.91893853320467274178f;
 }
 
 // One workgroup = rows_per_wg minibatch rows, processed kRP at a time.  Per

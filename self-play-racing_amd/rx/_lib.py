@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
 RX_EF_PENDING_RESET = 1
@@ -27,7 +27,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_assign", "rx_bind_state", "rx_set_speed_weight", "rx_reset", "rx_step", "rx_step_phases", "rx_gae",
            "rx_gae_scan", "rx_adam_workspace_floats", "rx_adam_clip_step", "rx_ppo_n_params", "rx_ppo_workspace_floats",
            "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act",
-           "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check",
+           "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check",
            "rx_profile", "rx_profile_read")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
@@ -68,6 +68,12 @@ class RxPPOBatch(ctypes.Structure):
                [(k, _P) for k in ("obs", "actions", "logprobs", "advantages", "returns", "values", "perm", "params",
                                   "log_std", "adv_stats")] + \
                [("clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float), ("kl_target", ctypes.c_float)]
+
+
+class RxRolloutIO(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_int32), ("obs_dim", ctypes.c_int32)] + \
+               [(k, _P) for k in ("params", "log_std", "eps", "obs", "actions", "logprobs", "values", "rewards",
+                                  "dones", "next_obs", "next_done")]
 
 
 class RxPolicyIO(ctypes.Structure):
@@ -124,6 +130,8 @@ def load(build_if_missing=True):
     L.rx_ppo_adv_stats.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P]
     L.rx_ppo_minibatch_grad.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P, _P, _P, _P, _P]
     L.rx_policy_act.argtypes = [ctypes.POINTER(RxPolicyIO), _P]
+    L.rx_rollout_supported.argtypes = [_P]
+    L.rx_rollout.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO), _P]
     L.rx_ppo_adv_moments.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P]
     L.rx_ppo_adv_finalize.argtypes = [_P, ctypes.c_int32, ctypes.c_int64, _P, _P]
     L.rx_ppo_minibatch_grad_shard.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, ctypes.c_float, _P, _P, _P,

@@ -115,6 +115,21 @@ class PPO:
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False)
         return contextlib.nullcontext()
 
+    def _fused_rollout(self, T):
+        """rx_rollout driver (config["fused_rollout"]: "auto" = up to
+        ppo_fused.ROLLOUT_AUTO_MAX_ENVS single-agent envs on the fused fp32
+        policy path), else None."""
+        from . import ppo_fused
+        c = self.config
+        if (not c.get("fused_policy", True) or c.get("policy_dtype", "fp32") != "fp32"
+                or getattr(self, "_flat", None) is None or not hasattr(self.envs, "_h")
+                or not ppo_fused.Rollout.supported(self.envs, self.agent, c)):
+            return None
+        ro = self.__dict__.get("_rollout")
+        if ro is None or ro.T != T or ro.n != self.envs.num_envs:
+            ro = self._rollout = ppo_fused.Rollout(self.agent, self._flat, self.envs, T)
+        return ro
+
     def _fused_policy(self, obs):
         """rx_policy_act driver when config["fused_policy"] (default on) and the
         policy is the reference layout in flat fp32 buffers; else None."""
@@ -133,6 +148,10 @@ class PPO:
         T = obs.shape[0]
         obs[0].copy_(next_obs)
         dones[0].copy_(next_done)
+        ro = self._fused_rollout(T)
+        if ro is not None:  # few envs: the whole rollout is one persistent launch
+            ro(obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
+            return
         fused = self._fused_policy(obs)
         for step in range(T):
             if fused is not None:  # one launch: forward, sample, log-prob, value into the buffers

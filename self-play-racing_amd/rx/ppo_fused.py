@@ -139,3 +139,63 @@ def policy_supported(agent, obs_dim):
     if obs_dim not in (15, 19):
         return False
     return sum(p.numel() for p in agent.parameters()) == _lib.load().rx_ppo_n_params(obs_dim)
+
+
+class Rollout:
+    """rx_rollout driver: a whole T-step rollout of few single-agent envs as
+    ONE persistent launch (include/rx.h; k_rollout) instead of T x (noise
+    draw + rx_policy_act + two env kernels).  The N(0, 1) noise of all T steps
+    is drawn up front with ONE torch normal_() on a [T, N, 2] buffer: the same
+    distribution as the per-step draws but a different sample of torch's
+    stream; given the same noise, every output equals the per-step fused path
+    (rx_policy_act + rx_step) bit for bit (tests/test_rollout_gpu.py)."""
+
+    def __init__(self, agent, flat, venv, T):
+        self.L = _lib.load()
+        self.agent, self.flat, self.venv, self.T = agent, flat, venv, int(T)
+        self.n, self.obs_dim = venv.num_envs, venv.D
+        self.eps = torch.empty((self.T, self.n, 2), dtype=torch.float32, device=flat.flat_param.device)
+        self._cache = {}
+
+    @staticmethod
+    def supported(venv, agent, config):
+        if venv.n_agents != 1 or not policy_supported(agent, venv.D):
+            return False
+        mode = config.get("fused_rollout", "auto")
+        if mode is False or mode == "off":
+            return False
+        if not _lib.load().rx_rollout_supported(venv._h):
+            return False
+        return mode is True or venv.num_envs <= ROLLOUT_AUTO_MAX_ENVS
+
+    def __call__(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done, eps=None, stream=None):
+        """obs[0] / dones[0] hold the rollout's first observation / done flags;
+        fills the rest like collect_rollout's step loop.  ``eps`` (tests): a
+        [T, N, 2] noise tensor to use instead of a fresh draw."""
+        T, n, D = self.T, self.n, self.obs_dim
+        shapes = {"obs": (obs, (T, n, D)), "actions": (actions, (T, n, 2)), "logprobs": (logprobs, (T, n)),
+                  "values": (values, (T, n)), "rewards": (rewards, (T, n)), "dones": (dones, (T, n)),
+                  "next_obs": (next_obs, (n, D)), "next_done": (next_done, (n,))}
+        for k, (t, shp) in shapes.items():
+            if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"rx_rollout: {k} must be a contiguous float32 {shp}, got {tuple(t.shape)} {t.dtype}")
+        e = self.eps if eps is None else eps
+        key = tuple(t.data_ptr() for t in (obs, actions, logprobs, dones, rewards, values, next_obs, next_done, e))
+        r = self._cache.get(key)
+        if r is None:
+            if len(self._cache) > 64:
+                self._cache.clear()
+            r = self._cache[key] = _lib.RxRolloutIO(
+                T, D, _lib.ptr(self.flat.flat_param), _lib.ptr(self.agent.log_std), _lib.ptr(e), _lib.ptr(obs),
+                _lib.ptr(actions), _lib.ptr(logprobs), _lib.ptr(values), _lib.ptr(rewards), _lib.ptr(dones),
+                _lib.ptr(next_obs), _lib.ptr(next_done))
+        if eps is None:
+            self.eps.normal_()
+        io = self.venv._io()
+        _lib.check(self.L.rx_rollout(self.venv._h, io, r, _lib.stream_ptr(stream)), "rx_rollout")
+
+
+# config["fused_rollout"] = "auto": the persistent rollout up to this many envs
+# (one workgroup per env runs all T steps; beyond what the chip holds at once
+# the workgroups would run in waves, each paying T steps of latency)
+ROLLOUT_AUTO_MAX_ENVS = 256

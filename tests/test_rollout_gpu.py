@@ -1,0 +1,79 @@
+"""Persistent small-N rollout (rx_rollout / k_rollout) == the per-step fused
+rollout (rx_policy_act + rx_step, agent/ppo.py:97-132) bit for bit, given the
+same N(0, 1) noise: observations, actions, log-probs, values, rewards, dones,
+the env state and the episode statistics."""
+import numpy as np
+import pytest
+import torch
+
+from tests.test_ppo_gpu import _train_single_style
+
+pytestmark = pytest.mark.gpu
+
+
+def _per_step(t, eps, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
+    """The fused per-step path with injected noise: rx_policy_act on eps[t], then rx_step."""
+    from rx import _lib
+    L = _lib.load()
+    T, n, D = obs.shape
+    for s in range(T):
+        io = _lib.RxPolicyIO(D, n, _lib.ptr(obs[s]), _lib.ptr(eps[s]), _lib.ptr(t._flat.flat_param),
+                             _lib.ptr(t.agent.log_std), _lib.ptr(actions[s]), _lib.ptr(logprobs[s]),
+                             _lib.ptr(values[s]), 0, 0)
+        _lib.check(L.rx_policy_act(io, _lib.stream_ptr()), "rx_policy_act")
+        last = s + 1 == T
+        t.envs.step_device(actions[s], obs_out=next_obs if last else obs[s + 1], reward_out=rewards[s],
+                           done_out=next_done if last else dones[s + 1])
+
+
+@pytest.mark.parametrize("n,T", [(16, 400), (200, 160)])
+def test_rollout_equals_per_step_path(n, T):
+    ta, c = _train_single_style(num_envs=n, num_steps=T)
+    tb, _ = _train_single_style(num_envs=n, num_steps=T)
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    from rx.ppo_fused import Rollout
+    assert Rollout.supported(ta.envs, ta.agent, c)
+    ro = ta._fused_rollout(T)
+    assert ro is not None
+    g = torch.Generator(device="cuda").manual_seed(4)
+    eps = torch.randn((T, n, 2), device="cuda", generator=g) * 1.5  # wide noise: crashes, resets, clamps
+    outs = []
+    for tr, fused in ((ta, True), (tb, False)):
+        bufs = tr._buffers()
+        nobs = tr.envs.buf["obs"].clone()
+        nd = torch.zeros(n, device="cuda")
+        for _ in range(2):  # two rollouts: the second starts from mid-episode state
+            obs, actions, logprobs, dones, rewards, values = bufs
+            obs[0].copy_(nobs)
+            dones[0].copy_(nd)
+            if fused:
+                ro(obs, actions, logprobs, dones, rewards, values, nobs, nd, eps=eps)
+            else:
+                _per_step(tr, eps, obs, actions, logprobs, dones, rewards, values, nobs, nd)
+        torch.cuda.synchronize()
+        outs.append(([x.clone() for x in bufs] + [nobs.clone(), nd.clone()], tr.envs.get_state(),
+                     tr.envs.episode_stats()))
+    (ba, sa, ea), (bb, sb, eb) = outs
+    names = ("obs", "actions", "logprobs", "dones", "rewards", "values", "next_obs", "next_done")
+    for k, x, y in zip(names, ba, bb):
+        assert torch.equal(x, y), k
+    assert (ba[3] > 0).any(), "no episode ended: the autoreset path was not exercised"
+    assert (ba[1].abs() == 1.0).any()  # clamped samples
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    assert ea[1:] == eb[1:] and ea[0] == pytest.approx(eb[0], rel=1e-12)
+
+
+def test_rollout_used_by_collect_rollout_and_trains():
+    """collect_rollout takes the persistent path for few envs (config
+    "fused_rollout" auto) and a short train() runs on it."""
+    t, c = _train_single_style(num_envs=16, num_steps=64)
+    assert t._fused_rollout(64) is not None
+    t2, _ = _train_single_style(num_envs=16, num_steps=64, fused_rollout=False)
+    assert t2._fused_rollout(64) is None
+    bufs = t._buffers()
+    nobs = t.envs.buf["obs"].clone()
+    nd = torch.zeros(16, device="cuda")
+    out = t.collect_rollout(*bufs, nobs, nd)
+    assert torch.isfinite(out[2]).all() and torch.isfinite(out[5]).all()
+    assert out[1].abs().max() <= 1.0
