@@ -1553,6 +1553,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
   __shared__ float sW1[2][D * H];  // [trunk][d][j] = W1[j][d]
   __shared__ float sW2[2][H * H];  // [trunk][k][j] = W2[j][k]
   __shared__ float sX[2][D], sH1[2][H], sH2[2][H];
+  __shared__ float sW3[NA * H];  // actor head
   const int b = blockIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t n = a.n_dyn_waves;  // = envs (one per dynamics wave)
@@ -1568,8 +1569,12 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     sW2[0][k * H + j] = P[L::aW2 + i];
     sW2[1][k * H + j] = P[L::cW2 + i];
   }
+  for (int i = threadIdx.x; i < NA * H; i += blockDim.x) sW3[i] = P[L::aW3 + i];
   __syncthreads();
   rx_kargs at = a;
+  // next-step / no autoreset: the split step's KIN / REWARD halves (as k_kin1 /
+  // k_step2), so the argmins and the reward run beside the 11 raycast waves
+  const bool split = a.autoreset != RX_AUTORESET_SAME_STEP;
   for (int t = 0; t < r.T; ++t) {
     const bool last = t + 1 == r.T;
     const int64_t row = (int64_t)t * n + e;
@@ -1593,7 +1598,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
           const int j = lane;
           float zz = 0.0f;
 #pragma unroll 16
-          for (int k = 0; k < H; ++k) zz = fmaf(P[L::aW3 + j * H + k], sH2[0][k], zz);
+          for (int k = 0; k < H; ++k) zz = fmaf(sW3[j * H + k], sH2[0][k], zz);
           const float mu = tanhf(zz + P[L::ab3 + j]);
           const float scale = expf(r.log_std[j]);
           const float var = scale * scale;
@@ -1615,14 +1620,25 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     at.io.obs = last ? r.next_obs : r.obs + (size_t)(t + 1) * n * D;
     at.io.reward = r.rewards + (size_t)t * n;
     at.io.done_f32 = last ? r.next_done : r.dones + (size_t)(t + 1) * n;
-    if (w == 0) {  // ---- RacingEnv.step
-      double ang[1], ep[3] = {0.0, 0.0, 0.0};
-      int ee = -1;
-      dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep);
-      add_episode_stats(at, ep);
+    double ang[1], ep[3] = {0.0, 0.0, 0.0};
+    int ee = -1;
+    if (split) {  // ---- RacingEnv.step as the split step: KIN, then REWARD beside the raycast
+      if (w == 0) dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep);
+      __syncthreads();  // stepped pose -> the raycast waves
+      if (w == 0) {
+        dyn1_env<64, RX_PART_REWARD>(at, b, ang, ee, ep);
+        add_episode_stats(at, ep);
+      } else {
+        for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, e, ray);
+      }
+    } else {  // same-step autoreset: the whole step first (k_dyn1's order)
+      if (w == 0) {
+        dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep);
+        add_episode_stats(at, ep);
+      }
+      __syncthreads();
+      for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray);
     }
-    __syncthreads();  // stepped pose -> the raycast waves
-    for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray);
     __syncthreads();  // obs[t+1] complete before the next policy step
   }
 }
