@@ -25,6 +25,7 @@ constexpr int kT = 256;  // threads per workgroup (4 waves)
 constexpr int kRP = 64;  // rows per pass (lane = row)
 constexpr int kS = 65;   // LDS row stride of the [64][64] tiles (lane-per-row reads hit distinct banks)
 constexpr int kMaxWG = 512;  // partials per minibatch (rows per workgroup grow beyond that)
+constexpr int kSplitNetsBelow = 256;  // workgroups per minibatch below which actor / critic get their own
 #ifndef RX_PPO_KQ
 #define RX_PPO_KQ 4
 #endif
@@ -87,8 +88,13 @@ __device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int o
   __syncthreads();
 }
 
-// One workgroup = rows_per_wg minibatch rows, processed kRP at a time.  Per
-// pass and per network (actor, then critic):
+// One workgroup = rows_per_wg minibatch rows, processed kRP at a time, of both
+// networks (actor, then critic) -- or, when the minibatch gives fewer than
+// kSplitNetsBelow workgroups, of ONE network (blockIdx.y: 0 = actor, 1 =
+// critic; their losses share no parameter, so the two backward passes are
+// independent workgroups writing disjoint ranges of the same partial row: a
+// latency-bound small minibatch then runs twice the workgroups, each half the
+// chain).  Per pass and network:
 //   forward  : wave w computes hidden columns [16w, 16w+16) for the 64 rows
 //              (lane = row), weights as SGPR operands, outputs to LDS;
 //   head     : wave 0 computes mu / value and the loss gradient per row;
@@ -118,6 +124,9 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
   const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
   double kl = 0.0;
   bool first = true;
+  // gridDim.y == 2: this workgroup's network only (small minibatches: twice the
+  // workgroups, half the chain each); 1: both networks, actor then critic
+  const int net0 = gridDim.y == 2 ? (int)blockIdx.y : 0, net1 = gridDim.y == 2 ? net0 + 1 : 2;
   for (int64_t base = row0; base < row_end; base += kRP, first = false) {
     if (t < kRP) {
       int64_t src = base + t < row_end ? b.perm[(int64_t)a.m * b.mb + base + t] : -1;
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
     const int64_t src = sSrc[lane];
     const bool live = src >= 0;
     __syncthreads();
-    for (int net = 0; net < 2; ++net) {
+    for (int net = net0; net < net1; ++net) {
       const int oW1 = net ? L::cW1 : L::aW1, ob1 = net ? L::cb1 : L::ab1;
       const int oW2 = net ? L::cW2 : L::aW2, ob2 = net ? L::cb2 : L::ab2;
       const int oW3 = net ? L::cW3 : L::aW3, ob3 = net ? L::cb3 : L::ab3;
@@ -267,7 +276,7 @@ __global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __r
       __syncthreads();
     }
   }
-  if (w == 0) {
+  if (w == 0 && net0 == 0) {
     for (int o = 32; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
     if (lane == 0) a.kl_partial[blockIdx.x] = kl;
   }
@@ -514,13 +523,14 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s) {
   const int rp = rows_per_wg(b->mb);
   const int n_wg = (b->mb + rp - 1) / rp;
+  const int ny = n_wg < kSplitNetsBelow ? 2 : 1;
   ppo_args a{*b, m, rp, stop, klp};
   int P, Pp;
   if (b->obs_dim == 15) {
-    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg), dim3(kT), 0, s, a, b->params, partial);
+    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg, ny), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
-    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg), dim3(kT), 0, s, a, b->params, partial);
+    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg, ny), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
   hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 4 * kRedCols - 1) / (4 * kRedCols)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
