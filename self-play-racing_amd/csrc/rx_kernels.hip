@@ -255,32 +255,53 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
 // in a lexicographic wave minimum: the reference's first-index argmin
 // (track.py:150-152) whatever the split.  All 64 lanes must be active; lane
 // P < 5 keeps point P's index.
+__device__ __forceinline__ void argmin_wave_take(const double2 w, int i, const double px[5], const double py[5],
+                                                 double best[5], int bi[5]) {
+#pragma unroll
+  for (int p = 0; p < 5; ++p) {
+    const double dx = w.x - px[p], dy = w.y - py[p];
+    const double d = dx * dx + dy * dy;
+    if (d < best[p]) {  // ascending i per lane: strict < keeps the first index
+      best[p] = d;
+      bi[p] = i;
+    }
+  }
+}
+
 __device__ __forceinline__ int argmin_wave(const double2* __restrict__ wp, int W, const double px[5],
                                            const double py[5], int P) {
   const int l = threadIdx.x & 63;
+  double best[5];
+  int bi[5];
+#pragma unroll
+  for (int p = 0; p < 5; ++p) {
+    best[p] = __builtin_inf();
+    bi[p] = 0x7fffffff;
+  }
+  // every waypoint is loaded once for the 5 points, four loads in flight at a time
+  int i = l;
+  for (; i + 192 < W; i += 256) {
+    const double2 w0 = wp[i], w1 = wp[i + 64], w2 = wp[i + 128], w3 = wp[i + 192];
+    argmin_wave_take(w0, i, px, py, best, bi);
+    argmin_wave_take(w1, i + 64, px, py, best, bi);
+    argmin_wave_take(w2, i + 128, px, py, best, bi);
+    argmin_wave_take(w3, i + 192, px, py, best, bi);
+  }
+  for (; i < W; i += 64) argmin_wave_take(wp[i], i, px, py, best, bi);
   int mine = 0;
 #pragma unroll
   for (int p = 0; p < 5; ++p) {
-    double best = __builtin_inf();
-    int bi = 0x7fffffff;
-    for (int i = l; i < W; i += 64) {  // ascending per lane: strict < keeps the first index
-      const double2 w = wp[i];
-      const double dx = w.x - px[p], dy = w.y - py[p];
-      const double d = dx * dx + dy * dy;
-      if (d < best) {
-        best = d;
-        bi = i;
-      }
-    }
+    double bp = best[p];
+    int ip = bi[p];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const double ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      const bool take = (ob < best) | ((ob == best) & (oi < bi));
-      best = take ? ob : best;
-      bi = take ? oi : bi;
+      const double ob = __shfl_xor(bp, o, 64);
+      const int oi = __shfl_xor(ip, o, 64);
+      const bool take = (ob < bp) | ((ob == bp) & (oi < ip));
+      bp = take ? ob : bp;
+      ip = take ? oi : ip;
     }
-    if (p == P) mine = bi;
+    if (p == P) mine = ip;
   }
   return mine;
 }
@@ -1460,7 +1481,15 @@ __device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray) {
   const double v3x = -sn, v3y = cs;
   double best = __builtin_inf();
   float bestf = __builtin_inff();
-  for (int j = threadIdx.x & 63; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
+  int j = threadIdx.x & 63;
+  for (; j + 192 < S_; j += 256) {  // four coalesced loads in flight before the (divergent) tests
+    const double4 g0 = seg[j], g1 = seg[j + 64], g2 = seg[j + 128], g3 = seg[j + 192];
+    seg_test(g0, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g1, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g2, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g3, ox, oy, v3x, v3y, best, bestf);
+  }
+  for (; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
   if ((threadIdx.x & 63) == 0) ray_finish<A>(a, iq, e, q, ray, ox, oy, v3x, v3y, best);
@@ -1575,7 +1604,14 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
   // next-step / no autoreset: the split step's KIN / REWARD halves (as k_kin1 /
   // k_step2), so the argmins and the reward run beside the 11 raycast waves
   const bool split = a.autoreset != RX_AUTORESET_SAME_STEP;
+#ifdef RX_ROLL_STAMPS  // profiling build (tools/rollout_stamps.py): phase boundaries of workgroup 0
+#define RX_RSTAMP(j) \
+  if (b == 0 && (threadIdx.x & 63) == 0 && a.io.counters && t < 512) a.io.counters[16 + 8 * t + (j)] = wall_clock64()
+#else
+#define RX_RSTAMP(j)
+#endif
   for (int t = 0; t < r.T; ++t) {
+    if (w == 0) RX_RSTAMP(0);
     const bool last = t + 1 == r.T;
     const int64_t row = (int64_t)t * n + e;
     if (w < 2) {  // ---- policy (k_policy_act's operations, one row)
@@ -1616,6 +1652,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
       }
     }
     __syncthreads();  // actions[t] -> the dynamics wave
+    if (w == 0) RX_RSTAMP(1);
     at.io.actions = r.actions + (size_t)t * n * NA;
     at.io.obs = last ? r.next_obs : r.obs + (size_t)(t + 1) * n * D;
     at.io.reward = r.rewards + (size_t)t * n;
@@ -1625,11 +1662,14 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     if (split) {  // ---- RacingEnv.step as the split step: KIN, then REWARD beside the raycast
       if (w == 0) dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep);
       __syncthreads();  // stepped pose -> the raycast waves
+      if (w == 0) RX_RSTAMP(2);
       if (w == 0) {
         dyn1_env<64, RX_PART_REWARD>(at, b, ang, ee, ep);
         add_episode_stats(at, ep);
+        RX_RSTAMP(4);
       } else {
         for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, e, ray);
+        if (w == 1) RX_RSTAMP(5);
       }
     } else {  // same-step autoreset: the whole step first (k_dyn1's order)
       if (w == 0) {
@@ -1640,6 +1680,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
       for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray);
     }
     __syncthreads();  // obs[t+1] complete before the next policy step
+    if (w == 0) RX_RSTAMP(3);
   }
 }
 
