@@ -693,15 +693,23 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream) {
 
 // rx_rollout: the persistent small-N rollout (k_rollout) on a handle in the
 // one-env-per-wave configuration; the per-step io pointers are set in-kernel.
+static int max_waypoints(const rx_env* h) {
+  int m = 0;
+  for (int k = 0; k < h->n_tracks; ++k) m = std::max(m, h->wp_off_h[k + 1] - h->wp_off_h[k]);
+  return m;
+}
+
 int rx_rollout_supported(const rx_env* h) {
-  return h && h->assigned && h->bound && h->cfg.n_agents == 1 && h->dyn_lpe == 64 && (h->D == 15 || h->D == 19);
+  return h && h->assigned && h->bound && h->cfg.n_agents == 1 && h->dyn_lpe == 64 && (h->D == 15 || h->D == 19) &&
+         max_waypoints(h) <= RX_ROLLOUT_MAX_W;
 }
 
 int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream) {
   if (!h || !io || !r) return fail(RX_EINVAL, "rx_rollout: null argument");
   if (!rx_rollout_supported(h))
     return fail(RX_ESTATE, "rx_rollout: needs an assigned, bound single-agent handle in the small-N (one env per "
-                           "wave) configuration with 15 or 19 observation columns");
+                           "wave) configuration with 15 or 19 observation columns and <= %d waypoints per slot",
+                RX_ROLLOUT_MAX_W);
   if (r->T <= 0) return fail(RX_EINVAL, "rx_rollout: T=%d must be > 0", r->T);
   if (r->obs_dim != h->D) return fail(RX_EINVAL, "rx_rollout: obs_dim %d != the handle's %d", r->obs_dim, h->D);
   if (!r->params || !r->log_std || !r->eps || !r->obs || !r->actions || !r->logprobs || !r->values || !r->rewards ||
@@ -715,7 +723,7 @@ int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream)
   a.tasks_out = nullptr;
   a.prof_ts = nullptr;
   int rc;
-  if ((rc = rx_launch_rollout(&a, r, (hipStream_t)stream)) != 0)
+  if ((rc = rx_launch_rollout(&a, r, max_waypoints(h), (hipStream_t)stream)) != 0)
     return fail(RX_EHIP, "k_rollout launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }

@@ -105,8 +105,10 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
-// persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env each
-extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, hipStream_t s);
+// persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env
+// each, its slot staged in max_w * 96 bytes of dynamic LDS
+#define RX_ROLLOUT_MAX_W 1024
+extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int max_w, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,

@@ -462,9 +462,18 @@ __device__ __forceinline__ double pick5(const double v[5], int P) {
 #define RX_PART_REWARD 2
 #define RX_EF_RESET_NOW 2u
 
+// The persistent rollout stages its env's slot (waypoints, normals, boundary
+// segments) in LDS once and hands the kernels' device functions these
+// pointers instead of the table in HBM (nullptr: the table).
+struct rx_slot_lds {
+  const double2* wp;
+  const double2* nrm;
+  const double4* seg;
+};
+
 template <int LPE, int PART>
 __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
-                                         int sub_block = 0) {
+                                         int sub_block = 0, const rx_slot_lds* sl = nullptr) {
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
 #ifdef RX_DYN_STAMPS
   unsigned long long stamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -481,8 +490,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
   const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
-  const double2* __restrict__ wp = reinterpret_cast<const double2*>(a.tr.wp) + wp0;
-  const double2* __restrict__ nrm = reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
+  const double2* __restrict__ wp = sl ? sl->wp : reinterpret_cast<const double2*>(a.tr.wp) + wp0;
+  const double2* __restrict__ nrm = sl ? sl->nrm : reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
   const double* __restrict__ meta = a.tr.meta + 8 * k;
   const double width = meta[3];
   if (lane >= we.count) return;
@@ -1469,12 +1478,12 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 // minimum.  Brute force, so no culling argument is involved; the min over the
 // exact t of hits is order-independent, hence bit-identical to k_rays.
 template <int A>
-__device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray) {
+__device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray, const double4* seg_lds = nullptr) {
   const int e = iq / A, q = iq - e * A;
   const int k = uniform(a.st.track[e]);
   const int wp0 = uniform(a.tr.wp_off[k]);
   const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
-  const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+  const double4* __restrict__ seg = seg_lds ? seg_lds : reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
   const double ox = a.st.x[iq], oy = a.st.y[iq];
   double sn, cs;
   rx_sincos(a.st.angle[iq] + a.rel_angles[ray], &sn, &cs);  // racing_env.py:50
@@ -1599,6 +1608,24 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     sW2[1][k * H + j] = P[L::cW2 + i];
   }
   for (int i = threadIdx.x; i < NA * H; i += blockDim.x) sW3[i] = P[L::aW3 + i];
+  // the env's slot, read every step by the argmins, the collision test and the
+  // 11 raycasts: LDS latency instead of L2 round trips (rx_rollout sizes it)
+  extern __shared__ double4 sSlot[];  // [2W] segments, then [W] waypoints, [W] normals (double2)
+  const int k = a.st.track[e];
+  const int wp0 = a.tr.wp_off[k], W = a.tr.wp_off[k + 1] - wp0;
+  {
+    const double4* __restrict__ gseg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+    const double2* __restrict__ gwp = reinterpret_cast<const double2*>(a.tr.wp) + wp0;
+    const double2* __restrict__ gnrm = reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
+    double2* lwp = reinterpret_cast<double2*>(sSlot + 2 * W);
+    for (int i = threadIdx.x; i < 2 * W; i += blockDim.x) sSlot[i] = gseg[i];
+    for (int i = threadIdx.x; i < W; i += blockDim.x) {
+      lwp[i] = gwp[i];
+      lwp[W + i] = gnrm[i];
+    }
+  }
+  const rx_slot_lds sl{reinterpret_cast<const double2*>(sSlot + 2 * W),
+                       reinterpret_cast<const double2*>(sSlot + 2 * W) + W, sSlot};
   __syncthreads();
   rx_kargs at = a;
   // next-step / no autoreset: the split step's KIN / REWARD halves (as k_kin1 /
@@ -1660,24 +1687,24 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     double ang[1], ep[3] = {0.0, 0.0, 0.0};
     int ee = -1;
     if (split) {  // ---- RacingEnv.step as the split step: KIN, then REWARD beside the raycast
-      if (w == 0) dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep);
+      if (w == 0) dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep, 0, &sl);
       __syncthreads();  // stepped pose -> the raycast waves
       if (w == 0) RX_RSTAMP(2);
       if (w == 0) {
-        dyn1_env<64, RX_PART_REWARD>(at, b, ang, ee, ep);
+        dyn1_env<64, RX_PART_REWARD>(at, b, ang, ee, ep, 0, &sl);
         add_episode_stats(at, ep);
         RX_RSTAMP(4);
       } else {
-        for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, e, ray);
+        for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, e, ray, sl.seg);
         if (w == 1) RX_RSTAMP(5);
       }
     } else {  // same-step autoreset: the whole step first (k_dyn1's order)
       if (w == 0) {
-        dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep);
+        dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep, 0, &sl);
         add_episode_stats(at, ep);
       }
       __syncthreads();
-      for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray);
+      for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray, sl.seg);
     }
     __syncthreads();  // obs[t+1] complete before the next policy step
     if (w == 0) RX_RSTAMP(3);
@@ -1833,11 +1860,12 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   return (int)hipGetLastError();
 }
 
-extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, hipStream_t s) {
+extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int max_w, hipStream_t s) {
+  const size_t lds = (size_t)max_w * (2 * sizeof(double4) + 2 * sizeof(double2));  // one slot, staged
   if (r->obs_dim == 15)
-    hipLaunchKernelGGL(k_rollout<15>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), 0, s, *a, *r);
+    hipLaunchKernelGGL(k_rollout<15>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), lds, s, *a, *r);
   else
-    hipLaunchKernelGGL(k_rollout<19>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), 0, s, *a, *r);
+    hipLaunchKernelGGL(k_rollout<19>, dim3(a->n_dyn_waves), dim3(64 * kRollWaves), lds, s, *a, *r);
   return (int)hipGetLastError();
 }
 
