@@ -82,7 +82,8 @@ struct rx_env {
   DevBuf<double> super_box;
   DevBuf<int32_t> wsuper_off;  // two-level closest-waypoint culling
   DevBuf<double> wsuper_box;
-  DevBuf<float> chunk_box_f, super_box_f;  // outward-rounded float32 copies (raycast box tests)
+  DevBuf<float> chunk_box_f, super_box_f;  // outward-rounded float32 copies (raycast box tests) + 4 quadrant blocks
+  int32_t n_chunk_boxes = 0, n_super_boxes = 0;
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
@@ -223,7 +224,26 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
     }
     return f;
   };
-  const std::vector<float> boxes_f = to_f32(boxes), sboxes_f = to_f32(sboxes);
+  // then 4 quadrant-ordered copies: block q = (near.x, near.y, far.x, far.y) for
+  // a ray direction whose x (bit 0) / y (bit 1) component is negative -- the
+  // slab planes k_rays' single-quadrant waves enter and leave through
+  auto with_quadrants = [](std::vector<float> f) {
+    const size_t n = f.size();
+    f.resize(5 * n);
+    for (int q = 0; q < 4; ++q)
+      for (size_t i = 0; i < n; i += 4) {
+        float* o = f.data() + (q + 1) * n + i;
+        const float* b = f.data() + i;
+        o[0] = (q & 1) ? b[2] : b[0];
+        o[1] = (q & 2) ? b[3] : b[1];
+        o[2] = (q & 1) ? b[0] : b[2];
+        o[3] = (q & 2) ? b[1] : b[3];
+      }
+    return f;
+  };
+  const std::vector<float> boxes_f = with_quadrants(to_f32(boxes)), sboxes_f = with_quadrants(to_f32(sboxes));
+  h->n_chunk_boxes = (int32_t)(boxes.size() / 4);
+  h->n_super_boxes = (int32_t)(sboxes.size() / 4);
   int rc;
   if ((rc = upload(h->chunk_box_f, boxes_f.data(), boxes_f.size()))) return rc;
   if (SG > 0 && (rc = upload(h->super_box_f, sboxes_f.data(), sboxes_f.size()))) return rc;
@@ -510,7 +530,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
                        h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
-                       h->chunk_box_f.p, h->super_box_f.p};
+                       h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes};
   a.st = h->st;
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;
@@ -539,6 +559,11 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.tasks = h->tasks.p;
   a.tasks_out = (h->cfg.ray_order == 2 && !a.wide) ? h->tasks.p : nullptr;
   a.cs_scratch = h->cs_scratch.p;
+  static const int quad = [] {  // A/B knob
+    const char* e = getenv("RX_BOX_QUAD");
+    return e ? atoi(e) : 1;
+  }();
+  a.box_quadrants = quad;
 }
 
 static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {

@@ -39,8 +39,10 @@ struct rx_track_view {
   // closest-waypoint super-chunks: RX_WP_SUPER consecutive waypoint chunks
   const int32_t* wsuper_off; // [n+1]
   const double* wsuper_box;  // [n_wsuper][4]
-  const float* chunk_box_f;  // chunk_box / super_box in float32, rounded outward (k_rays' packed-f32 box tests)
-  const float* super_box_f;
+  const float* chunk_box_f;  // chunk_box / super_box in float32, rounded outward (k_rays' packed-f32 box tests),
+  const float* super_box_f;  // then 4 quadrant blocks of (near.x, near.y, far.x, far.y) (rx_api.cpp)
+  int32_t n_chunk_boxes;     // boxes per block
+  int32_t n_super_boxes;
 };
 
 #ifndef RX_WP_CHUNK
@@ -97,6 +99,7 @@ struct rx_kargs {
   double speed_weight;
   uint64_t seed;
   uint32_t* reset_count;  // [N] (2-car envs), advanced by k_dyn2 at every reset
+  int32_t box_quadrants;  // k_rays: single-quadrant waves use the quadrant-ordered box tables (RX_BOX_QUAD=0: off)
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

@@ -48,6 +48,32 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
 }
 
 // f32 np.clip with Python-float bounds (stays float32 under NEP 50)
+// Load of track-table data at a wave-uniform address through the constant
+// address space: the tables are never written by a kernel, and the cast lets
+// the compiler issue s_load (scalar cache, SGPR operands) even after the
+// kernel's first global store -- a generic pointer loses that proof at the
+// first store (prof_mark, the REWARD half) and falls back to vector loads.
+#ifdef RX_NO_LDU  // A/B knob: plain generic loads
+typedef const double* rx_cdp;
+typedef const float* rx_cfp;
+#else
+typedef const __attribute__((address_space(4))) double* rx_cdp;
+typedef const __attribute__((address_space(4))) float* rx_cfp;
+#endif
+__device__ __forceinline__ double ldu(const double* p) { return *(rx_cdp)p; }
+__device__ __forceinline__ double2 ldu(const double2* p) {
+  const rx_cdp q = (rx_cdp)(const double*)p;
+  return make_double2(q[0], q[1]);
+}
+__device__ __forceinline__ double4 ldu(const double4* p) {
+  const rx_cdp q = (rx_cdp)(const double*)p;
+  return make_double4(q[0], q[1], q[2], q[3]);
+}
+__device__ __forceinline__ float4 ldu(const float4* p) {
+  const rx_cfp q = (rx_cfp)(const float*)p;
+  return make_float4(q[0], q[1], q[2], q[3]);
+}
+
 __device__ __forceinline__ float clipf(float a, float lo, float hi) {
   float y = a < lo ? lo : a;
   return y > hi ? hi : y;
@@ -80,7 +106,7 @@ __device__ __forceinline__ void argmin_pts(const double2* __restrict__ wp, int W
   }
 #pragma unroll 2
   for (int i = 0; i < W; ++i) {
-    const double2 w = wp[i];  // uniform address -> s_load_dwordx4
+    const double2 w = ldu(wp + i);  // uniform address -> s_load_dwordx4
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       double dx = w.x - px[p], dy = w.y - py[p];
@@ -118,7 +144,7 @@ __device__ __forceinline__ void argmin_take(double d, int i, double& best, int& 
 template <int NC>
 __device__ __forceinline__ bool box_may_hold_c(const double* __restrict__ b, const double cxs[NC], const double cys[NC],
                                                const double T[NC]) {
-  const double x0 = b[0], y0 = b[1], x1 = b[2], y1 = b[3];
+  const double x0 = ldu(b), y0 = ldu(b + 1), x1 = ldu(b + 2), y1 = ldu(b + 3);
   bool need = false;
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
@@ -223,7 +249,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
       int i = c * RX_WP_CHUNK;
       for (; i + 4 <= i1; i += 4) {  // four waypoints per batch of scalar loads
-        const double2 w[4] = {wp[i], wp[i + 1], wp[i + 2], wp[i + 3]};  // uniform -> s_load
+        const double2 w[4] = {ldu(wp + i), ldu(wp + i + 1), ldu(wp + i + 2), ldu(wp + i + 3)};  // uniform -> s_load
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
 #pragma unroll
@@ -234,7 +260,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
         }
       }
       for (; i < i1; ++i) {
-        const double2 w = wp[i];
+        const double2 w = ldu(wp + i);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const double dx = w.x - px[p], dy = w.y - py[p];
@@ -1260,13 +1286,13 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
                                              double v3x, double v3y, double& best, float& bestf) {
   int j = j0;
   for (; j + 4 <= j1; j += 4) {
-    const double4 g0 = seg[j], g1 = seg[j + 1], g2 = seg[j + 2], g3 = seg[j + 3];  // wave-uniform -> s_load
+    const double4 g0 = ldu(seg + j), g1 = ldu(seg + j + 1), g2 = ldu(seg + j + 2), g3 = ldu(seg + j + 3);  // uniform -> s_load
     seg_test(g0, ox, oy, v3x, v3y, best, bestf);
     seg_test(g1, ox, oy, v3x, v3y, best, bestf);
     seg_test(g2, ox, oy, v3x, v3y, best, bestf);
     seg_test(g3, ox, oy, v3x, v3y, best, bestf);
   }
-  for (; j < j1; ++j) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
+  for (; j < j1; ++j) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
 }
 
 // Chunk culling (exact; derivation in DESIGN.md §3).  The 2W boundary
@@ -1294,7 +1320,7 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
 typedef float rx_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 nlo, rx_f2 nhi, rx_f2 id2,
                                                float mtf, float bestf) {
-  const float4 b = *reinterpret_cast<const float4*>(box);
+  const float4 b = ldu(reinterpret_cast<const float4*>(box));
   const rx_f2 t1 = (rx_f2{b.x, b.y} + nlo) * id2;
   const rx_f2 t2 = (rx_f2{b.z, b.w} + nhi) * id2;
   const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1.x, t2.x), __builtin_fminf(t1.y, t2.y)), -mtf);
@@ -1307,6 +1333,89 @@ __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx
 template <int A>
 __device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int q, int ray, double ox, double oy,
                                            double v3x, double v3y, double best);
+
+// chunk_needed_f for a wave whose lanes all cast into one direction quadrant:
+// the box comes quadrant-ordered as (near.x, near.y, far.x, far.y) and nn / nf
+// are the matching origin offsets, so each axis' entry / exit distance needs no
+// min / max (4 fewer VALU).  Same decision as chunk_needed_f: with the axis'
+// direction sign fixed, rounding is monotone, so min(t1, t2) IS the near
+// plane's t and max(t1, t2) the far one's; only where chunk_needed_f meets a
+// NaN (0 * inf: origin on a slab plane, f32 direction component 0) does this
+// test drop the NaN and keep the box -- more conservative, never less.
+__device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx_f2 nn, rx_f2 nf, rx_f2 id2,
+                                               float mtf, float bestf) {
+  const float4 b = ldu(reinterpret_cast<const float4*>(box));
+  const rx_f2 tn = (rx_f2{b.x, b.y} + nn) * id2;
+  const rx_f2 tf = (rx_f2{b.z, b.w} + nf) * id2;
+  const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), -mtf);
+  const float hi = __builtin_fminf(tf.x, tf.y);
+  const float k = 0x1p-20f;
+  const bool miss = (lo - hi) > __builtin_fmaf(__builtin_fabsf(lo) + __builtin_fabsf(hi), k, 1e-6f);
+  return !miss && (__builtin_fmaf(-__builtin_fabsf(lo), k, lo) - mtf < bestf);
+}
+
+// The culled scan of one lane's ray over slot k's chunks (cull_chunk G > 0),
+// visiting them outward from chunk c0.  FAST: quadrant-ordered box block
+// `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far);
+// otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi).
+template <bool FAST>
+__device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
+                                          int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
+                                          double oy, double v3x, double v3y, double& best, float& bestf, int& tested,
+                                          int& scanned) {
+  const int G = a.cull_chunk;
+  const float* __restrict__ fboxes =
+      a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uniform(a.tr.chunk_off[k]));
+  auto needed = [&](const float* box) {
+    return FAST ? chunk_needed_q(box, n1, n2, id2, mtf, bestf) : chunk_needed_f(box, n1, n2, id2, mtf, bestf);
+  };
+  const int SG = a.cull_super;
+  if (SG <= 0) {
+    for (int s = 0; s < nch; ++s) {
+      const int off = (s + 1) >> 1;
+      int c = (s & 1) ? c0 - off : c0 + off;
+      c = c < 0 ? c + nch : (c >= nch ? c - nch : c);
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        ++tested;
+        if (__any(needed(fboxes + 4 * (side * nch + c)))) {
+          ++scanned;
+          ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
+        }
+      }
+    }
+    return;
+  }
+  // two levels: a super-chunk box (union of SG chunk boxes) first; its
+  // chunks are tested only if some lane may need it.  A chunk inside a
+  // skipped super-chunk is skipped by the same bound, so the result is
+  // unchanged (exactness argument of chunk_needed applies to any box that
+  // contains the segments).
+  const int nsup = (nch + SG - 1) / SG;
+  const float* __restrict__ sboxes =
+      a.tr.super_box_f + 4 * ((size_t)block * a.tr.n_super_boxes + (size_t)uniform(a.tr.super_off[k]));
+  const int u0 = uniform(c0 / SG);
+  for (int s = 0; s < nsup; ++s) {
+    const int off = (s + 1) >> 1;
+    const bool back = (s & 1) != 0;
+    int u = back ? u0 - off : u0 + off;
+    u = u < 0 ? u + nsup : (u >= nsup ? u - nsup : u);
+    const int l0 = u * SG, nl = min(nch, l0 + SG) - l0;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      ++tested;
+      if (!__any(needed(sboxes + 4 * (side * nsup + u)))) continue;
+      for (int q = 0; q < nl; ++q) {
+        const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
+        ++tested;
+        if (__any(needed(fboxes + 4 * (side * nch + c)))) {
+          ++scanned;
+          ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
+        }
+      }
+    }
+  }
+}
 
 template <int A>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
@@ -1354,7 +1463,6 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
     ray_segments(seg, 0, S_, ox, oy, v3x, v3y, best, bestf);
   } else {
     const int nch = (W + G - 1) / G;  // chunks per side
-    const float* __restrict__ fboxes = a.tr.chunk_box_f + 4 * (size_t)uniform(a.tr.chunk_off[k]);
     const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
     const double cx = sg[0], cy = sg[1], rad = sg[2], L = sg[3];
     const double ddx = ox - cx, ddy = oy - cy;
@@ -1369,57 +1477,24 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
                       3.0f * (__builtin_fabsf(oxf) + __builtin_fabsf(oyf) + 1.0f) * 0x1p-24f;
     const float mtf = (float)mt * (1.0f + 0x1p-20f) + 1e-6f;
     const rx_f2 nlo = {-(oxf + mbf), -(oyf + mbf)}, nhi = {mbf - oxf, mbf - oyf};
-    const rx_f2 id2 = {1.0f / (float)cs, 1.0f / (float)sn};
+    const float csf = (float)cs, snf = (float)sn;
+    const rx_f2 id2 = {1.0f / csf, 1.0f / snf};
     // visit chunks outward from the wave's first car
     int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
     const int c0 = uniform(w0 / G);
+    // direction quadrant (sign bits of the f32 direction, as id2's signs): a
+    // wave whose lanes all share it takes the quadrant-ordered box tables
+    const int quad = (int)(__float_as_uint(csf) >> 31) | (int)((__float_as_uint(snf) >> 31) << 1);
+    const int quad0 = uniform(quad);
     int scanned = 0, tested = 0;
-    const int SG = a.cull_super;
-    if (SG <= 0) {
-      for (int s = 0; s < nch; ++s) {
-        const int off = (s + 1) >> 1;
-        int c = (s & 1) ? c0 - off : c0 + off;
-        c = c < 0 ? c + nch : (c >= nch ? c - nch : c);
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-          ++tested;
-          const bool need = chunk_needed_f(fboxes + 4 * (side * nch + c), nlo, nhi, id2, mtf, bestf);
-          if (__any(need)) {
-            ++scanned;
-            ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
-          }
-        }
-      }
+    if (a.box_quadrants && __all(quad == quad0)) {
+      const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
+      const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
+      cull_scan<true>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
+                      scanned);
     } else {
-      // two levels: a super-chunk box (union of SG chunk boxes) first; its
-      // chunks are tested only if some lane may need it.  A chunk inside a
-      // skipped super-chunk is skipped by the same bound, so the result is
-      // unchanged (exactness argument of chunk_needed applies to any box that
-      // contains the segments).
-      const int nsup = (nch + SG - 1) / SG;
-      const float* __restrict__ sboxes = a.tr.super_box_f + 4 * (size_t)uniform(a.tr.super_off[k]);
-      const int u0 = uniform(c0 / SG);
-      for (int s = 0; s < nsup; ++s) {
-        const int off = (s + 1) >> 1;
-        const bool back = (s & 1) != 0;
-        int u = back ? u0 - off : u0 + off;
-        u = u < 0 ? u + nsup : (u >= nsup ? u - nsup : u);
-        const int l0 = u * SG, nl = min(nch, l0 + SG) - l0;
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-          ++tested;
-          if (!__any(chunk_needed_f(sboxes + 4 * (side * nsup + u), nlo, nhi, id2, mtf, bestf))) continue;
-          for (int q = 0; q < nl; ++q) {
-            const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
-            ++tested;
-            if (__any(chunk_needed_f(fboxes + 4 * (side * nch + c), nlo, nhi, id2, mtf, bestf))) {
-              ++scanned;
-              ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
-            }
-          }
-        }
-      }
+      cull_scan<false>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested, scanned);
     }
     if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
       atomicAdd(&a.io.counters[0], (unsigned long long)tested);
