@@ -64,6 +64,12 @@ def test_update_abi_validates_without_device():
     io = _lib.RxPolicyIO()
     io.obs_dim, io.n = 15, 4
     assert L.rx_policy_act(ctypes.byref(io), None) == _lib.RX_EINVAL
+    # persistent rollout: null handle / buffers are rejected before any HIP call
+    assert L.rx_rollout_supported(None) == 0
+    r = _lib.RxRolloutIO()
+    r.T, r.obs_dim = 8, 15
+    assert L.rx_rollout(None, ctypes.byref(_lib.RxIO()), ctypes.byref(r), None) == _lib.RX_EINVAL
+    assert b"null" in L.rx_last_error()
     cfg = _lib.RxAdamConfig()
     cfg.n_tensors = 0
     assert L.rx_adam_clip_step(ctypes.byref(cfg), None, None, None, None, None, None, None, None, None) \
