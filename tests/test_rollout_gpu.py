@@ -64,6 +64,57 @@ def test_rollout_equals_per_step_path(n, T):
     assert ea[1:] == eb[1:] and ea[0] == pytest.approx(eb[0], rel=1e-12)
 
 
+@pytest.mark.parametrize("autoreset", ["same_step", "disabled"])
+def test_rollout_other_autoreset_modes(autoreset):
+    """k_rollout's one-kernel branch (same-step autoreset: dyn1_env FULL before
+    the raycast) and the split branch with autoreset disabled, each == the
+    per-step path on a twin env, bit for bit."""
+    from rx.agent import Agent
+    from rx.optim import FlatAdam
+    from rx.ppo_fused import Rollout
+    from rx.spaces import Box
+    from rx.vector_env import RacingVectorEnv
+    from rx.track import gen_tracks
+    n, T = 24, 300
+    pool = gen_tracks(num_tracks=n, seed=3)
+    widths = [6 + (i % 4) for i in range(n)]
+    torch.manual_seed(9)
+    ag = Agent(Box(-1, 1, (15,)), Box(-1, 1, (2,))).cuda()
+    ag.log_std.fill_(-0.3)
+    fl = FlatAdam(ag, torch.optim.Adam(ag.parameters(), lr=1e-3, eps=1e-5), 0.5)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    eps = torch.randn((T, n, 2), device="cuda", generator=g) * 1.5
+    outs = []
+    for fused in (True, False):
+        venv = RacingVectorEnv(pool, widths, device="cuda", autoreset=autoreset)
+        obs = torch.zeros((T, n, 15), device="cuda")
+        actions = torch.zeros((T, n, 2), device="cuda")
+        logprobs, dones, rewards, values = (torch.zeros((T, n), device="cuda") for _ in range(4))
+        nobs = venv.reset_device().clone()
+        nd = torch.zeros(n, device="cuda")
+        obs[0].copy_(nobs)
+        dones[0].copy_(nd)
+        if fused:
+            Rollout(ag, fl, venv, T)(obs, actions, logprobs, dones, rewards, values, nobs, nd, eps=eps)
+        else:
+            class _T:  # the attributes _per_step reads
+                pass
+            tr = _T()
+            tr._flat, tr.agent, tr.envs = fl, ag, venv
+            _per_step(tr, eps, obs, actions, logprobs, dones, rewards, values, nobs, nd)
+        torch.cuda.synchronize()
+        outs.append(([x.clone() for x in (obs, actions, logprobs, dones, rewards, values, nobs, nd)],
+                     venv.get_state()))
+        venv.close()
+    (ba, sa), (bb, sb) = outs
+    for k, x, y in zip(("obs", "actions", "logprobs", "dones", "rewards", "values", "next_obs", "next_done"), ba, bb):
+        assert torch.equal(x, y), k
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    if autoreset == "same_step":
+        assert (ba[3] > 0).any(), "no episode ended: the reset path was not exercised"
+
+
 def test_rollout_used_by_collect_rollout_and_trains():
     """collect_rollout takes the persistent path for few envs (config
     "fused_rollout" auto) and a short train() runs on it."""
