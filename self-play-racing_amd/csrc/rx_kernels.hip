@@ -52,7 +52,7 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
 // address space: the tables are never written by a kernel, and the cast lets
 // the compiler issue s_load (scalar cache, SGPR operands) even after the
 // kernel's first global store -- a generic pointer loses that proof at the
-// first store (prof_mark, the REWARD half) and falls back to vector loads.
+// first store (the REWARD half's) and falls back to vector loads.
 #ifdef RX_NO_LDU  // A/B knob: plain generic loads
 typedef const double* rx_cdp;
 typedef const float* rx_cfp;
@@ -795,9 +795,16 @@ __device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const doubl
 // launch's duration -- the kernel's execution span, as rocprofv3 measures it,
 // without the dispatch / cache-flush time that stream events around a launch
 // include.
-__device__ __forceinline__ void prof_mark(const rx_kargs& a, int wave, bool end) {
+// Both stamps are stored at the END of the wave: a global store at the start
+// would precede every table load in program order and cost the compiler its
+// proof that those loads see unclobbered memory (vector instead of scalar loads).
+__device__ __forceinline__ unsigned long long prof_start(const rx_kargs& a) {
+  return a.prof_ts ? wall_clock64() : 0ull;
+}
+__device__ __forceinline__ void prof_end(const rx_kargs& a, int wave, unsigned long long t0) {
   if (!a.prof_ts || (threadIdx.x & 63) != 0 || wave >= a.prof_stride) return;
-  a.prof_ts[(end ? a.prof_stride : 0) + wave] = wall_clock64();
+  a.prof_ts[wave] = t0;
+  a.prof_ts[a.prof_stride + wave] = wall_clock64();
 }
 
 // k_dyn1 (PART = FULL) and k_kin1 (PART = KIN): 4 waves per workgroup.
@@ -809,13 +816,13 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
-  prof_mark(a, wave, false);
+  const unsigned long long prof_t0 = prof_start(a);
   double ang[1], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;  // set on the lane that finishes an env (sub 0)
   dyn1_env<LPE, PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
-  prof_mark(a, wave, true);
+  prof_end(a, wave, prof_t0);
 #ifdef RX_DYN_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t7 = __builtin_amdgcn_s_memtime();
@@ -1231,13 +1238,13 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   int32_t* cnt = tcnt[threadIdx.x >> 6];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
-  prof_mark(a, wave, false);
+  const unsigned long long prof_t0 = prof_start(a);
   double ang[2], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;
   dyn2_env<PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
-  prof_mark(a, wave, true);
+  prof_end(a, wave, prof_t0);
 }
 
 // ============================================================ k_rays
@@ -1542,9 +1549,9 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int 
 template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  prof_mark(a, wave, false);
+  const unsigned long long prof_t0 = prof_start(a);
   rays_body<A>(a, wave);
-  prof_mark(a, wave, true);
+  prof_end(a, wave, prof_t0);
 }
 
 // Small-N raycast (a.wide: few envs, latency-bound): one WAVE per (env,
@@ -1582,13 +1589,13 @@ __device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray, con
 template <int A>
 __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  prof_mark(a, wave, false);
+  const unsigned long long prof_t0 = prof_start(a);
   const int R = a.n_sensors;
   if (wave < a.n_wide_tasks) {
     const int iq = wave / R;
     ray_wide<A>(a, iq, wave - iq * R);
   }
-  prof_mark(a, wave, true);
+  prof_end(a, wave, prof_t0);
 }
 
 // Second kernel of the split step (A = 1, rx_api.cpp): one wave per
@@ -1614,7 +1621,7 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 template <int A>
 __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
-  prof_mark(a, b, false);
+  const unsigned long long prof_t0 = prof_start(a);
   if (b < n_rw) {
 #if RX_REWARD_PRIO > 0
     // issue priority over the raycast waves sharing the SIMD: the REWARD
@@ -1631,7 +1638,7 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
   } else {
     rays_body<A>(a, b - n_rw);
   }
-  prof_mark(a, b, true);
+  prof_end(a, b, prof_t0);
 }
 
 // ============================================================ k_rollout
