@@ -242,8 +242,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     const int l0 = u * RX_WP_SUPER, nl = min(nwc, l0 + RX_WP_SUPER) - l0;
     for (int q = 0; q < nl; ++q) {
       const int c = l0 + (back ? nl - 1 - q : q);
-      ++tested;
-      car_thresholds<NP, NC>(best, T, active);
+      ++tested;  // T is current: the bests change only inside a leaf scan, which refreshes it
       if (!__any(box_may_hold_c<NC>(wbox + 4 * c, cxs, cys, T))) continue;
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
@@ -267,6 +266,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
           argmin_take(dx * dx + dy * dy, i, best[p], idx[p]);
         }
       }
+      car_thresholds<NP, NC>(best, T, active);
     }
   }
   if (counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
