@@ -564,6 +564,11 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
     return e ? atoi(e) : 1;
   }();
   a.box_quadrants = quad;
+  static const int no_ep = [] {  // measurement knob: drop the episode-statistics atomics
+    const char* e = getenv("RX_NO_EPSTATS");
+    return e ? atoi(e) : 0;
+  }();
+  if (no_ep) a.io.ep_stats = nullptr;
 }
 
 static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {

@@ -269,10 +269,12 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
       car_thresholds<NP, NC>(best, T, active);
     }
   }
+#ifndef RX_DYN_STAMPS  // the stamp build reuses io.counters for its stamps: no culling counts there
   if (counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
     atomicAdd(&counters[2], (unsigned long long)tested);
     atomicAdd(&counters[3], (unsigned long long)scanned);
   }
+#endif
 }
 
 // Wide closest-waypoint argmin (one env per wave, dyn_lpe 64, small N): for
