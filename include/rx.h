@@ -39,7 +39,8 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 11
+#define RX_ABI_VERSION 12
+#define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
 #define RX_F_CRASHED 1u      /* Car.crashed                      car.py:22,80 */
@@ -123,7 +124,8 @@ typedef struct {
   float* done_f32;       /* [N] float(terminated | truncated): next_done, agent/ppo.py:120 */
   double* info;          /* [N][A][RX_INFO_W] */
   uint8_t* ep_done;      /* [N] an episode ended this step (infos['_episode']) */
-  double* ep_stats;      /* [3] += (sum return, sum length, count) of episodes ended */
+  double* ep_stats;      /* [RX_EP_SHARDS][4] += (sum return, sum length, count, -) of episodes ended;
+                            the caller sums the shard rows */
   unsigned long long* counters; /* [4] profiling, NULL = off: += per wave (raycast chunk tests,
                                    raycast chunks scanned, waypoint chunk tests, waypoint chunks scanned) */
 } rx_io;

@@ -773,8 +773,10 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
 }
 
 // Episode statistics of the envs that ended this step, summed over the wave
-// (all 64 lanes present) and added with ONE atomic per counter per wave: per-
-// env device-scope atomics on the same three addresses serialised the launch.
+// (all 64 lanes present) and added with ONE atomic per counter per wave into
+// one of RX_EP_SHARDS accumulator rows: per-env device-scope atomics on the
+// same three addresses serialised the launch, and even one per wave on three
+// shared addresses cost ~1.5 % of the step (RX_NO_EPSTATS A/B).
 __device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const double v[3]) {
   if (!a.io.ep_stats || !__any(v[2] != 0.0)) return;
   double s0 = v[0], s1 = v[1], s2 = v[2];
@@ -784,10 +786,11 @@ __device__ __forceinline__ void add_episode_stats(const rx_kargs& a, const doubl
     s1 += __shfl_xor(s1, o, 64);
     s2 += __shfl_xor(s2, o, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&a.io.ep_stats[0], s0);
-    atomicAdd(&a.io.ep_stats[1], s1);
-    atomicAdd(&a.io.ep_stats[2], s2);
+  if ((threadIdx.x & 63) == 0) {  // RX_EP_SHARDS rows of 4 (3 used): the reader sums them
+    double* st = a.io.ep_stats + 4 * ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (RX_EP_SHARDS - 1));
+    atomicAdd(&st[0], s0);
+    atomicAdd(&st[1], s1);
+    atomicAdd(&st[2], s2);
   }
 }
 

@@ -109,7 +109,7 @@ class RacingVectorEnv:
                 done_f32=torch.zeros(N, dtype=torch.float32, device=dev),
                 info=torch.zeros((N, A, _lib.RX_INFO_W), **f64),
                 ep_done=torch.zeros(N, dtype=torch.uint8, device=dev),
-                ep_stats=torch.zeros(3, **f64),
+                ep_stats=torch.zeros(_lib.RX_EP_SHARDS * 4, **f64),
             )
             cfg = _lib.RxConfig(N, A, R, self.max_steps, _AUTORESET[autoreset], dev.index or 0, int(seed) & (2**64 - 1),
                                 float(half_cone), self.speed_weight, int(cull_chunk), int(sort_interval),
@@ -258,7 +258,7 @@ class RacingVectorEnv:
     def episode_stats(self, reset=True):
         """(sum of returns, sum of lengths, count) of episodes that ended since the
         last call -- one device->host copy."""
-        s = self.buf["ep_stats"].cpu().numpy().copy()
+        s = self.buf["ep_stats"].view(_lib.RX_EP_SHARDS, 4).sum(0).cpu().numpy()
         if reset:
             self.buf["ep_stats"].zero_()
         return float(s[0]), float(s[1]), int(s[2])
