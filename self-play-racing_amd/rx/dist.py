@@ -47,6 +47,14 @@ def shard(n):
     return r * k, k
 
 
+def sampling_seed(seed):
+    """Seed of this rank's sampling streams (action noise, device shuffles,
+    random opponents): seed + rank, so rank 0 equals the single-process run
+    and no two ranks draw the same noise.  The initial policy stays shared
+    (every rank seeds its init with ``seed``)."""
+    return int(seed) + rank()
+
+
 def sum_stats(s, device):
     """Sum (sum_return, sum_length, count) over ranks."""
     if not active():

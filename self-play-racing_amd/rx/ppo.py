@@ -90,6 +90,7 @@ class PPO:
         torch.manual_seed(config["seed"])
         self.agent = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
         self.optimizer = optim.Adam(self.agent.parameters(), lr=config["learning_rate"], eps=1e-5)
+        self._seed_sampling()
         # parameters move into one flat buffer here, BEFORE any graph captures their addresses
         self._flat = FlatAdam(self.agent, self.optimizer, config["max_grad_norm"])
         # one forward now: BLAS handle / kernel-module initialisation belongs to
@@ -97,6 +98,18 @@ class PPO:
         with torch.no_grad():
             self.agent.get_value(self.envs.buf["obs"].reshape(-1, self.envs.buf["obs"].shape[-1])[:1])
         self._fresh_obs = True
+
+    def _seed_sampling(self):
+        """Data parallel: every rank built the SAME initial policy from
+        torch.manual_seed(seed) above, but must draw DIFFERENT action noise /
+        device shuffles / random opponent actions -- otherwise rank r's envs
+        replay rank 0's (the seed-1 pool repeats tracks, and every env starts on
+        its track's start line), and an optimizer step sees ~1/W unique samples.
+        The device generator is reseeded with seed + rank (rank 0 keeps the
+        single-process stream)."""
+        if rdist.world() > 1 and self.device.type == "cuda":
+            with torch.cuda.device(self.device):
+                torch.cuda.manual_seed(rdist.sampling_seed(self.config["seed"]))
 
     def _make_envs(self, env_fn):
         c = self.config

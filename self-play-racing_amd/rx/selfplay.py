@@ -120,6 +120,19 @@ class SelfPlayPPO(PPO):
             p.requires_grad = False
         return snap
 
+    def advance_pool(self, update):
+        """agent/self_play_ppo.py:115-122: snapshot every snapshot_freq updates
+        (not at update 0) into the FIFO pool of pool_size."""
+        if update > 0 and update % self.snapshot_freq == 0:
+            self.opponent_pool.append(self.snapshot_agent())
+            if len(self.opponent_pool) > self.pool_size:
+                self.opponent_pool.pop(0)
+
+    @staticmethod
+    def checkpoint_due(update):
+        """agent/self_play_ppo.py:154: a full checkpoint every 10 updates, not at 0."""
+        return update > 0 and update % 10 == 0
+
     def select_opponent(self):
         if not self.opponent_pool:
             return None
@@ -183,10 +196,7 @@ class SelfPlayPPO(PPO):
             start, global_step = 0, 0
             info = {"steps": [], "rewards": [], "opponent_pool_size": []}
         for update in range(start, num_updates):
-            if update > 0 and update % self.snapshot_freq == 0:
-                self.opponent_pool.append(self.snapshot_agent())
-                if len(self.opponent_pool) > self.pool_size:
-                    self.opponent_pool.pop(0)
+            self.advance_pool(update)
             self.update_opponent()
             if c.get("refresh_obs_on_rebuild", False):
                 next_obs.copy_(self.envs.buf["obs"])
@@ -199,7 +209,7 @@ class SelfPlayPPO(PPO):
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
             global_step += c["batch_size"]
-            if update > 0 and update % 10 == 0 and rdist.rank() == 0:
+            if self.checkpoint_due(update) and rdist.rank() == 0:
                 self.save_checkpoint(update, global_step, info)
             if ep:
                 info["opponent_pool_size"].append(len(self.opponent_pool))

@@ -21,6 +21,10 @@ Sets:
   step_multi.npz  G5  state-injected MultiRacingEnv.step KATs (+ reset order).
   gae.npz         G6  PPO.compute_advantages.
   agent.npz       G7  Agent init state_dict + forward on a fixed batch.
+  ppo_update.npz  G8  PPO.ppo_update run unbound (full, obs-19, KL early stop).
+  schedules.npz   A21 PPO.train / SelfPlayPPO.train per-update schedules
+                      (lr, log_std, speed weight, snapshot pool, opponent
+                      draws, checkpoint cadence).
 
 Metadata (numpy/scipy/torch versions, libm behaviour notes, CPU model) is stored
 in every file under ``meta_*`` keys.
@@ -494,9 +498,280 @@ def gen_agent():
     _save("agent.npz", **out)
 
 
+def _np_state(prefix, out):
+    st = np.random.get_state()
+    out[prefix + "_keys"] = np.asarray(st[1], dtype=np.uint32)
+    out[prefix + "_pos"] = np.array(st[2], dtype=np.int64)
+
+
+def _ppo_cfg(**over):
+    c = {"learning_rate": 3e-4, "gamma": 0.99, "gae_lambda": 0.95, "clip_coef": 0.2, "ent_coef": 0.01,
+         "vf_coef": 0.5, "update_epochs": 2, "num_minibatches": 4, "max_grad_norm": 0.5, "kl_target": 0.015}
+    c.update(over)
+    c["batch_size"] = c["num_steps"] * c["num_envs"]
+    c["minibatch_size"] = c["batch_size"] // c["num_minibatches"]
+    return c
+
+
+def _ppo_batch(torch, Agent, spaces, obs_dim, T, N, seed, log_std, adv_scale):
+    """A realistic rollout batch: actions sampled from the policy itself (some
+    clamped to the box edge, agent/ppo.py:44-53 Q7), its own log-probs and
+    values, random advantages, returns = advantages + values."""
+    torch.manual_seed(seed)
+    ag = Agent(spaces.Box(-1.0, 1.0, shape=(obs_dim,), dtype=np.float32),
+               spaces.Box(np.array([-1.0, 0.0]), np.array([1.0, 1.0]), shape=(2,), dtype=np.float32))
+    ag.log_std.fill_(log_std)
+    g = torch.Generator().manual_seed(seed + 1)
+    obs = (torch.rand(T, N, obs_dim, generator=g) * 2 - 1).float()
+    with torch.no_grad():
+        act, logp, _, val = ag.get_action_and_value(obs.reshape(-1, obs_dim))
+    act = act.reshape(T, N, 2)
+    logp = logp.reshape(T, N)
+    val = val.reshape(T, N)
+    adv = (torch.randn(T, N, generator=g) * adv_scale + 0.2).float()
+    ret = adv + val
+    return ag, dict(obs=obs, actions=act, logprobs=logp, values=val, advantages=adv, returns=ret)
+
+
+def gen_ppo_update():
+    """G8: PPO.ppo_update (agent/ppo.py:156-209) run unbound on CPU torch.
+
+    Cases: 'full' (2 epochs x 4 minibatches, no KL stop, obs 15), 'd19' (obs
+    19, 3 x 2, larger lr), 'stop' (KL early stop inside epoch 2, at a
+    minibatch chosen from the KLs the unstopped run sees).  Recorded: the
+    initial state_dict and batch, np.random state before/after, every
+    optimizer step's gradient as Adam sees it (flat, parameter order,
+    after clip_grad_norm_; the first two steps), the
+    post-update parameters and Adam state, the number of optimizer steps,
+    the KL per minibatch and the stop point."""
+    sys.path.insert(0, REF)
+    import contextlib
+    import io
+    import torch
+    from torch import optim
+    from agent.ppo import Agent, PPO
+    from gymnasium import spaces
+
+    class _Self:
+        pass
+
+    def run(ag0, batch, cfg, np_seed, record_kl=False):
+        ag = Agent(spaces.Box(-1.0, 1.0, shape=(batch["obs"].shape[-1],), dtype=np.float32),
+                   spaces.Box(np.array([-1.0, 0.0]), np.array([1.0, 1.0]), shape=(2,), dtype=np.float32))
+        ag.load_state_dict(ag0.state_dict())
+        opt = optim.Adam(ag.parameters(), lr=cfg["learning_rate"], eps=1e-5)
+        grads, kls = [], []
+        orig_step = opt.step
+
+        def step(*a, **k):
+            grads.append(torch.cat([p.grad.reshape(-1) for p in ag.parameters()]).clone())
+            return orig_step(*a, **k)
+        opt.step = step
+        if record_kl:  # the KL the reference tests at each minibatch (agent/ppo.py:178-180)
+            orig_gav = ag.get_action_and_value
+            b_lp = batch["logprobs"].reshape(-1)
+            inds_seen = []
+
+            def gav(x, action=None):
+                r = orig_gav(x, action)
+                inds_seen.append(r[1].detach().clone())
+                return r
+            ag.get_action_and_value = gav
+        s = _Self()
+        s.config, s.agent, s.optimizer, s.device = cfg, ag, opt, torch.device("cpu")
+        np.random.seed(np_seed)
+        st0 = {}
+        _np_state("rng_before", st0)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            PPO.ppo_update(s, batch["advantages"], batch["returns"], batch["values"], batch["logprobs"],
+                           batch["actions"], batch["obs"])
+        st1 = {}
+        _np_state("rng_after", st1)
+        if record_kl:
+            # replay the shuffles from the same seed to recover mb_inds
+            rs = np.random.RandomState(np_seed)
+            b_inds = np.arange(cfg["batch_size"])
+            k = 0
+            for _ in range(cfg["update_epochs"]):
+                rs.shuffle(b_inds)
+                for s0 in range(0, cfg["batch_size"], cfg["minibatch_size"]):
+                    if k >= len(inds_seen):
+                        break
+                    mb = b_inds[s0:s0 + cfg["minibatch_size"]]
+                    kls.append(float((b_lp[mb] - inds_seen[k]).mean()))
+                    k += 1
+        return ag, opt, grads, kls, st0, st1, buf.getvalue()
+
+    out = {}
+    cases = {
+        "full": dict(obs_dim=15, T=64, N=16, seed=11, log_std=-0.5, adv_scale=3.0, np_seed=5,
+                     cfg=dict(num_steps=64, num_envs=16, update_epochs=2, num_minibatches=4, kl_target=1e9)),
+        "d19": dict(obs_dim=19, T=32, N=16, seed=12, log_std=-0.9, adv_scale=8.0, np_seed=6,
+                    cfg=dict(num_steps=32, num_envs=16, update_epochs=3, num_minibatches=2, kl_target=1e9,
+                             learning_rate=1e-3, ent_coef=0.02, gae_lambda=0.97)),
+        "stop": dict(obs_dim=15, T=64, N=16, seed=13, log_std=-1.2, adv_scale=5.0, np_seed=7,
+                     cfg=dict(num_steps=64, num_envs=16, update_epochs=3, num_minibatches=4, kl_target=None,
+                              learning_rate=3e-3)),
+    }
+    for tag, cs in cases.items():
+        ag0, batch = _ppo_batch(torch, Agent, spaces, cs["obs_dim"], cs["T"], cs["N"], cs["seed"], cs["log_std"],
+                                cs["adv_scale"])
+        cfg = dict(cs["cfg"])
+        kl_stop_at = -1
+        if cfg["kl_target"] is None:
+            # KLs of an unstopped run; the target sits just below the first KL of
+            # epoch 2 that exceeds every earlier one -> the update returns there
+            probe = _ppo_cfg(**dict(cfg, kl_target=1e9))
+            _, _, _, kls, _, _, _ = run(ag0, batch, probe, cs["np_seed"], record_kl=True)
+            per_epoch = probe["num_minibatches"]
+            j = next(k for k in range(per_epoch + 1, len(kls)) if kls[k] > max(kls[:k]))
+            cfg["kl_target"] = 0.5 * (kls[j] + max(kls[:j]))
+            kl_stop_at = j
+        c = _ppo_cfg(**cfg)
+        ag, opt, grads, kls, st0, st1, text = run(ag0, batch, c, cs["np_seed"], record_kl=True)
+        if kl_stop_at >= 0:
+            assert len(grads) == kl_stop_at and "Early stopping" in text, (len(grads), kl_stop_at, text)
+        for k, v in ag0.state_dict().items():
+            out[f"{tag}_sd0_{k}"] = v.numpy()
+        for k, v in batch.items():
+            out[f"{tag}_{k}"] = v.numpy()
+        for k, v in ag.state_dict().items():
+            out[f"{tag}_sd1_{k}"] = v.numpy()
+        st = opt.state_dict()["state"]
+        out[f"{tag}_adam_exp_avg"] = torch.cat([st[i]["exp_avg"].reshape(-1) for i in sorted(st)]).numpy()
+        out[f"{tag}_adam_exp_avg_sq"] = torch.cat([st[i]["exp_avg_sq"].reshape(-1) for i in sorted(st)]).numpy()
+        out[f"{tag}_adam_step"] = np.array([float(st[i]["step"]) for i in sorted(st)])
+        out[f"{tag}_grads"] = torch.stack(grads[:2]).numpy()  # first two optimizer steps
+        out[f"{tag}_n_steps"] = np.array(len(grads))
+        out[f"{tag}_kls"] = np.array(kls)
+        out[f"{tag}_kl_stop_at"] = np.array(kl_stop_at)
+        out[f"{tag}_np_seed"] = np.array(cs["np_seed"])
+        for k, v in c.items():
+            out[f"{tag}_cfg_{k}"] = np.array(v)
+        for d in (st0, st1):
+            for k, v in d.items():
+                out[f"{tag}_{k}"] = v
+        print(f"ppo_update {tag}: {len(grads)} optimizer steps, stop_at={kl_stop_at}, kl_target={c['kl_target']:.6g}")
+    out["meta_torch"] = np.array(torch.__version__)
+    _save("ppo_update.npz", **out)
+
+
+def gen_schedules():
+    """A21: the per-update schedules of PPO.train (agent/ppo.py:235-258) and
+    SelfPlayPPO.train (agent/self_play_ppo.py:113-139, 154-167), recorded by
+    running the reference's own train loops with the rollout / advantage /
+    update phases replaced by recorders (no envs exist here).  Recorded per
+    update: lr, log_std, the speed_weight the loop setattr's on envs.envs[i];
+    self-play: pool membership after the snapshot step (ids = the update a
+    snapshot was taken at), the opponent np.random.choice draws, the updates
+    that write a checkpoint."""
+    sys.path.insert(0, REF)
+    import tempfile
+    import contextlib
+    import io
+    import types
+    import torch
+    from torch import optim
+    from agent.ppo import Agent, PPO
+    from agent.self_play_ppo import SelfPlayPPO
+    from gymnasium import spaces
+
+    out = {}
+    obs_sp = spaces.Box(-1.0, 1.0, shape=(15,), dtype=np.float32)
+    act_sp = spaces.Box(np.array([-1.0, 0.0]), np.array([1.0, 1.0]), shape=(2,), dtype=np.float32)
+
+    def stub(cfg, sp_obs):
+        s = types.SimpleNamespace()
+        s.config, s.device = cfg, torch.device("cpu")
+        N, D = cfg["num_envs"], sp_obs.shape[0]
+        s.envs = types.SimpleNamespace(single_observation_space=sp_obs, single_action_space=act_sp,
+                                       envs=[types.SimpleNamespace() for _ in range(N)],
+                                       reset=lambda: (np.zeros((N, D), np.float32), {}), close=lambda: None)
+        torch.manual_seed(cfg["seed"])
+        s.agent = Agent(sp_obs, act_sp)
+        s.optimizer = optim.Adam(s.agent.parameters(), lr=cfg["learning_rate"], eps=1e-5)
+        s.rec = {"lr": [], "log_std": [], "speed_weight": [], "opponent": [], "pool": []}
+        s.update_idx = [0]
+
+        def collect(*bufs):
+            s.rec["lr"].append(s.optimizer.param_groups[0]["lr"])
+            s.rec["log_std"].append(s.agent.log_std.detach().clone().numpy())
+            s.rec["speed_weight"].append(getattr(s.envs.envs[0], "speed_weight", np.nan))
+            return bufs + ([],)
+        s.collect_rollout = collect
+        s.compute_advantages = lambda r, d, v, nv, nd: (r, r)
+
+        def upd(*a):  # tag the weights with the update index: snapshots become identifiable
+            with torch.no_grad():
+                s.agent.critic[4].bias.fill_(float(s.update_idx[0]))
+            s.update_idx[0] += 1
+        s.ppo_update = upd
+        return s
+
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        os.makedirs("models")  # SelfPlayPPO.train torch.save's checkpoints there unguarded
+        try:
+            # single-agent: base_config values, 37 updates
+            cfg = _ppo_cfg(num_steps=4, num_envs=2, update_epochs=10, num_minibatches=2)
+            cfg.update(seed=1, total_timesteps=8 * 37 + 5)
+            s = stub(cfg, obs_sp)
+            with contextlib.redirect_stdout(io.StringIO()):
+                PPO.train(s)
+            out["single_num_updates"] = np.array(len(s.rec["lr"]))
+            out["single_lr"] = np.array(s.rec["lr"])
+            out["single_log_std"] = np.stack(s.rec["log_std"])
+            out["single_speed_weight"] = np.array(s.rec["speed_weight"])
+            out["single_learning_rate"] = np.array(cfg["learning_rate"])
+            # self-play: self_play_config values, 64 updates (snapshots at 15, 30, 45, 60)
+            cfg = _ppo_cfg(num_steps=4, num_envs=2, update_epochs=10, num_minibatches=2, learning_rate=3e-4,
+                           gae_lambda=0.97, ent_coef=0.02)
+            cfg.update(seed=1, total_timesteps=8 * 64, snapshot_freq=15, pool_size=3)
+            sp_obs = spaces.Box(-1.0, 1.0, shape=(19,), dtype=np.float32)
+            s = stub(cfg, sp_obs)
+            s.opponent_pool, s.curr_opponent = [], None
+            s.snapshot_freq, s.pool_size = cfg["snapshot_freq"], cfg["pool_size"]
+            s.snapshot_agent = lambda: SelfPlayPPO.snapshot_agent(s)
+            s.select_opponent = lambda: SelfPlayPPO.select_opponent(s)
+
+            def update_opponent():  # agent/self_play_ppo.py:46-50 minus the env rebuild
+                s.curr_opponent = s.select_opponent()
+                s.rec["opponent"].append(-1 if s.curr_opponent is None else int(s.curr_opponent.critic[4].bias.item()))
+                s.rec["pool"].append([int(o.critic[4].bias.item()) for o in s.opponent_pool]
+                                     + [-2] * (cfg["pool_size"] - len(s.opponent_pool)))
+            s.update_opponent = update_opponent
+            np.random.seed(1)
+            with contextlib.redirect_stdout(io.StringIO()):
+                SelfPlayPPO.train(s)
+            out["selfplay_num_updates"] = np.array(len(s.rec["lr"]))
+            out["selfplay_lr"] = np.array(s.rec["lr"])
+            out["selfplay_log_std"] = np.stack(s.rec["log_std"])
+            out["selfplay_opponent"] = np.array(s.rec["opponent"], dtype=np.int64)
+            out["selfplay_pool"] = np.array(s.rec["pool"], dtype=np.int64)
+            out["selfplay_np_seed"] = np.array(1)
+            out["selfplay_snapshot_freq"] = np.array(cfg["snapshot_freq"])
+            out["selfplay_pool_size"] = np.array(cfg["pool_size"])
+            out["selfplay_checkpoints"] = np.array(sorted(int(f.split("_")[-1].split(".")[0])
+                                                          for f in os.listdir("models")), dtype=np.int64)
+        finally:
+            os.chdir(cwd)
+    out["meta_torch"] = np.array(torch.__version__)
+    _save("schedules.npz", **out)
+
+
 def main(argv):
+    want = set(argv[1:]) or {"geometry", "raycast", "step_single", "traj_single", "step_multi", "gae", "agent",
+                             "ppo_update", "schedules"}
+    if want <= {"ppo_update", "schedules"}:
+        sys.path.insert(0, os.path.join(HERE, "_gym_stub"))
+        if "ppo_update" in want:
+            gen_ppo_update()
+        if "schedules" in want:
+            gen_schedules()
+        return
     track, car, racing_env, multi_racing_env = _import_reference()
-    want = set(argv[1:]) or {"geometry", "raycast", "step_single", "traj_single", "step_multi", "gae", "agent"}
     recs = None
     if want & {"geometry", "raycast", "step_single", "traj_single", "step_multi"}:
         recs = gen_geometry(track) if "geometry" in want else _tracks_set(track)[0]
@@ -512,6 +787,10 @@ def main(argv):
         gen_gae()
     if "agent" in want:
         gen_agent()
+    if "ppo_update" in want:
+        gen_ppo_update()
+    if "schedules" in want:
+        gen_schedules()
 
 
 if __name__ == "__main__":

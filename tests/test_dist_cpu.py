@@ -134,3 +134,31 @@ def test_shard_bounds():
         finally:
             dist.world = old
         del types
+
+
+def _seed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as td
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rx.dist as rd
+        q.put((rank, rd.sampling_seed(1), rd.shard(8)))
+    finally:
+        td.destroy_process_group()
+
+
+def test_two_rank_sampling_seeds_differ():
+    """Each rank's sampling streams get seed + rank (rank 0 == single process):
+    identical noise on every rank would make rank r replay rank 0's envs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict((r, (s, sh)) for r, s, sh in (q.get(timeout=120) for _ in procs))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert res[0][0] == 1 and res[1][0] == 2
+    assert res[0][1] == (0, 4) and res[1][1] == (4, 4)

@@ -109,3 +109,36 @@ def test_two_rank_flat_update_in_sync(fused):
             p._flat.step()
     assert rd.world() == 1
     np.testing.assert_allclose(res[0][0], p._flat.flat_param.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _noise_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as td
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = _make_ppo(_cfg(True))  # torch.manual_seed(3) -> identical initial policy on every rank
+        p._seed_sampling()
+        eps = torch.empty(64, 2, device="cuda").normal_()
+        q.put((rank, eps.cpu().numpy(), p._flat.flat_param.cpu().numpy()))
+    finally:
+        td.destroy_process_group()
+
+
+def test_two_rank_action_noise_differs():
+    """PPO._seed_sampling: same initial parameters on every rank, different
+    action-noise streams (rank 0's == the single-process stream of config seed)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_noise_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict((r, (e, w)) for r, e, w in (q.get(timeout=300) for _ in procs))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert np.array_equal(res[0][1], res[1][1])
+    assert not np.array_equal(res[0][0], res[1][0])
+    torch.manual_seed(_cfg()["seed"])
+    want = torch.empty(64, 2, device="cuda").normal_()
+    assert np.array_equal(res[0][0], want.cpu().numpy())
