@@ -20,10 +20,21 @@ optimizer step over RCCL).  With N GPUs
 (torch.distributed.run, one rank per GPU) every rank owns 65,536 envs of a
 N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
 
-Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel
-(k_rays, the raycast), timed live from per-wave device wall-clock stamps
-(rx_profile: first wave start to last wave end, the span rocprofv3 reports); ``cpu_baseline`` times oracle/np_env.py -- the reference's NumPy step
-restated (bit-exact vs the reference's golden vectors) -- on this host.
+Order of a run: CPU baseline (host only, before the GPU is touched), at
+least --burn-in untimed steps (the steady state: cars spread over their tracks,
+episodes ending and resetting), the timed region of --steps production steps
+(one rx_step each, nothing instrumented), then --profile-steps instrumented
+steps whose per-wave device wall-clock stamps (rx_profile: first wave start
+to last wave end, the span rocprofv3 reports) give the kernel durations.
+
+Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant production
+kernel, k_step2 (REWARD half beside the raycast), with its algorithmic bytes;
+``compute_roofline`` is its VALU busy fraction from the committed steady-state
+PMC counts (profiles/r02/pmc_steady.json, same launch size); ``cpu_baseline``
+times oracle/np_env.py -- the reference's NumPy step restated (bit-exact vs
+the reference's golden vectors) -- on this host's cores; ``time_to_90`` is the
+second half of the metric (PPO wall-clock to 90 % success, evaluate.py
+protocol) at the reference config and at configs[1].
 """
 import argparse
 import gc
@@ -41,13 +52,51 @@ sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-FP64_VALU_PEAK_TF = 78.6  # MI355X FP64 vector peak (AMD spec)
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each (16 lanes; FP64 FMA is
-# full rate: 1024 x 16 x 2 flop x 2.4 GHz = 78.6 TF), at 2.4 GHz
-VALU_WAVE_INST_PEAK_G = 1024 * 2.4e9 / 4 / 1e9  # 614.4 G wave-instructions/s
-RAY_FLOPS_PER_SEG = 13    # 2 sub, 3 dotp, 3 cross, 3 v1.v3, 2 div per ray x segment
 RAYS_BYTES_PER_ENV = 24 + 11 * 4   # k_rays algorithmic HBM bytes/env: read x,y,angle (f64), write 11 f32 obs
+# k_step2 algorithmic HBM bytes/env: REWARD half reads x, y, vx, vy, progress, last_progress,
+# ep_return (f64), steps, ep_length (i32), flags, env_flags (u8) = 74 B with the raycast's angle; writes progress,
+# last_progress, ep_return (f64), ep_length (i32), flags, env_flags, reward, done (f32) = 38 B; raycast writes
+# 11 f32 obs = 44 B
+STEP2_BYTES_PER_ENV = 74 + 38 + 44
 STEP_BYTES_PER_ENV = 218           # whole step, SURVEY.md §8(d)
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_steady.json")
+
+
+def load_pmc(n):
+    """Per-launch PMC counts of the production kernels (rocprofv3, tools/pmc.sh) committed
+    under profiles/: valid only for launches of the same size and the steady state
+    (the bench's own state distribution after its burn-in)."""
+    try:
+        pj = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return {}
+    if pj.get("envs_per_launch") != n:
+        return {}
+    out = {k: v for k, v in pj.items() if isinstance(v, dict)}
+    out["source"] = "profiles (steady state): " + os.path.relpath(PMC_FILE, ROOT)
+    return out
+
+
+def compute_roofline(pmc, launch_ms):
+    """VALU view of the VALU-bound env kernels: busy fraction of the SIMDs' VALU
+    issue over the launch, from PMC SQ_ACTIVE_INST_VALU (quad-cycles per wave,
+    summed) against 1,024 SIMDs x the launch's cycles at the clock PMC saw
+    (GRBM_GUI_ACTIVE / 8 XCDs per launch)."""
+    res = {"bound": "valu", "source": pmc.get("source")}
+    for k, t in launch_ms.items():
+        c = pmc.get(k, {})
+        act, gui = c.get("SQ_ACTIVE_INST_VALU"), c.get("GRBM_GUI_ACTIVE")
+        if act is None or gui is None or not np.isfinite(t):
+            continue
+        cycles = gui / 8.0  # GRBM_GUI_ACTIVE: summed over the 8 XCDs
+        busy = 4.0 * act / (1024.0 * cycles)
+        res[k] = {"valu_busy_frac": round(busy, 4), "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
+                  "launch_cycles": round(cycles), "launch_ms_pmc": round(cycles / 2.4e9 * 1e3, 5),
+                  "launch_ms_live": round(t, 5)}
+    if "k_step2" in res:
+        res["frac"] = res["k_step2"]["valu_busy_frac"]
+        res["kernel"] = "k_step2"
+    return res
 
 
 def seed1_pool(n_total):
@@ -85,33 +134,114 @@ def gae_roofline(n_envs, dev, T=128, reps=20):
             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
 
 
-def cpu_baseline(pool, widths, budget_s=15.0, n_envs=16):
-    """The reference's CPU execution model (NumPy step per env, sequential loop,
-    16 envs = configs/base_config.py num_envs) on one host core, bounded in time."""
-    from oracle.np_env import NpRacingEnv, NpSyncVectorEnv, NpTrack
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _np_envs(pool, widths, n_envs, first=0):
+    from oracle.np_env import NpRacingEnv, NpTrack
     from rx.track import TrackGeometry
-    envs = []
-    geo = {}
-    for i in range(n_envs):
+    envs, geo = [], {}
+    for i in range(first, first + n_envs):
         key = (id(pool[i]), widths[i])
         if key not in geo:
             g = TrackGeometry(pool[i], widths[i])
             geo[key] = NpTrack(g.waypoints, g.normals, g.segment_cache["starts"], g.segment_cache["v2"],
                                g.track_width, g.get_start_pos())
         envs.append(NpRacingEnv(geo[key], 11))
-    venv = NpSyncVectorEnv(envs)
+    return envs
+
+
+def _cpu_worker(args):
+    """Mode B worker: ONE env on one core (SyncVectorEnv of 1), random actions, bounded time."""
+    cp, width, budget_s, seed = args
+    from oracle.np_env import NpSyncVectorEnv
+    venv = NpSyncVectorEnv(_np_envs([cp], [width], 1))
+    venv.reset()
+    rng = np.random.default_rng(seed)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        venv.step(np.array([[rng.uniform(-1, 1), rng.uniform(0, 1)]], dtype=np.float32))
+        steps += 1
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
+    """BASELINE.md §3 CPU baseline on this host: oracle/np_env.py (the reference's
+    NumPy step restated, bit-exact vs the reference's golden vectors).
+
+    Mode B (the reported value): one process per host core, one env each
+    (OPENBLAS_NUM_THREADS=1), aggregate env-steps/s.  Cores = the CPUs this
+    process may run on (sched_getaffinity), capped by OMP_NUM_THREADS where the
+    host sets it (the GPU box exposes the whole machine's CPUs but gives one
+    GPU's job a 16-core share).  Mode A: the reference's plumbing, one process
+    stepping 16 envs sequentially (SyncVectorEnv, configs/base_config.py)."""
+    import multiprocessing as mp
+    from oracle.np_env import NpSyncVectorEnv
+    aff = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    cores = min(aff, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else aff
+    # Mode A
+    venv = NpSyncVectorEnv(_np_envs(pool, widths, n_envs))
     venv.reset()
     rng = np.random.default_rng(0)
     steps = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
+    while time.perf_counter() - t0 < budget_s / 2:
         a = np.stack([rng.uniform(-1, 1, n_envs), rng.uniform(0, 1, n_envs)], 1).astype(np.float32)
         venv.step(a)
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": round(steps * n_envs / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/np_env.py NumPy restatement, {n_envs} envs x {steps} sequential steps "
-                      f"({steps * n_envs} env-steps, {dt:.1f} s), seed-1 pool, random actions, 1 host core"}
+    mode_a = {"value": round(steps * n_envs / dt, 1), "unit": "env-steps/s", "cores": 1,
+              "sample": f"{n_envs} envs x {steps} sequential steps ({steps * n_envs} env-steps, {dt:.1f} s)"}
+    # Mode B
+    ctx = mp.get_context("spawn")
+    old = os.environ.get("OPENBLAS_NUM_THREADS")
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"  # inherited by the spawned workers before they import numpy
+    try:
+        with ctx.Pool(cores) as p:
+            res = p.map(_cpu_worker, [(pool[i % len(pool)], widths[i % len(pool)], budget_s, i)
+                                      for i in range(cores)])
+    finally:
+        if old is None:
+            os.environ.pop("OPENBLAS_NUM_THREADS", None)
+        else:
+            os.environ["OPENBLAS_NUM_THREADS"] = old
+    tot = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": round(tot / el, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "cpu_model": _cpu_model(), "sched_getaffinity": aff,
+            "sample": f"oracle/np_env.py NumPy restatement of RacingEnv.step (bit-exact vs the reference's golden "
+                      f"vectors), Mode B: {cores} processes x 1 env, {tot} env-steps in {el:.1f} s, seed-1 pool, "
+                      f"uniform random actions, OPENBLAS_NUM_THREADS=1",
+            "mode_a_one_core_16_envs": mode_a}
+
+
+def time_to_90(configs):
+    """Second half of BASELINE.json's metric: PPO wall-clock to 90 % success
+    (evaluate.py protocol; tools/time_to_success.py), training time only."""
+    from tools.time_to_success import run as tts
+    out = []
+    for ne, ns, shuffle in configs:
+        r = tts(num_envs=ne, num_steps=ns, eval_every=1, device_shuffle=shuffle == "device", max_minutes=2.0,
+                quiet=True)
+        out.append({"num_envs": ne, "num_steps": ns, "shuffle": shuffle, "value_s": r["value_s"],
+                    "reached_at_step": r["reached_at_step"],
+                    "updates": len(r["curve"]),
+                    "success_rate": r["curve"][-1].get("success_rate") if r["curve"] else None})
+    return {"metric": "PPO wall-clock to 90% success rate", "unit": "s", "higher_is_better": False,
+            "protocol": "evaluate.py: 40 tracks (seed 42) x 5 runs, widths by run, <= 2000 steps, stochastic "
+                        "policy, evaluated after every update; training time only (evaluations excluded)",
+            "runs": out}
 
 
 def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
@@ -173,9 +303,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--burn-in", type=int, default=100,
+                    help="untimed steps before the timed region counted together with --warmup: at least this many "
+                         "(a run that starts with every car on its start line is not the steady state)")
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cull-chunk", type=int, default=8, help="raycast chunk culling (0 = brute force)")
     ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
     ap.add_argument("--ray-order", type=int, default=2,
@@ -186,14 +319,14 @@ def main():
     ap.add_argument("--async-probe-groups", type=int, default=4,
                     help="after the timed region, also time the same workload as this many stream groups "
                          "(reported as 'async_stream_groups'; 0 = skip)")
-    ap.add_argument("--no-kernel-profile", action="store_true",
-                    help="time without per-launch timestamp events (no per-kernel durations)")
-    ap.add_argument("--sample-every", type=int, default=16,
-                    help="instrument every k-th timed step with per-kernel HIP events (1 = every step)")
+    ap.add_argument("--profile-steps", type=int, default=128,
+                    help="instrumented steps AFTER the timed region: per-kernel durations from per-wave device "
+                         "wall-clock stamps (0 = none)")
     ap.add_argument("--ppo-updates", type=int, default=2,
                     help="also time this many PPO updates (configs[1] per GPU; 0 = skip), reported as 'ppo_train'")
     ap.add_argument("--ppo-envs-per-gpu", type=int, default=4096)
     ap.add_argument("--ppo-steps", type=int, default=128)
+    ap.add_argument("--no-time-to-90", action="store_true", help="skip the PPO wall-clock-to-90%% runs")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on one GPU)")
     args = ap.parse_args()
@@ -203,6 +336,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    E = args.envs_per_gpu
+    G = args.stream_groups
+    if G < 1 or E % G:
+        raise SystemExit(f"--stream-groups {G} must divide --envs-per-gpu {E}")
+    n_total = E * world
+    pool, widths = seed1_pool(n_total)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:  # host-only work first: no process here has touched the GPU yet
+        cpu = cpu_baseline(pool, widths, budget_s=args.cpu_budget)
+
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and local >= ndev:
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs visible")
@@ -218,16 +361,11 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     from rx.vector_env import RacingVectorEnv
-    E = args.envs_per_gpu
-    G = args.stream_groups
-    if G < 1 or E % G:
-        raise SystemExit(f"--stream-groups {G} must divide --envs-per-gpu {E}")
-    n_total = E * world
-    pool, widths = seed1_pool(n_total)
     lo = rank * E
     torch.manual_seed(1234 + rank)
     scale = torch.tensor([2.0, 1.0], device=dev)
     shift = torch.tensor([-1.0, 0.0], device=dev)
+    untimed = max(args.warmup, args.burn_in)
 
     def make_groups(G):
         """G independent env groups, each stepping on its own HIP stream (a group's
@@ -242,7 +380,7 @@ def main():
         # synthetic inputs resident in HBM before the timed region: a bank of uniform random
         # actions (steer ~ U(-1, 1), throttle ~ U(0, 1)), one [n, 2] slice per step, cycled
         # when the run is longer than the bank (<= 512 MB per GPU)
-        bank = max(1, min(args.steps + args.warmup, (512 << 20) // (8 * E)))
+        bank = max(1, min(args.steps + untimed + args.profile_steps, (512 << 20) // (8 * E)))
         acts = [torch.addcmul(shift, torch.rand((bank, n, 2), device=dev), scale) for _ in range(G)]
         for e in envs:
             e.reset_device()
@@ -267,11 +405,14 @@ def main():
                         envs[g].profile(0)
         return envs, one_step, n
 
-    def timed(one_step, steps, events=None):
+    def sync_all():
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+
+    def timed(one_step, steps, events=None):
+        sync_all()
         gc.collect()
         gc.disable()  # a full collection over the 65,536-track pool stalls the host for tens of ms
         t0 = time.perf_counter()
@@ -292,29 +433,30 @@ def main():
     envs, one_step, n = make_groups(G)
     env0 = envs[0]
     n_slots = len(env0.tracks)
-    S_of_env = 2 * np.diff(env0.tracks.arrays()["wp_off"])[env0.track_of_env]
-    ray_flops_per_launch = float(np.sum(11 * S_of_env * RAY_FLOPS_PER_SEG))  # one launch = group 0's envs
-    for _ in range(args.warmup):
+    for _ in range(untimed):
         one_step()
-    # kernel durations from the dispatch packets' own timestamps (rx_profile, what rocprofv3
-    # reports) over the whole timed region; every --sample-every'th step launches the raycast
-    # on its own (dynamics phase first), so the dominant kernel has its own duration
-    half = max(1, args.sample_every // 2)
-    events = {} if args.no_kernel_profile else \
-        {k: ("split" if k % args.sample_every == 0 else "step") for k in range(args.steps) if k % half == 0}
-    env0.profile(1)
-    env0.profile(0)
-    elapsed = timed(one_step, args.steps, events)
-    prof = env0.profile_read()
-    ray_ms = prof["k_rays"][0] if "k_rays" in prof else float("nan")
+    sync_all()
+    ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
+    # ---- timed region: production steps only (one rx_step per step, no instrumentation)
+    elapsed = timed(one_step, args.steps)
     ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
+    # ---- instrumented region (after, same state distribution): per-kernel durations of the
+    # production launches (k_kin1, k_step2) on every other step; on the others the dynamics
+    # phase and the raycast run as separate launches so the raycast has a duration of its own
+    prof = {}
+    if args.profile_steps > 0:
+        events = {k: ("step" if k % 2 == 0 else "split") for k in range(args.profile_steps)}
+        env0.profile(1)
+        env0.profile(0)
+        prof_el = timed(one_step, args.profile_steps, events)
+        prof = env0.profile_read()
     for e in envs:
         e.close()
     async_probe = None
     Ga = args.async_probe_groups
     if Ga > 1 and E % Ga == 0 and Ga != G:
         a_envs, a_step, _ = make_groups(Ga)
-        for _ in range(args.warmup):
+        for _ in range(untimed):
             a_step()
         a_el = timed(a_step, args.steps)
         async_probe = {"groups": Ga, "envs_per_group": E // Ga, "value": round(n_total * args.steps / a_el, 1),
@@ -326,22 +468,17 @@ def main():
     gae = gae_roofline(E, dev) if rank == 0 else None
     ppo = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
                   args.ppo_updates) if args.ppo_updates > 0 else None
+    tt90 = None
+    if world == 1 and not args.no_time_to_90:
+        tt90 = time_to_90([(16, 2048, "numpy"), (4096, 128, "device")])
 
     if rank == 0:
         value = n_total * args.steps / elapsed
-        achieved_gbs = RAYS_BYTES_PER_ENV * n / (ray_ms * 1e-3) / 1e9
-        achieved_tf = ray_flops_per_launch / (ray_ms * 1e-3) / 1e12
-        traffic = valu_insts = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_rays.json")
-        if os.path.exists(pmc):
-            try:
-                pj = json.load(open(pmc))
-                # PMC counts are per launch: only valid for launches of the same size
-                if pj.get("envs_per_launch") == n:
-                    traffic = pj.get("hbm_bytes_per_launch")
-                    valu_insts = pj.get("valu_insts_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        ms = lambda k: prof[k][0] if k in prof else float("nan")  # noqa: E731
+        step2_ms, kin_ms, ray_ms = ms("k_step2"), ms("k_kin1"), ms("k_rays")
+        pmc = load_pmc(n)
+        step2_gbs = STEP2_BYTES_PER_ENV * n / (step2_ms * 1e-3) / 1e9
+        ray_gbs = RAYS_BYTES_PER_ENV * n / (ray_ms * 1e-3) / 1e9
         out = {
             "metric": "env-steps/sec (whole node) @65536 envs",
             "value": round(value, 1),
@@ -361,38 +498,41 @@ def main():
                        "stream_groups": G, "envs_per_launch": n,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
-                       "kernel_timing": "per-wave device wall-clock stamps (rx_profile: first wave start .. last "
-                                        "wave end) of group 0's kernels on every "
-                                        f"{max(1, args.sample_every // 2)}th timed step; every "
-                                        f"{args.sample_every}th step launches the raycast on its own",
                        "parallelism": f"env shards x{world}, no collective in the step"},
-            "roofline": {"bound": "hbm", "kernel": "k_rays", "achieved": round(achieved_gbs, 3),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": traffic, "bytes_per_env": RAYS_BYTES_PER_ENV, "envs_per_launch": n,
-                         "avg_launch_ms": round(ray_ms, 5)},
-            # the raycast is VALU-issue bound: wave-level VALU instructions per launch (PMC SQ_INSTS_VALU,
-            # profiles/pmc_k_rays.json) / launch time vs the chip's issue rate.  The SURVEY §8(d) algorithmic
-            # flop count assumes every segment is tested (brute force); culling skips most of them, so that
-            # rate is reported as an equivalent, not against the peak.
-            "compute_roofline": {"bound": "valu_issue", "kernel": "k_rays",
-                                 "achieved": round(valu_insts / (ray_ms * 1e-3) / 1e9, 1) if valu_insts else None,
-                                 "peak": VALU_WAVE_INST_PEAK_G, "unit": "G wave-VALU-instructions/s",
-                                 "frac": (valu_insts / (ray_ms * 1e-3) / 1e9 / VALU_WAVE_INST_PEAK_G)
-                                 if valu_insts else None,
-                                 "valu_insts_per_launch": valu_insts,
-                                 "brute_force_equiv_tflops": round(achieved_tf, 3),
-                                 "brute_force_flops_per_launch": ray_flops_per_launch},
-            # production step = k_kin1 + k_step2 (REWARD half beside the raycast); sampled steps run
-            # k_kin1 + k_step2_reward (REWARD half alone) + k_rays (raycast alone)
+            "steady_state": {"untimed_steps_before_timing": untimed,
+                             "episodes_ended_before_timing": ep_untimed[2],
+                             "episodes_ended_in_timed_region": ep[2],
+                             "timed_region": "production steps only: one rx_step (k_kin1 + k_step2) per step, "
+                                             "no instrumentation"},
+            # dominant kernel of the production step: k_step2 (REWARD half beside the raycast)
+            "roofline": {"bound": "hbm", "kernel": "k_step2", "achieved": round(step2_gbs, 3),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step2_gbs / HBM_PEAK_GBS,
+                         "traffic": pmc.get("k_step2", {}).get("hbm_bytes_per_launch"),
+                         "traffic_source": pmc.get("source"),
+                         "bytes_per_env": STEP2_BYTES_PER_ENV, "envs_per_launch": n,
+                         "avg_launch_ms": round(step2_ms, 5),
+                         "note": "the step is VALU-bound (branchy f64 ray/segment math): the HBM fraction is "
+                                 "expected to be tiny; see compute_roofline"},
+            "compute_roofline": compute_roofline(pmc, {"k_step2": step2_ms, "k_rays": ray_ms}),
             "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
             "kernel_launches": {k: v[1] for k, v in prof.items()},
+            "kernel_timing": f"{args.profile_steps} instrumented steps after the timed region (per-wave device "
+                             "wall-clock stamps, rx_profile: first wave start .. last wave end); even steps record "
+                             "the production launches, odd steps run k_kin1 + k_step2_reward + k_rays so the "
+                             "raycast has its own duration",
+            "k_rays_alone": {"avg_launch_ms": round(ray_ms, 5), "bytes_per_env": RAYS_BYTES_PER_ENV,
+                             "achieved_GBs": round(ray_gbs, 3),
+                             "traffic": pmc.get("k_rays", {}).get("hbm_bytes_per_launch")},
+            "step_roofline": {"kernels": "k_kin1 + k_step2", "avg_step_kernels_ms": round(kin_ms + step2_ms, 5),
+                              "bytes_per_env_step": STEP_BYTES_PER_ENV,
+                              "achieved_GBs": round(STEP_BYTES_PER_ENV * n / ((kin_ms + step2_ms) * 1e-3) / 1e9, 3)},
             "gae": gae,
-            "episodes_ended": ep[2],
             "async_stream_groups": async_probe,
             "ppo_train": ppo,
+            "time_to_90": tt90,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(pool, widths, budget_s=args.cpu_budget)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
