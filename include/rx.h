@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 12
+#define RX_ABI_VERSION 13
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -243,7 +243,7 @@ typedef struct rx_adam_config {
   int64_t offsets[RX_ADAM_MAX_TENSORS + 1];
   double beta1, beta2, eps, max_grad_norm;
 } rx_adam_config;
-#define RX_ADAM_NORM_ELEMS 1024
+#define RX_ADAM_NORM_ELEMS 64  /* gradient entries per clip-norm partial (rx_adam_workspace_floats) */
 size_t rx_adam_workspace_floats(const rx_adam_config* cfg); /* 0 for an invalid cfg */
 int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
                       float* step, const double* lr, const uint8_t* stop, float* ws, void* stream);
@@ -285,6 +285,19 @@ size_t rx_ppo_workspace_doubles(int32_t mb);
 int rx_ppo_adv_stats(const rx_ppo_batch* b, int32_t n_mb, float* stats, void* stream);
 int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, double* ws_f64, float* grad,
                           uint8_t* stop, float* kl_at_stop, void* stream);
+
+/* One whole optimizer step of the single-rank update (agent/ppo.py:170-207:
+ * minibatch forward / loss / backward, KL check, clip_grad_norm_, Adam) in
+ * three launches: rx_ppo_minibatch_grad's gradient + reduce (which also writes
+ * the per-tensor sums of squares to adam_ws and bumps *step unless it raises
+ * *stop), then the clip + Adam update of params / exp_avg / exp_avg_sq
+ * (rx_adam_clip_step's arithmetic; skipped when *stop is set).  params must be
+ * b->params; cfg the rx_adam_clip_step layout of the same P parameters;
+ * adam_ws holds rx_ppo_update_workspace_floats(obs_dim, cfg) floats. */
+size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg);
+int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
+                            float* ws_f32, double* ws_f64, float* grad, float* exp_avg, float* exp_avg_sq, float* step,
+                            const double* lr, uint8_t* stop, float* kl_at_stop, float* adam_ws, void* stream);
 
 /* Data-parallel variant of the same minibatch step (one rank's shard of a
  * global minibatch; rx.dist).  Replaces the per-rank part of

@@ -870,6 +870,35 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
   return RX_OK;
 }
 
+size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg) {
+  if ((obs_dim != 15 && obs_dim != 19) || adam_cfg_error(cfg) != RX_OK) return 0;
+  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors;
+}
+
+int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
+                            float* ws_f32, double* ws_f64, float* grad, float* exp_avg, float* exp_avg_sq, float* step,
+                            const double* lr, uint8_t* stop, float* kl_at_stop, float* adam_ws, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if ((rc = adam_cfg_error(cfg))) return rc;
+  if (!b->adv_stats) return fail(RX_EINVAL, "rx_ppo_minibatch_update: adv_stats is null");
+  if (m < 0 || (int64_t)(m + 1) * b->mb > b->n_rows)
+    return fail(RX_EINVAL, "rx_ppo_minibatch_update: m=%d out of range", m);
+  if (!params || params != b->params) return fail(RX_EINVAL, "rx_ppo_minibatch_update: params must be b->params");
+  if (cfg->offsets[cfg->n_tensors] != rx_ppo_n_params(b->obs_dim))
+    return fail(RX_EINVAL, "rx_ppo_minibatch_update: cfg covers %lld parameters, the policy has %d",
+                (long long)cfg->offsets[cfg->n_tensors], rx_ppo_n_params(b->obs_dim));
+  if (!ws_f32 || !ws_f64 || !grad || !exp_avg || !exp_avg_sq || !step || !lr || !stop || !kl_at_stop || !adam_ws)
+    return fail(RX_EINVAL, "rx_ppo_minibatch_update: null buffer");
+  const hipStream_t s = (hipStream_t)stream;
+  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step)))
+    return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
+  if ((rc = rx_launch_adam_apply(cfg, params, grad, exp_avg, exp_avg_sq, step, lr, stop, adam_ws,
+                                 rx_ppo_reduce_blocks(b->obs_dim), s)))
+    return fail(RX_EHIP, "adam launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
 int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, float* ws_f32, double* ws_f64,
                                 float* grad, float* kl_out, const uint8_t* stop, void* stream) {
   int rc = check_ppo_batch(b);

@@ -123,6 +123,11 @@ extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats
 extern "C" int rx_launch_adv_finalize(const double* moments, int n_mb, int64_t count, float* stats, hipStream_t s);
 extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, hipStream_t s);
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
-                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s);
+                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
+                                  const rx_adam_config* cfg = nullptr, float* norm_ws = nullptr,
+                                  float* step = nullptr);
+extern "C" int rx_ppo_reduce_blocks(int obs_dim);
+extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
+                                    const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s);
 extern "C" int rx_sort_pairs(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                              int32_t* vout, int n, int end_bit, hipStream_t s);

@@ -1652,9 +1652,11 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
 // (small N: one env per wave), and per step t
 //   policy   : waves 0 / 1 = actor / critic trunk on obs[t], lane = hidden
 //              unit, weights staged once in LDS (transposed: lane reads are
-//              conflict-free).  Every output is the same fmaf chain in the same
-//              order as k_policy_act (rx_ppo.hip), so actions, log-probs and
-//              values equal rx_policy_act's with the same eps bit for bit;
+//              conflict-free).  Every output is the fmaf chain, in the same
+//              order, that k_policy_act's MFMAs compute (rx_ppo.hip: inputs in
+//              order, hidden units in the order t, r, q), so actions,
+//              log-probs and values equal rx_policy_act's with the same eps
+//              bit for bit;
 //   dynamics : wave 0 runs RacingEnv.step (dyn1_env<64, FULL>, as k_dyn1<64>);
 //   raycast  : wave w casts rays w, w + kRollWaves, ... (ray_wide, as
 //              k_rays_wide) into obs[t+1].
@@ -1732,15 +1734,23 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
       const int tr = w;  // 0 = actor, 1 = critic
       if (lane < D) sX[tr][lane] = r.obs[row * D + lane];
       wave_sync();
+      // k_policy_act's MFMA chains (rx_ppo.hip): inputs d = 0 .. D-1 then the
+      // zero padding to a multiple of 4; hidden units in the order t, r, q
+      // (h = 16t + 4q + r)
       float z = 0.0f;
 #pragma unroll
       for (int d = 0; d < D; ++d) z = fmaf(sW1[tr][d * H + lane], sX[tr][d], z);
-      sH1[tr][lane] = tanhf(z + P[(tr ? L::cb1 : L::ab1) + lane]);
+#pragma unroll
+      for (int d = D; d < (D + 3) / 4 * 4; ++d) z = fmaf(0.0f, 0.0f, z);
+      sH1[tr][lane] = rx_policy::tanh_fast(z + P[(tr ? L::cb1 : L::ab1) + lane]);
       wave_sync();
       z = 0.0f;
 #pragma unroll 16
-      for (int k = 0; k < H; ++k) z = fmaf(sW2[tr][k * H + lane], sH1[tr][k], z);
-      sH2[tr][lane] = tanhf(z + P[(tr ? L::cb2 : L::ab2) + lane]);
+      for (int k = 0; k < H; ++k) {
+        const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);  // k = 16t + 4r + q -> h = 16t + 4q + r
+        z = fmaf(sW2[tr][h * H + lane], sH1[tr][h], z);
+      }
+      sH2[tr][lane] = rx_policy::tanh_fast(z + P[(tr ? L::cb2 : L::ab2) + lane]);
       wave_sync();
       if (tr == 0) {
         float lp = 0.0f;
@@ -1748,8 +1758,11 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
           const int j = lane;
           float zz = 0.0f;
 #pragma unroll 16
-          for (int k = 0; k < H; ++k) zz = fmaf(sW3[j * H + k], sH2[0][k], zz);
-          const float mu = tanhf(zz + P[L::ab3 + j]);
+          for (int k = 0; k < H; ++k) {
+            const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
+            zz = fmaf(sW3[j * H + h], sH2[0][h], zz);
+          }
+          const float mu = rx_policy::tanh_fast(zz + P[L::ab3 + j]);
           const float scale = expf(r.log_std[j]);
           const float var = scale * scale;
           const float smp = r.eps[row * NA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
@@ -1761,7 +1774,10 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         if (lane == 0) r.logprobs[row] = (0.0f + lp) + lp1;  // logp = 0; logp += lp_j in j order
       } else if (lane == 0) {
         float v = 0.0f;
-        for (int k = 0; k < H; ++k) v = fmaf(P[L::cW3 + k], sH2[1][k], v);
+        for (int k = 0; k < H; ++k) {
+          const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
+          v = fmaf(P[L::cW3 + h], sH2[1][h], v);
+        }
         r.values[row] = v + P[L::cb3];
       }
     }

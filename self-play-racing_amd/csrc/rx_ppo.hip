@@ -1,17 +1,31 @@
-// Fused PPO minibatch gradient (agent/ppo.py:170-203) for the actor-critic MLP
-// (agent/ppo.py:11-62): gather -> actor/critic forward -> clipped PG + clipped
-// value loss -> backward -> weight gradients, in one kernel, plus a
-// deterministic split-K reduce.  Replaces ~100 torch launches per minibatch
-// whose weight-gradient GEMMs (M=N<=64, K=minibatch) hipBLASLt runs on a
-// handful of workgroups (profiles/r01/ppo_update_kernel_stats.csv).
+// Fused PPO minibatch gradient (agent/ppo.py:170-203) and the rollout policy
+// step (agent/ppo.py:105-110) for the actor-critic MLP (agent/ppo.py:11-62),
+// on the f32-input matrix cores: v_mfma_f32_16x16x4_f32 is bit for bit a
+// k-ordered fmaf chain (exact f32, 64 FLOP/clk/SIMD), so every dot product
+// here is a DEFINED fmaf chain whose order k_rollout (rx_kernels.hip) repeats
+// with VALU fmaf to stay bit-identical with rx_policy_act.
 //
-// Layout: lane = minibatch row, the 4 waves of a workgroup split the hidden
-// columns; weights are wave-uniform and read through scalar loads (SGPR
-// operands of the FMAs); activations are staged in LDS (row stride 65, so
-// lane-per-row reads are bank-conflict free).  Weight gradients
-// dW = sum_r dZ[r] (x) H[r] are register tiles over the LDS-staged rows, added
-// into one partial per workgroup (<= 512 per minibatch); k_ppo_reduce sums the
-// partials in a fixed order (run-to-run deterministic, no float atomics).
+// Orientation: activations are kept TRANSPOSED, hidden unit = MFMA row, batch
+// row = MFMA column.  A 16x16 output tile leaves lane l holding batch row
+// l & 15 and hidden units 16*tile + 4*(l >> 4) + r in its 4 registers, which
+// is exactly the B-operand fragment of the next layer if that layer's k-steps
+// are ordered (tile t, register r) and an MFMA's 4-wide k index is the lane
+// group q = l >> 4: hidden unit h = 16t + 4q + r.  So Z1 -> H1 -> Z2 -> H2 ->
+// head, and dZ2 -> dH1, chain in registers with no LDS transposes; the weight
+// operand of each step is read in the matching permuted order.  Every sum
+// over hidden units therefore runs in the order t, r, q (h = 16t + 4q + r);
+// over input features in the natural order d = 0 .. D-1 (zero-padded to 4k).
+//
+// k_ppo_grad: a workgroup (4 waves) owns rows_per_wg minibatch rows of ONE
+// trunk (blockIdx.y: actor or critic), 64 per pass, 16 per wave for the
+// forward / loss / dZ2 / dH1 chains.  Weight gradients sum over batch rows,
+// which sit on lanes, so their operands go through LDS transposes of the
+// pass's 64 rows ([hidden][row]) and the MFMA k index becomes the row; wave w
+// owns output rows [16w, 16w+16) of dW2 and of dW1 (+ db1: a ones column at
+// d = D of the input tile), so the tile accumulators go straight to the
+// workgroup's partial row.  db2, dW3, db3 and the KL are per-wave sums (lane =
+// hidden unit) folded in a fixed order; k_ppo_reduce sums the partial rows in a
+// fixed order (run-to-run deterministic, no float atomics).
 #include <hip/hip_runtime.h>
 
 #include "rx.h"
@@ -21,18 +35,30 @@ namespace {
 
 using rx_policy::kH;   // hidden width (agent/ppo.py:20-29)
 using rx_policy::kNA;  // action dims
-constexpr int kT = 256;  // threads per workgroup (4 waves)
-constexpr int kRP = 64;  // rows per pass (lane = row)
-constexpr int kS = 65;   // LDS row stride of the [64][64] tiles (lane-per-row reads hit distinct banks)
-constexpr int kMaxWG = 512;  // partials per minibatch (rows per workgroup grow beyond that)
-constexpr int kSplitNetsBelow = 256;  // workgroups per minibatch below which actor / critic get their own
-#ifndef RX_PPO_KQ
-#define RX_PPO_KQ 4
+constexpr int kT = 256;      // threads per workgroup (4 waves)
+constexpr int kRP = 64;      // rows per workgroup pass (16 per wave)
+constexpr int kMaxWG = 256;  // row workgroups per minibatch and trunk (rows per workgroup grow beyond that)
+constexpr int kWS = 68;      // LDS row stride of W2 [o][i] (float4-aligned; transposed reads conflict-free)
+constexpr int kTS = 66;      // LDS row stride of the [hidden][row] transposes (operand reads conflict-free)
+#ifndef RX_PPO_MINW
+#define RX_PPO_MINW 2  // k_ppo_grad: min waves per SIMD (register budget 512 / RX_PPO_MINW)
 #endif
-constexpr int kQ = RX_PPO_KQ;  // hidden columns per weight-load group (SGPR budget vs load batching)
 
 using rx_policy::Lay;
 using rx_policy::normal_logp;
+using f4 = float __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int D>
+struct Geo {
+  static constexpr int KS1 = (D + 3) / 4;   // layer-1 k-steps: d = 4s + q, zero beyond D (15 -> 4, 19 -> 5)
+  static constexpr int DP = 4 * KS1 + 1;    // LDS row stride of W1 (odd)
+  static constexpr int NT1 = (D + 16) / 16;  // dW1 column tiles including the ones column d = D (1 / 2)
+  static constexpr int XS = 16 * NT1 + 1;   // LDS row stride of the per-wave [row][d] input tile
+};
 
 struct ppo_args {
   rx_ppo_batch b;
@@ -42,286 +68,106 @@ struct ppo_args {
   double* kl_partial;   // [n_wg]
 };
 
-__device__ __forceinline__ void put(float* p, float v, bool first) { *p = first ? v : *p + v; }
+// Weights of one trunk, read either from the flat parameter buffer (global,
+// L2-resident) or from the workgroup's LDS copy (same element order, padded
+// row strides).  o = output unit, i / d = input unit.
+struct WGlobal {
+  const float* __restrict__ W1;  // [64][D]
+  const float* __restrict__ b1;
+  const float* __restrict__ W2;  // [64][64]
+  const float* __restrict__ b2;
+  const float* __restrict__ W3;  // [n_out][64]
+  const float* __restrict__ b3;
+  int D;
+  __device__ float w1(int o, int d) const { return d < D ? W1[o * D + d] : 0.0f; }
+  __device__ float4 w2row4(int o, int i0) const { return *reinterpret_cast<const float4*>(W2 + o * kH + i0); }
+  __device__ float w2(int o, int i) const { return W2[o * kH + i]; }
+  __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
+};
+struct WLds {
+  const float* W1;  // [64][DP], zero beyond D
+  const float* b1;
+  const float* W2;  // [64][kWS]
+  const float* b2;
+  const float* W3;  // [n_out][64]
+  const float* b3;
+  int DP;
+  __device__ float w1(int o, int d) const { return W1[o * DP + d]; }
+  __device__ float4 w2row4(int o, int i0) const { return *reinterpret_cast<const float4*>(W2 + o * kWS + i0); }
+  __device__ float w2(int o, int i) const { return W2[o * kWS + i]; }
+  __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
+};
 
-// The two 64-wide tanh layers of one trunk (agent/ppo.py:20-29) for kRP rows:
-// lane = row, wave w computes hidden columns [16w, 16w+16) with the weights as
-// SGPR operands; h1 -> sH1, h2 -> sH2 (row stride kS).  Ends with the
-// barrier that publishes sH2.
-template <int D>
-__device__ __forceinline__ void hidden_layers(const float* __restrict__ W, int oW1, int ob1, int oW2, int ob2,
-                                              const float* sX, float* sH1, float* sH2, int lane, int w) {
-  constexpr int XS = D + 1;
-  {
-    float x[D];
+// Forward of one trunk for the wave's 16 rows: x[s] = X[row l15][4s + q]
+// (B fragments of layer 1).  H1 / H2 tiles in the transposed register layout;
+// y = head pre-activations: lane (q = 0, l15) holds output j in y[j].
+template <int D, int NOUT, class Wt>
+__device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>::KS1], f4 (&H1)[4], f4 (&H2)[4],
+                                            f4& y, int l15, int q) {
+  constexpr int KS1 = Geo<D>::KS1;
 #pragma unroll
-    for (int d = 0; d < D; ++d) x[d] = sX[lane * XS + d];
-    for (int cg = 0; cg < 16 / kQ; ++cg) {
-      const int c0 = w * 16 + cg * kQ;
-      float z[kQ] = {};
+  for (int mt = 0; mt < 4; ++mt) {
+    f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
+    for (int s = 0; s < KS1; ++s) z = mma(w.w1(16 * mt + l15, 4 * s + q), x[s], z);
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) z[q] = fmaf(W[oW1 + (c0 + q) * D + d], x[d], z[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) sH1[lane * kS + c0 + q] = tanhf(z[q] + W[ob1 + c0 + q]);
-    }
+    for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
   }
-  __syncthreads();
-  {
-    float h[kH];
 #pragma unroll
-    for (int k = 0; k < kH; ++k) h[k] = sH1[lane * kS + k];
-    for (int cg = 0; cg < 16 / kQ; ++cg) {
-      const int c0 = w * 16 + cg * kQ;
-      float z[kQ] = {};
+  for (int mt = 0; mt < 4; ++mt) {
+    f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int k = 0; k < kH; ++k) {
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) z[q] = fmaf(W[oW2 + (c0 + q) * kH + k], h[k], z[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) sH2[lane * kS + c0 + q] = tanhf(z[q] + W[ob2 + c0 + q]);
+    for (int t = 0; t < 4; ++t) {
+      const float4 a = w.w2row4(16 * mt + l15, 16 * t + 4 * q);
+      z = mma(a.x, H1[t][0], z);
+      z = mma(a.y, H1[t][1], z);
+      z = mma(a.z, H1[t][2], z);
+      z = mma(a.w, H1[t][3], z);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
   }
-  __syncthreads();
-}
-
-// One workgroup = rows_per_wg minibatch rows, processed kRP at a time, of both
-// networks (actor, then critic) -- or, when the minibatch gives fewer than
-// kSplitNetsBelow workgroups, of ONE network (blockIdx.y: 0 = actor, 1 =
-// critic; their losses share no parameter, so the two backward passes are
-// independent workgroups writing disjoint ranges of the same partial row: a
-// latency-bound small minibatch then runs twice the workgroups, each half the
-// chain).  Per pass and network:
-//   forward  : wave w computes hidden columns [16w, 16w+16) for the 64 rows
-//              (lane = row), weights as SGPR operands, outputs to LDS;
-//   head     : wave 0 computes mu / value and the loss gradient per row;
-//   backward : dZ2 / dZ1 likewise column-split over waves;
-//   dW       : LDS-staged register tiles over the pass's rows, added into the
-//              workgroup's partial (each entry owned by one thread).
-template <int D>
-__global__ __launch_bounds__(kT, 2) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
-                                                    float* __restrict__ partial) {
-  using L = Lay<D>;
-  constexpr int XS = D + 1;
-  if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
-  __shared__ float sX[kRP * XS];
-  __shared__ float sH1[kRP * kS];
-  __shared__ float sH2[kRP * kS];
-  __shared__ float sDZ[kRP * kS];
-  __shared__ float sHead[kRP * kNA];
-  __shared__ int64_t sSrc[kRP];
-  const rx_ppo_batch& b = a.b;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave index, provably uniform
-  float* __restrict__ out = partial + (size_t)blockIdx.x * L::Pp;
-  const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
-  const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
-  const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
-  const float invM = 1.0f / (float)b.mb;
-  const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
-  double kl = 0.0;
-  bool first = true;
-  // gridDim.y == 2: this workgroup's network only (small minibatches: twice the
-  // workgroups, half the chain each); 1: both networks, actor then critic
-  const int net0 = gridDim.y == 2 ? (int)blockIdx.y : 0, net1 = gridDim.y == 2 ? net0 + 1 : 2;
-  for (int64_t base = row0; base < row_end; base += kRP, first = false) {
-    if (t < kRP) {
-      int64_t src = base + t < row_end ? b.perm[(int64_t)a.m * b.mb + base + t] : -1;
-      sSrc[t] = (src >= 0 && src < b.n_rows) ? src : -1;  // out-of-range indices contribute nothing
-    }
-    __syncthreads();
-    for (int e = t; e < kRP * D; e += kT) {
-      const int r = e / D, d = e - r * D;
-      const int64_t src = sSrc[r];
-      sX[r * XS + d] = src >= 0 ? b.obs[src * D + d] : 0.0f;
-    }
-    const int64_t src = sSrc[lane];
-    const bool live = src >= 0;
-    __syncthreads();
-    for (int net = net0; net < net1; ++net) {
-      const int oW1 = net ? L::cW1 : L::aW1, ob1 = net ? L::cb1 : L::ab1;
-      const int oW2 = net ? L::cW2 : L::aW2, ob2 = net ? L::cb2 : L::ab2;
-      const int oW3 = net ? L::cW3 : L::aW3, ob3 = net ? L::cb3 : L::ab3;
-      const int n_out = net ? 1 : kNA;
-      hidden_layers<D>(W, oW1, ob1, oW2, ob2, sX, sH1, sH2, lane, w);
-      // ---- head and loss gradient (wave 0, lane = row)
-      if (w == 0) {
-        float h[kH];
+  const int j = l15 < NOUT ? l15 : 0;
+  const float on = l15 < NOUT ? 1.0f : 0.0f;
+  y = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int k = 0; k < kH; ++k) h[k] = sH2[lane * kS + k];
-        if (net == 0) {
-          // Normal(mu, exp(log_std)).log_prob(action).sum(-1); clipped surrogate
-          float mu[kNA], diff[kNA], var[kNA], logp = 0.0f;
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int j = 0; j < kNA; ++j) {
-            float z = 0.0f;
-#pragma unroll
-            for (int k = 0; k < kH; ++k) z = fmaf(W[oW3 + j * kH + k], h[k], z);
-            mu[j] = tanhf(z + W[ob3 + j]);
-            const float scale = expf(b.log_std[j]);
-            var[j] = scale * scale;
-            diff[j] = (live ? b.actions[src * kNA + j] : 0.0f) - mu[j];
-            logp += normal_logp(diff[j], var[j], logf(scale));
-          }
-          const float oldlp = live ? b.logprobs[src] : 0.0f;
-          const float An = live ? (b.advantages[src] - mean) / (sd + 1e-8f) : 0.0f;
-          const float ratio = expf(logp - oldlp);
-          const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
-          const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;  // torch.max splits ties
-          const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-          const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
-#pragma unroll
-          for (int j = 0; j < kNA; ++j) sHead[lane * kNA + j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
-          if (live) kl += (double)(oldlp - logp);
-        } else {
-          float v = 0.0f;
-#pragma unroll
-          for (int k = 0; k < kH; ++k) v = fmaf(W[oW3 + k], h[k], v);
-          v += W[ob3];
-          // 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
-          const float R = live ? b.returns[src] : 0.0f, ov = live ? b.values[src] : 0.0f;
-          const float vd = v - ov;
-          const float vc = ov + fminf(fmaxf(vd, -clip), clip);
-          const float e1 = v - R, e2 = vc - R;
-          const float q1 = e1 * e1, q2 = e2 * e2;
-          const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
-          const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
-          sHead[lane] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
-        }
-      }
-      __syncthreads();
-      // ---- dW3 / db3 = sum_r head[r] (x) h2[r]
-      if (t < n_out * kH) {
-        const int j = t / kH, k = t - j * kH;
-        float s = 0.0f;
-        for (int r = 0; r < kRP; ++r) s = fmaf(sHead[r * n_out + j], sH2[r * kS + k], s);
-        put(out + oW3 + t, s, first);
-      } else if (t < n_out * kH + n_out) {
-        const int j = t - n_out * kH;
-        float s = 0.0f;
-        for (int r = 0; r < kRP; ++r) s += sHead[r * n_out + j];
-        put(out + ob3 + j, s, first);
-      }
-      // ---- dz2 = (W3^T head) * (1 - h2^2), columns [16w, 16w+16)
-      for (int q = 0; q < 16; ++q) {
-        const int k = w * 16 + q;
-        float dh = 0.0f;
-        for (int j = 0; j < n_out; ++j) dh = fmaf(sHead[lane * n_out + j], W[oW3 + j * kH + k], dh);
-        const float h2 = sH2[lane * kS + k];
-        sDZ[lane * kS + k] = dh * (1.0f - h2 * h2);
-      }
-      __syncthreads();
-      // ---- dW2 / db2 = sum_r dz2[r] (x) h1[r]: 4x4 tile per thread
-      {
-        const int c0 = (t >> 4) * 4, k0 = (t & 15) * 4;
-        float acc[4][4] = {}, bacc[4] = {};
-        for (int r = 0; r < kRP; ++r) {
-          float dz[4], hh[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            dz[q] = sDZ[r * kS + c0 + q];
-            hh[q] = sH1[r * kS + k0 + q];
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(dz[i], hh[q], acc[i][q]);
-            bacc[i] += dz[i];
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) put(out + oW2 + (c0 + i) * kH + k0 + q, acc[i][q], first);
-          if (k0 == 0) put(out + ob2 + c0 + i, bacc[i], first);
-        }
-      }
-      // ---- dz1 = (W2^T dz2) * (1 - h1^2), columns [16w, 16w+16) -> sH2 (h2 is dead)
-      {
-        float dz[kH];
-#pragma unroll
-        for (int c = 0; c < kH; ++c) dz[c] = sDZ[lane * kS + c];
-        for (int kg = 0; kg < 16 / kQ; ++kg) {
-          const int k0 = w * 16 + kg * kQ;
-          float acc[kQ] = {};
-#pragma unroll
-          for (int c = 0; c < kH; ++c) {
-#pragma unroll
-            for (int q = 0; q < kQ; ++q) acc[q] = fmaf(W[oW2 + c * kH + k0 + q], dz[c], acc[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < kQ; ++q) {
-            const float h1 = sH1[lane * kS + k0 + q];
-            sH2[lane * kS + k0 + q] = acc[q] * (1.0f - h1 * h1);
-          }
-        }
-      }
-      __syncthreads();
-      // ---- dW1 / db1 = sum_r dz1[r] (x) x[r]
-      for (int e = t; e < kH * D + kH; e += kT) {
-        float s = 0.0f;
-        if (e < kH * D) {
-          const int c = e / D, d = e - c * D;
-          for (int r = 0; r < kRP; ++r) s = fmaf(sH2[r * kS + c], sX[r * XS + d], s);
-          put(out + oW1 + e, s, first);
-        } else {
-          const int c = e - kH * D;
-          for (int r = 0; r < kRP; ++r) s += sH2[r * kS + c];
-          put(out + ob1 + c, s, first);
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (w == 0 && net0 == 0) {
-    for (int o = 32; o > 0; o >>= 1) kl += __shfl_xor(kl, o, 64);
-    if (lane == 0) a.kl_partial[blockIdx.x] = kl;
-  }
+    for (int r = 0; r < 4; ++r) y = mma(on * w.w3(j, 16 * t + 4 * q + r), H2[t][r], y);
 }
 
 // Rollout policy step (agent/ppo.py:105-110, get_action_and_value on obs[t]):
-// actor + critic forward for kRP rows per workgroup, then per row
-//   action = clamp(eps * std + mu, -1, 1)        (Normal.sample() = normal_() * std + mu)
-//   logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs)
+// per row  action = clamp(eps * std + mu, -1, 1)   (Normal.sample() = normal_() * std + mu)
+//          logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs).
 // eps [N][2] is drawn by the caller with torch's normal_() so the sampling
-// stream is torch's.  Outputs go straight into the rollout buffers.
+// stream is torch's.  Wave = 16 rows of one trunk (even waves actor, odd
+// critic), weights straight from the (L2-resident) parameter buffer.
 template <int D>
-__global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const float* __restrict__ W) {
-  // blockIdx.y = trunk: 0 = actor (mu -> action, log-prob), 1 = critic (value);
-  // the two trunks are independent, so they run as separate workgroups
+__global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P) {
   using L = Lay<D>;
-  constexpr int XS = D + 1;
-  __shared__ float sX[kRP * XS];
-  __shared__ float sH1[kRP * kS];
-  __shared__ float sH2[kRP * kS];
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const bool critic = blockIdx.y != 0;
-  const int64_t base = (int64_t)blockIdx.x * kRP;
-  const int64_t row = base + lane;
+  constexpr int KS1 = Geo<D>::KS1;
+  const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (kT / 64) + (threadIdx.x >> 6));
+  const bool critic = gw & 1;
+  const int64_t row = (int64_t)(gw >> 1) * 16 + l15;
+  if ((int64_t)(gw >> 1) * 16 >= io.n) return;
   const bool live = row < io.n;
   const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
-  for (int e = t; e < kRP * D; e += kT) {
-    const int r = e / D, d = e - r * D;
-    sX[r * XS + d] = base + r < io.n ? io.obs[(base + r) * os + d] : 0.0f;
-  }
-  __syncthreads();
-  if (!critic) {
-    hidden_layers<D>(W, L::aW1, L::ab1, L::aW2, L::ab2, sX, sH1, sH2, lane, w);
-    if (w != 0 || !live) return;
-    float h[kH];
+  float x[KS1];
 #pragma unroll
-    for (int k = 0; k < kH; ++k) h[k] = sH2[lane * kS + k];
+  for (int s = 0; s < KS1; ++s) {
+    const int d = 4 * s + q;
+    x[s] = (live && d < D) ? io.obs[row * os + d] : 0.0f;
+  }
+  f4 H1[4], H2[4], y;
+  if (!critic) {
+    const WGlobal w{P + L::aW1, P + L::ab1, P + L::aW2, P + L::ab2, P + L::aW3, P + L::ab3, D};
+    mlp_forward<D, kNA>(w, x, H1, H2, y, l15, q);
+    if (q != 0 || !live) return;
     float logp = 0.0f;
 #pragma unroll
     for (int j = 0; j < kNA; ++j) {
-      float z = 0.0f;
-#pragma unroll
-      for (int k = 0; k < kH; ++k) z = fmaf(W[L::aW3 + j * kH + k], h[k], z);
-      const float mu = tanhf(z + W[L::ab3 + j]);
+      const float mu = rx_policy::tanh_fast(y[j] + P[L::ab3 + j]);
       const float scale = expf(io.log_std[j]);
       const float var = scale * scale;
       const float smp = io.eps[row * kNA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
@@ -331,13 +177,302 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
     }
     io.logprobs[row] = logp;
   } else {
-    hidden_layers<D>(W, L::cW1, L::cb1, L::cW2, L::cb2, sX, sH1, sH2, lane, w);
-    if (w != 0 || !live) return;
-    float v = 0.0f;
-#pragma unroll
-    for (int k = 0; k < kH; ++k) v = fmaf(W[L::cW3 + k], sH2[lane * kS + k], v);
-    io.values[row] = v + W[L::cb3];
+    const WGlobal w{P + L::cW1, P + L::cb1, P + L::cW2, P + L::cb2, P + L::cW3, P + L::cb3, D};
+    mlp_forward<D, 1>(w, x, H1, H2, y, l15, q);
+    if (q != 0 || !live) return;
+    io.values[row] = y[0] + P[L::cb3];
   }
+}
+
+// LDS words of k_ppo_grad's workgroup
+template <int D>
+struct GradLds {
+  static constexpr int W1 = 0, B1 = W1 + 64 * Geo<D>::DP, W2 = B1 + 64, B2 = W2 + 64 * kWS, W3 = B2 + 64,
+                       B3 = W3 + kNA * 64, WEND = B3 + 4;  // trunk weights
+  // the pass's 64 rows: [hidden][row] transposes (dZ2 then dZ1; H1 then H2), [row][d] = [X | 1], [row][j] = g
+  static constexpr int SZ = WEND, SH = SZ + 64 * kTS, SX = SH + 64 * kTS, SG = SX + kRP * Geo<D>::XS,
+                       SMALL = SG + kRP * kNA;  // per-wave db2, dW3, db3, kl
+  static constexpr int SMALL_PER = 64 + kNA * 64 + kNA + 2, TOTAL = SMALL + 4 * SMALL_PER;
+};
+
+// One trunk (NET: 0 = actor, 1 = critic) of one workgroup: rows_per_wg rows,
+// kRP = 64 per pass.  Per pass:
+//   A  each wave: forward, loss gradient g and dZ2 for its 16 rows (registers);
+//      dZ2^T, H1^T, [X | 1] and g of its rows -> LDS;                  barrier
+//   B  wave w: dW2 rows [16w, 16w+16) over the pass's 64 rows (k = row);
+//      db2 of its rows (lane = hidden unit); dH1 = W2^T dZ2, dZ1 (registers); barrier
+//   C  each wave: dZ1^T, H2^T of its rows -> LDS;                       barrier
+//   D  wave w: dW1 (+ db1) rows [16w, 16w+16); dW3 / db3 of its rows;   barrier
+// Each wave owns distinct output tiles, so the tile accumulators go straight
+// to the partial row; the per-wave db2 / dW3 / db3 / KL sums are folded in a
+// fixed order ((w0 + w2) + (w1 + w3)).
+template <int D, int NET>
+__device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* __restrict__ W, float* lds,
+                                               float* __restrict__ out) {
+  using L = Lay<D>;
+  using G = Geo<D>;
+  using S = GradLds<D>;
+  constexpr int NOUT = NET ? 1 : kNA, KS1 = G::KS1, NT1 = G::NT1;
+  constexpr int oW1 = NET ? L::cW1 : L::aW1, ob1 = NET ? L::cb1 : L::ab1, oW2 = NET ? L::cW2 : L::aW2,
+                ob2 = NET ? L::cb2 : L::ab2, oW3 = NET ? L::cW3 : L::aW3, ob3 = NET ? L::cb3 : L::ab3;
+  const rx_ppo_batch& b = a.b;
+  const int t0 = threadIdx.x, lane = t0 & 63, l15 = lane & 15, q = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(t0 >> 6);
+  // ---- stage the trunk's weights (zero-padded rows)
+  for (int e = t0; e < 64 * G::DP; e += kT) {
+    const int o = e / G::DP, d = e - o * G::DP;
+    lds[S::W1 + e] = d < D ? W[oW1 + o * D + d] : 0.0f;
+  }
+  for (int e = t0; e < 64 * 64; e += kT) lds[S::W2 + (e >> 6) * kWS + (e & 63)] = W[oW2 + e];
+  for (int e = t0; e < 64; e += kT) {
+    lds[S::B1 + e] = W[ob1 + e];
+    lds[S::B2 + e] = W[ob2 + e];
+  }
+  for (int e = t0; e < NOUT * 64; e += kT) lds[S::W3 + e] = W[oW3 + e];
+  if (t0 < NOUT) lds[S::B3 + t0] = W[ob3 + t0];
+  __syncthreads();
+  const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
+  float* sZ = lds + S::SZ;  // [hidden][row]
+  float* sH = lds + S::SH;  // [hidden][row]
+  float* sX = lds + S::SX;  // [row][d]
+  float* sG = lds + S::SG;  // [row][j]
+  const int rr = 16 * wv + l15;  // this lane's row within the pass
+
+  const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
+  const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
+  const float invM = 1.0f / (float)b.mb;
+  const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
+  float var[kNA], lsc[kNA];
+#pragma unroll
+  for (int j = 0; j < kNA; ++j) {
+    const float scale = expf(b.log_std[j]);
+    var[j] = scale * scale;
+    lsc[j] = logf(scale);
+  }
+  f4 acc2[4], acc1[NT1];  // dW2 rows [16 wv, +16) x 4 column tiles; dW1 (+ db1) rows [16 wv, +16)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc2[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < NT1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  float db2 = 0.0f, dw3[NOUT] = {}, db3 = 0.0f;  // lane = hidden unit (db2, dW3), output (db3)
+  double kl = 0.0;
+  // inputs of a row, loaded one pass ahead (the perm index two passes ahead):
+  // the dependent gathers perm -> obs / actions / ... never stall a pass
+  struct RowIn {
+    float x[KS1], s0, s1, s2, s3;  // actor: action 0/1, old log-prob, advantage; critic: return, value
+  };
+  auto src_of = [&](int64_t base) -> int64_t {
+    const int64_t r_mb = base + rr;
+    if (r_mb >= row_end) return -1;
+    const int64_t v = b.perm[(int64_t)a.m * b.mb + r_mb];
+    return (v >= 0 && v < b.n_rows) ? v : -1;  // out-of-range indices contribute nothing
+  };
+  auto load_row = [&](int64_t src) -> RowIn {
+    RowIn in;
+    const bool ok = src >= 0;
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const int d = 4 * s + q;
+      in.x[s] = (ok && d < D) ? b.obs[src * D + d] : 0.0f;
+    }
+    if (NET == 0) {
+      in.s0 = ok ? b.actions[src * kNA] : 0.0f;
+      in.s1 = ok ? b.actions[src * kNA + 1] : 0.0f;
+      in.s2 = ok ? b.logprobs[src] : 0.0f;
+      in.s3 = ok ? b.advantages[src] : 0.0f;
+    } else {
+      in.s0 = ok ? b.returns[src] : 0.0f;
+      in.s1 = ok ? b.values[src] : 0.0f;
+      in.s2 = in.s3 = 0.0f;
+    }
+    return in;
+  };
+  int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
+  RowIn cur = load_row(src);
+  for (int64_t base = row0; base < row_end; base += kRP) {
+    // ================================================================ A
+    const int64_t src_nn = src_of(base + 2 * kRP);
+    const RowIn nxt = load_row(src_n);
+    const bool live = src >= 0;
+    float x[KS1];
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const int d = 4 * s + q;
+      x[s] = cur.x[s];
+      sX[rr * G::XS + d] = d == D ? 1.0f : x[s];  // the ones column (d = D) carries db1
+    }
+    f4 H1[4], H2[4], y;
+    mlp_forward<D, NOUT>(w, x, H1, H2, y, l15, q);
+    float g[NOUT];  // d loss / d head pre-activation, row rr (every lane of the row)
+    if (NET == 0) {
+      float mu[kNA], diff[kNA], logp = 0.0f;
+#pragma unroll
+      for (int j = 0; j < kNA; ++j) {
+        mu[j] = rx_policy::tanh_fast(__shfl(y[j], l15, 64) + w.b3[j]);
+        diff[j] = (j ? cur.s1 : cur.s0) - mu[j];
+        logp += normal_logp(diff[j], var[j], lsc[j]);
+      }
+      const float oldlp = cur.s2;
+      const float An = live ? (cur.s3 - mean) / (sd + 1e-8f) : 0.0f;
+      const float ratio = expf(logp - oldlp);
+      const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
+      const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;  // torch.max splits ties
+      const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+      const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) g[j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
+      if (live && q == 0) kl += (double)(oldlp - logp);
+    } else {
+      const float v = __shfl(y[0], l15, 64) + w.b3[0];
+      // 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
+      const float R = cur.s0, ov = cur.s1;
+      const float vd = v - ov;
+      const float vc = ov + fminf(fmaxf(vd, -clip), clip);
+      const float e1 = v - R, e2 = vc - R;
+      const float q1 = e1 * e1, q2 = e2 * e2;
+      const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
+      const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
+      g[0] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
+    }
+    f4 dZ[4];  // dZ2 = (W3^T g) * (1 - H2^2)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * t + 4 * q + r;
+        float dh = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NOUT; ++j) dh = fmaf(w.w3(j, h), g[j], dh);
+        dZ[t][r] = dh * (1.0f - H2[t][r] * H2[t][r]);
+        sZ[h * kTS + rr] = dZ[t][r];
+        sH[h * kTS + rr] = H1[t][r];
+      }
+    if (q == 0) {
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) sG[rr * kNA + j] = g[j];
+    }
+    __syncthreads();
+    // ================================================================ B
+    // dW2[16 wv + i][16 nt + c] += sum_rows dZ2 x H1 (k = row 4s + q)
+#pragma unroll 4
+    for (int s = 0; s < kRP / 4; ++s) {
+      const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
+      float bv[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bv[nt] = sH[(16 * nt + l15) * kTS + 4 * s + q];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma(av, bv[nt], acc2[nt]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) db2 += sZ[lane * kTS + 16 * wv + k];  // lane = hidden unit, own rows
+    // dH1 = W2^T dZ2 (k = output unit o = 16t + 4q + r), dZ1 = dH1 * (1 - H1^2) in registers
+    f4 dZ1[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z = mma(w.w2(16 * t + 4 * q + r, 16 * mt + l15), dZ[t][r], z);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
+    }
+    __syncthreads();
+    // ================================================================ C
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * t + 4 * q + r;
+        sZ[h * kTS + rr] = dZ1[t][r];
+        sH[h * kTS + rr] = H2[t][r];
+      }
+    __syncthreads();
+    // ================================================================ D
+    // dW1[16 wv + i][d] (+ db1 at d = D) += sum_rows dZ1 x [X | 1]
+#pragma unroll 4
+    for (int s = 0; s < kRP / 4; ++s) {
+      const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
+      float bv[NT1];
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt) {
+        const int d = 16 * nt + l15;
+        bv[nt] = d <= D ? sX[(4 * s + q) * G::XS + d] : 0.0f;
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt) acc1[nt] = mma(av, bv[nt], acc1[nt]);
+    }
+    // dW3 / db3 of own rows (lane = hidden unit / output)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = 16 * wv + k;
+      const float h2 = sH[lane * kTS + row];
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) dw3[j] = fmaf(sG[row * kNA + j], h2, dw3[j]);
+      if (lane < NOUT) db3 += sG[row * kNA + lane];
+    }
+    __syncthreads();  // the next pass overwrites the transposes
+    src = src_n;
+    src_n = src_nn;
+    cur = nxt;
+  }
+  // ---- tile accumulators -> the partial row (each wave owns rows [16 wv, 16 wv + 16))
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = 16 * wv + 4 * q + r;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) out[oW2 + o * kH + 16 * nt + l15] = acc2[nt][r];
+#pragma unroll
+    for (int nt = 0; nt < NT1; ++nt) {
+      const int d = 16 * nt + l15;
+      if (d < D)
+        out[oW1 + o * D + d] = acc1[nt][r];
+      else if (d == D)
+        out[ob1 + o] = acc1[nt][r];
+    }
+  }
+  // ---- per-wave small sums, folded over the waves in a fixed order
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) kl += __shfl_xor(kl, o, 64);
+  float* small = lds + S::SMALL + wv * S::SMALL_PER;
+  small[lane] = db2;
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) small[64 + j * 64 + lane] = dw3[j];
+  if (lane < NOUT) small[64 + kNA * 64 + lane] = db3;
+  if (lane == 0) reinterpret_cast<double*>(small + 64 + kNA * 64 + kNA)[0] = kl;  // 8-aligned: SMALL_PER is even
+  __syncthreads();
+  if (wv != 0) return;
+  const float* sm = lds + S::SMALL;
+  for (int e = lane; e < 64 + NOUT * 64 + NOUT; e += 64) {
+    const int k = e < 64 + NOUT * 64 ? e : 64 + kNA * 64 + (e - 64 - NOUT * 64);
+    const float v = (sm[k] + sm[2 * S::SMALL_PER + k]) + (sm[S::SMALL_PER + k] + sm[3 * S::SMALL_PER + k]);
+    if (e < 64)
+      out[ob2 + e] = v;
+    else if (e < 64 + NOUT * 64)
+      out[oW3 + (e - 64)] = v;
+    else
+      out[ob3 + (e - 64 - NOUT * 64)] = v;
+  }
+  if (NET == 0 && lane == 0) {
+    const double* kd = reinterpret_cast<const double*>(sm + 64 + kNA * 64 + kNA);
+    const int st = S::SMALL_PER / 2;
+    a.kl_partial[blockIdx.x] = (kd[0] + kd[2 * st]) + (kd[st] + kd[3 * st]);
+  }
+}
+
+// blockIdx.y = trunk (0 actor, 1 critic: their losses share no parameter, so
+// they write disjoint ranges of the same partial row); blockIdx.x = row group.
+template <int D>
+__global__ __launch_bounds__(kT, RX_PPO_MINW) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
+                                                    float* __restrict__ partial) {
+  if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
+  __shared__ __attribute__((aligned(16))) float lds[GradLds<D>::TOTAL];
+  float* out = partial + (size_t)blockIdx.x * Lay<D>::Pp;
+  if (blockIdx.y == 0)
+    ppo_grad_trunk<D, 0>(a, W, lds, out);
+  else
+    ppo_grad_trunk<D, 1>(a, W, lds, out);
 }
 
 // grad[p] = sum_w partial[w][p] in a fixed order.  One workgroup owns 64
@@ -350,10 +485,22 @@ __global__ __launch_bounds__(kT, 2) void k_policy_act(rx_policy_io io, const flo
 constexpr int kRedCols = 16;                    // float4 columns per workgroup
 constexpr int kRedSlices = 1024 / kRedCols;     // 64
 constexpr int kRedBatch = 8;                    // partial rows loaded per thread per round trip
+// With ``norm`` (the fused minibatch update, rx_ppo_minibatch_update) each
+// workgroup also writes the per-tensor sums of squares of its 64 gradient
+// entries to norm->ws[block][tensor] (clip_grad_norm_'s per-tensor norms, folded
+// by k_adam_apply) and block 0 bumps the Adam step count unless it raises the
+// early-stop flag: the optimizer launch that follows needs no norm pass.
+struct norm_args {
+  rx_adam_config cfg;
+  float* ws;    // [gridDim.x][n_tensors]
+  float* step;  // Adam step count
+};
+
 __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
                                                      const double* __restrict__ klp, int n_wg, int P, int Pp, int mb,
                                                      float kl_target, float scale, float* grad, uint8_t* stop,
-                                                     float* kl_at_stop, float* kl_out) {
+                                                     float* kl_at_stop, float* kl_out, const norm_args* norm_p,
+                                                     norm_args norm) {
   if (*stop) return;
   __shared__ float4 red[kRedSlices][kRedCols];
   const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
@@ -392,7 +539,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
     red2[sl][c] = t;
   }
   __syncthreads();
-  if (threadIdx.x < kRedCols && p4 < P) {
+  if (threadIdx.x < kRedCols) {  // (lanes past P take part in the norm tree with zeros)
     float4 t = red2[0][c];
     for (int k = 1; k < 8; ++k) {
       const float4 v = red2[k][c];
@@ -403,6 +550,24 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
     }
     const float o[4] = {t.x, t.y, t.z, t.w};
     for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o[q] * scale;
+    if (norm_p) {  // per-tensor sums of squares of this block's 64 entries, lanes 0..15 in a fixed tree
+      const int nt = norm.cfg.n_tensors;
+      const int64_t b0 = (int64_t)blockIdx.x * 4 * kRedCols, b1 = b0 + 4 * kRedCols;
+      for (int u = 0; u < nt; ++u) {
+        const int64_t lo = norm.cfg.offsets[u], hi = norm.cfg.offsets[u + 1];
+        if (hi <= b0 || lo >= b1) {  // tensor outside this block (uniform over the 16 lanes)
+          if (threadIdx.x == 0) norm.ws[(size_t)blockIdx.x * nt + u] = 0.0f;
+          continue;
+        }
+        float sq = 0.0f;
+        for (int k = 0; k < 4; ++k) {
+          const float gk = o[k] * scale;
+          if (p4 + k < P && p4 + k >= lo && p4 + k < hi) sq = fmaf(gk, gk, sq);
+        }
+        for (int off = 1; off < kRedCols; off <<= 1) sq += __shfl_xor(sq, off, kRedCols);
+        if (threadIdx.x == 0) norm.ws[(size_t)blockIdx.x * nt + u] = sq;
+      }
+    }
   }
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
@@ -415,6 +580,8 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
     } else if (lane == 0 && kl > kl_target) {
       *kl_at_stop = kl;
       *stop = 1;  // read by the optimizer launch that follows on the stream
+    } else if (lane == 0 && norm_p) {
+      *norm.step += 1.0f;  // the Adam step this minibatch takes (k_adam_apply reads it)
     }
   }
 }
@@ -519,30 +686,43 @@ extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* sto
   return (int)hipGetLastError();
 }
 
+extern "C" int rx_ppo_reduce_blocks(int obs_dim) {
+  const int Pp = obs_dim == 15 ? Lay<15>::Pp : Lay<19>::Pp;
+  return (Pp + 4 * kRedCols - 1) / (4 * kRedCols);
+}
+
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
-                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s) {
+                                  float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
+                                  const rx_adam_config* cfg, float* norm_ws, float* step) {
   const int rp = rows_per_wg(b->mb);
   const int n_wg = (b->mb + rp - 1) / rp;
-  const int ny = n_wg < kSplitNetsBelow ? 2 : 1;
   ppo_args a{*b, m, rp, stop, klp};
   int P, Pp;
   if (b->obs_dim == 15) {
-    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg, ny), dim3(kT), 0, s, a, b->params, partial);
+    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
-    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg, ny), dim3(kT), 0, s, a, b->params, partial);
+    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
-  hipLaunchKernelGGL(k_ppo_reduce, dim3((Pp + 4 * kRedCols - 1) / (4 * kRedCols)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
-                     b->kl_target, scale, grad, stop, kl_at_stop, kl_out);
+  norm_args na{};
+  const norm_args* np = nullptr;
+  if (cfg) {
+    na = norm_args{*cfg, norm_ws, step};
+    np = &na;  // only its non-nullness reaches the device: the struct travels by value
+  }
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(rx_ppo_reduce_blocks(b->obs_dim)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp,
+                     b->mb, b->kl_target, scale, grad, stop, kl_at_stop, kl_out, np, na);
   return (int)hipGetLastError();
 }
 
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
-  const int n_wg = (int)((io->n + kRP - 1) / kRP);
+  // one wave per 16 rows and trunk, 4 waves per workgroup
+  const int64_t waves = 2 * ((io->n + 15) / 16);
+  const int n_wg = (int)((waves + 3) / 4);
   if (io->obs_dim == 15)
-    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg, 2), dim3(kT), 0, s, *io, io->params);
+    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
   else
-    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg, 2), dim3(kT), 0, s, *io, io->params);
+    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
   return (int)hipGetLastError();
 }

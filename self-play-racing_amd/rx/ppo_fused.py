@@ -4,8 +4,8 @@
 advantages, returns, values -- persistent buffers), the flat policy
 parameters of rx.optim.FlatAdam and the epoch's index tensor, and issues per
 epoch: one rx_ppo_adv_stats launch (every minibatch's advantage mean/std),
-then per minibatch rx_ppo_minibatch_grad (forward + loss + backward + split-K
-reduce + KL check) followed by rx_adam_clip_step.  Everything is enqueued on
+then per minibatch rx_ppo_minibatch_update (forward + loss + backward,
+split-K reduce + KL check + clip norms, Adam).  Everything is enqueued on
 the current stream with no host sync, so PPO captures an epoch as one graph.
 """
 import torch
@@ -80,12 +80,26 @@ class FusedMinibatchGrad:
                                          _lib.ptr(kl_at_stop), s), "rx_ppo_kl_check")
             flat.step(stop=stop)
 
+    def update(self, m, stop, kl_at_stop, stream=None):
+        """One optimizer step on minibatch m (rx_ppo_minibatch_update: gradient,
+        reduce + clip norms + step count, Adam: three launches)."""
+        f = self.flat
+        ws = self.__dict__.get("adam_ws")
+        if ws is None:
+            n = self.L.rx_ppo_update_workspace_floats(self.batch.obs_dim, f.cfg)
+            if n == 0:
+                raise RuntimeError(self.L.rx_last_error().decode())
+            ws = self.adam_ws = torch.empty(n, dtype=torch.float32, device=self.stats.device)
+        _lib.check(self.L.rx_ppo_minibatch_update(
+            self.batch, int(m), f.cfg, _lib.ptr(f.flat_param), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
+            _lib.ptr(f.flat_grad), _lib.ptr(f.exp_avg), _lib.ptr(f.exp_avg_sq), _lib.ptr(f.step_t), _lib.ptr(f.lr_t),
+            _lib.ptr(stop), _lib.ptr(kl_at_stop), _lib.ptr(ws), _lib.stream_ptr(stream)), "rx_ppo_minibatch_update")
+
     def epoch(self, stop, kl_at_stop):
         """All minibatch steps of one epoch over the current perm."""
         self.adv_stats()
         for m in range(self.n_mb):
-            self.grad(m, stop, kl_at_stop)
-            self.flat.step(stop=stop)
+            self.update(m, stop, kl_at_stop)
 
 
 class PolicyAct:

@@ -78,4 +78,10 @@ def test_update_abi_validates_without_device():
     assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 0
     cfg.n_tensors, cfg.beta1, cfg.beta2 = 2, 0.9, 0.999
     cfg.offsets[1], cfg.offsets[2] = 1000, 2050
-    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 3 * 2  # ceil(2050 / 1024) slices x 2 tensors
+    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 33 * 2  # ceil(2050 / 64) norm blocks x 2 tensors
+    # fused minibatch update (ABI v13): argument checks before any launch
+    assert L.rx_ppo_update_workspace_floats(15, ctypes.byref(cfg)) > 0
+    assert L.rx_ppo_update_workspace_floats(7, ctypes.byref(cfg)) == 0
+    b.obs_dim = 15
+    args = [None] * 12
+    assert L.rx_ppo_minibatch_update(ctypes.byref(b), 0, ctypes.byref(cfg), *args) == _lib.RX_EINVAL

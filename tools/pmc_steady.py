@@ -94,14 +94,19 @@ def main():
     ap.add_argument("--scratch", default=os.path.join(os.environ.get("GRAFT_REPO_ROOT", ROOT), "gpurun_out",
                                                       "pmc_steady"))
     ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--cmd", default=None, help="profile this command instead of bench.py (e.g. tools/bench_ppo.py ...)")
+    ap.add_argument("--passes", default=None, help="counter passes 'C1,C2;C3,...' instead of the default four")
     ap.add_argument("--bench-args", default="--steps 24 --burn-in 100 --warmup 0 --profile-steps 16 "
                                             "--no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 "
                                             "--no-time-to-90")
     args = ap.parse_args()
     cmd = [sys.executable, "bench.py", "--envs-per-gpu", str(args.envs)] + args.bench_args.split()
+    if args.cmd:
+        cmd = [sys.executable] + args.cmd.split()
+    passes = [p.split(",") for p in args.passes.split(";")] if args.passes else PASSES
     acc = defaultdict(dict)
-    for i, counters in enumerate(PASSES):
-        d = run_pass(args.scratch, i, counters, cmd, args.timeout, required=i < 3)
+    for i, counters in enumerate(passes):
+        d = run_pass(args.scratch, i, counters, cmd, args.timeout, required=args.passes is not None or i < 3)
         if d is None:
             continue
         for (k, g), cs in collect(d).items():
@@ -110,7 +115,7 @@ def main():
                 acc[(k, g)][c] = sum(keep) / len(keep)
                 acc[(k, g)]["dispatches_seen"] = max(acc[(k, g)].get("dispatches_seen", 0), len(vals))
     res = {"envs_per_launch": args.envs, "command": " ".join(["rocprofv3", "--pmc", "<pass>", "--"] + cmd[1:]),
-           "passes": PASSES, "last_dispatches_kept": args.last,
+           "passes": passes, "last_dispatches_kept": args.last,
            "units": "per launch: FETCH_SIZE / WRITE_SIZE in bytes (rocprofv3 KiB x 1024, raw, no x2 read "
                     "correction); SQ_* summed over waves (quad-cycles for *_CYCLES / WAIT / ACTIVE); "
                     "GRBM_GUI_ACTIVE summed over 8 XCDs"}
