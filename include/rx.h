@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 13
+#define RX_ABI_VERSION 14
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -260,6 +260,13 @@ int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, fl
  * kl_target it sets *stop (and *kl_at_stop) so the rx_adam_clip_step that
  * follows is skipped.  With *stop already set the call does nothing.
  * fp32; equal to torch autograd within float rounding (tests/test_ppo_fused_gpu.py). */
+/* Matrix-core precision of the policy kernels (rx_ppo_batch / rx_policy_io):
+ * FP32 = v_mfma_f32_16x16x4_f32, exact float32 products (an fmaf chain);
+ * BF16 = v_mfma_f32_16x16x32_bf16: weights / activations / gradients rounded to
+ * bf16 as matrix operands, float32 accumulation, float32 everywhere else
+ * (BASELINE.json configs[1], "PPO bf16"). */
+#define RX_PREC_FP32 0
+#define RX_PREC_BF16 1
 typedef struct rx_ppo_batch {
   int32_t obs_dim;          /* D: 15 (single-agent) or 19 (two-car) */
   int32_t mb;               /* minibatch rows */
@@ -275,6 +282,7 @@ typedef struct rx_ppo_batch {
   const float* log_std;     /* [2] Agent.log_std buffer */
   const float* adv_stats;   /* [n_mb][2] (mean, unbiased std) from rx_ppo_adv_stats */
   float clip_coef, vf_coef, kl_target;
+  int32_t precision;        /* RX_PREC_FP32 (default) or RX_PREC_BF16 (ABI v14) */
 } rx_ppo_batch;
 /* P for obs_dim (10,563 for 15, 11,075 for 19; 0 = unsupported). */
 int rx_ppo_n_params(int32_t obs_dim);
@@ -347,6 +355,7 @@ typedef struct rx_policy_io {
   float* values;          /* [n] out */
   int64_t obs_stride;     /* e.g. 2*19 for one car's rows of a two-car [n][2][19] buffer */
   int64_t act_stride;     /* e.g. 4 for one car's actions in [n][2][2] */
+  int32_t precision;      /* RX_PREC_FP32 (default) or RX_PREC_BF16 (ABI v14) */
 } rx_policy_io;
 int rx_policy_act(const rx_policy_io* io, void* stream);
 

@@ -823,6 +823,8 @@ static int check_ppo_batch(const rx_ppo_batch* b) {
   if (!b) return fail(RX_EINVAL, "rx_ppo: batch is null");
   if (b->obs_dim != 15 && b->obs_dim != 19) return fail(RX_EINVAL, "rx_ppo: obs_dim=%d (15 or 19)", b->obs_dim);
   if (b->mb <= 0 || b->n_rows <= 0) return fail(RX_EINVAL, "rx_ppo: mb=%d n_rows=%lld", b->mb, (long long)b->n_rows);
+  if (b->precision != RX_PREC_FP32 && b->precision != RX_PREC_BF16)
+    return fail(RX_EINVAL, "rx_ppo: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", b->precision);
   if (!b->obs || !b->actions || !b->logprobs || !b->advantages || !b->returns || !b->values || !b->perm ||
       !b->params || !b->log_std)
     return fail(RX_EINVAL, "rx_ppo: null buffer");
@@ -927,6 +929,8 @@ int rx_policy_act(const rx_policy_io* io, void* stream) {
   if (!io) return fail(RX_EINVAL, "rx_policy_act: io is null");
   if (io->obs_dim != 15 && io->obs_dim != 19) return fail(RX_EINVAL, "rx_policy_act: obs_dim=%d (15 or 19)", io->obs_dim);
   if (io->n <= 0) return fail(RX_EINVAL, "rx_policy_act: n=%lld", (long long)io->n);
+  if (io->precision != RX_PREC_FP32 && io->precision != RX_PREC_BF16)
+    return fail(RX_EINVAL, "rx_policy_act: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", io->precision);
   if ((io->obs_stride != 0 && io->obs_stride < io->obs_dim) || (io->act_stride != 0 && io->act_stride < 2))
     return fail(RX_EINVAL, "rx_policy_act: row strides overlap (obs %lld, act %lld)", (long long)io->obs_stride,
                 (long long)io->act_stride);

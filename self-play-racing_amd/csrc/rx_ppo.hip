@@ -52,12 +52,47 @@ __device__ __forceinline__ f4 mma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 precision (rx_ppo_batch / rx_policy_io .precision = RX_PREC_BF16,
+// config["policy_dtype"] = "bf16"): the same products on
+// v_mfma_f32_16x16x32_bf16, operands rounded to bf16, f32 accumulation.
+// Lane l holds A[row l & 15][k = 8(l >> 4) + j] and B[k][col l & 15], j < 8.
+// A k-step of 32 hidden units is ordered so that its B fragment is lane-local
+// in the transposed register layout: slot (q, j) <-> hidden unit
+// h = 32s + 16(j >> 2) + 4q + (j & 3), i.e. tile 2s + (j >> 2), register j & 3.
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+constexpr int kF32 = RX_PREC_FP32, kBF16 = RX_PREC_BF16;
+
+__device__ __forceinline__ f4 mma16(bf8 a, bf8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf8 to_bf8(float4 lo, float4 hi) {
+  bf8 v;
+  v[0] = (__bf16)lo.x, v[1] = (__bf16)lo.y, v[2] = (__bf16)lo.z, v[3] = (__bf16)lo.w;
+  v[4] = (__bf16)hi.x, v[5] = (__bf16)hi.y, v[6] = (__bf16)hi.z, v[7] = (__bf16)hi.w;
+  return v;
+}
+__device__ __forceinline__ bf8 to_bf8(const f4& lo, const f4& hi) {
+  return to_bf8(make_float4(lo[0], lo[1], lo[2], lo[3]), make_float4(hi[0], hi[1], hi[2], hi[3]));
+}
+
+// 8 consecutive floats of an LDS row (8-byte aligned) as a bf16 fragment
+__device__ __forceinline__ bf8 rows8(const float* p) {
+  const float2 a = *reinterpret_cast<const float2*>(p), b = *reinterpret_cast<const float2*>(p + 2),
+               c = *reinterpret_cast<const float2*>(p + 4), d = *reinterpret_cast<const float2*>(p + 6);
+  return to_bf8(make_float4(a.x, a.y, b.x, b.y), make_float4(c.x, c.y, d.x, d.y));
+}
+
 template <int D>
 struct Geo {
   static constexpr int KS1 = (D + 3) / 4;   // layer-1 k-steps: d = 4s + q, zero beyond D (15 -> 4, 19 -> 5)
   static constexpr int DP = 4 * KS1 + 1;    // LDS row stride of W1 (odd)
   static constexpr int NT1 = (D + 16) / 16;  // dW1 column tiles including the ones column d = D (1 / 2)
   static constexpr int XS = 16 * NT1 + 1;   // LDS row stride of the per-wave [row][d] input tile
+  // input fragment per lane: fp32 x[s] = X[row][4s + q] (s < KS1); bf16 x[j] = X[row][8q + j] (j < 8)
+  template <int PREC>
+  static constexpr int XN = PREC == kBF16 ? 8 : KS1;
+  template <int PREC>
+  __device__ static constexpr int d_of(int s, int q) { return PREC == kBF16 ? 8 * q + s : 4 * s + q; }
 };
 
 struct ppo_args {
@@ -92,48 +127,81 @@ struct WLds {
   const float* W3;  // [n_out][64]
   const float* b3;
   int DP;
-  __device__ float w1(int o, int d) const { return W1[o * DP + d]; }
+  __device__ float w1(int o, int d) const { return d < DP ? W1[o * DP + d] : 0.0f; }  // zero-padded to DP
   __device__ float4 w2row4(int o, int i0) const { return *reinterpret_cast<const float4*>(W2 + o * kWS + i0); }
   __device__ float w2(int o, int i) const { return W2[o * kWS + i]; }
   __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
 };
 
-// Forward of one trunk for the wave's 16 rows: x[s] = X[row l15][4s + q]
-// (B fragments of layer 1).  H1 / H2 tiles in the transposed register layout;
-// y = head pre-activations: lane (q = 0, l15) holds output j in y[j].
-template <int D, int NOUT, class Wt>
-__device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>::KS1], f4 (&H1)[4], f4 (&H2)[4],
-                                            f4& y, int l15, int q) {
+// Forward of one trunk for the wave's 16 rows: x = the lane's input fragment
+// (Geo::d_of).  H1 / H2 tiles in the transposed register layout; y = head
+// pre-activations: lane (q = 0, l15) holds output j in y[j].
+template <int D, int NOUT, int PREC, class Wt>
+__device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>::template XN<PREC>], f4 (&H1)[4],
+                                            f4 (&H2)[4], f4& y, int l15, int q) {
   constexpr int KS1 = Geo<D>::KS1;
+  const int j3 = l15 < NOUT ? l15 : 0;
+  const float on = l15 < NOUT ? 1.0f : 0.0f;
+  if constexpr (PREC == kBF16) {
+    const bf8 bx = to_bf8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]));
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int mt = 0; mt < 4; ++mt) {  // layer 1: one k-step (d = 8q + j < 32)
+      const int o = 16 * mt + l15;
+      const float4 lo = make_float4(w.w1(o, 8 * q), w.w1(o, 8 * q + 1), w.w1(o, 8 * q + 2), w.w1(o, 8 * q + 3));
+      const float4 hi = make_float4(w.w1(o, 8 * q + 4), w.w1(o, 8 * q + 5), w.w1(o, 8 * q + 6), w.w1(o, 8 * q + 7));
+      const f4 z = mma16(to_bf8(lo, hi), bx, f4{0.0f, 0.0f, 0.0f, 0.0f});
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) z = mma(w.w1(16 * mt + l15, 4 * s + q), x[s], z);
+      for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
+    }
+    const bf8 bh[2] = {to_bf8(H1[0], H1[1]), to_bf8(H1[2], H1[3])};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
-  }
+    for (int mt = 0; mt < 4; ++mt) {
+      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int s = 0; s < 2; ++s)
+        z = mma16(to_bf8(w.w2row4(16 * mt + l15, 32 * s + 4 * q), w.w2row4(16 * mt + l15, 32 * s + 16 + 4 * q)),
+                  bh[s], z);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float4 a = w.w2row4(16 * mt + l15, 16 * t + 4 * q);
-      z = mma(a.x, H1[t][0], z);
-      z = mma(a.y, H1[t][1], z);
-      z = mma(a.z, H1[t][2], z);
-      z = mma(a.w, H1[t][3], z);
+      for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
+    }
+    y = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) v[jj] = on * w.w3(j3, 32 * s + 16 * (jj >> 2) + 4 * q + (jj & 3));
+      y = mma16(to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])),
+                to_bf8(H2[2 * s], H2[2 * s + 1]), y);
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) z = mma(w.w1(16 * mt + l15, 4 * s + q), x[s], z);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
+    for (int mt = 0; mt < 4; ++mt) {
+      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 a = w.w2row4(16 * mt + l15, 16 * t + 4 * q);
+        z = mma(a.x, H1[t][0], z);
+        z = mma(a.y, H1[t][1], z);
+        z = mma(a.z, H1[t][2], z);
+        z = mma(a.w, H1[t][3], z);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
+    }
+    y = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y = mma(on * w.w3(j3, 16 * t + 4 * q + r), H2[t][r], y);
   }
-  const int j = l15 < NOUT ? l15 : 0;
-  const float on = l15 < NOUT ? 1.0f : 0.0f;
-  y = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y = mma(on * w.w3(j, 16 * t + 4 * q + r), H2[t][r], y);
 }
 
 // Rollout policy step (agent/ppo.py:105-110, get_action_and_value on obs[t]):
@@ -142,10 +210,10 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
 // eps [N][2] is drawn by the caller with torch's normal_() so the sampling
 // stream is torch's.  Wave = 16 rows of one trunk (even waves actor, odd
 // critic), weights straight from the (L2-resident) parameter buffer.
-template <int D>
+template <int D, int PREC>
 __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P) {
   using L = Lay<D>;
-  constexpr int KS1 = Geo<D>::KS1;
+  constexpr int XN = Geo<D>::template XN<PREC>;
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (kT / 64) + (threadIdx.x >> 6));
   const bool critic = gw & 1;
@@ -153,16 +221,16 @@ __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float*
   if ((int64_t)(gw >> 1) * 16 >= io.n) return;
   const bool live = row < io.n;
   const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
-  float x[KS1];
+  float x[XN];
 #pragma unroll
-  for (int s = 0; s < KS1; ++s) {
-    const int d = 4 * s + q;
+  for (int s = 0; s < XN; ++s) {
+    const int d = Geo<D>::template d_of<PREC>(s, q);
     x[s] = (live && d < D) ? io.obs[row * os + d] : 0.0f;
   }
   f4 H1[4], H2[4], y;
   if (!critic) {
     const WGlobal w{P + L::aW1, P + L::ab1, P + L::aW2, P + L::ab2, P + L::aW3, P + L::ab3, D};
-    mlp_forward<D, kNA>(w, x, H1, H2, y, l15, q);
+    mlp_forward<D, kNA, PREC>(w, x, H1, H2, y, l15, q);
     if (q != 0 || !live) return;
     float logp = 0.0f;
 #pragma unroll
@@ -178,7 +246,7 @@ __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float*
     io.logprobs[row] = logp;
   } else {
     const WGlobal w{P + L::cW1, P + L::cb1, P + L::cW2, P + L::cb2, P + L::cW3, P + L::cb3, D};
-    mlp_forward<D, 1>(w, x, H1, H2, y, l15, q);
+    mlp_forward<D, 1, PREC>(w, x, H1, H2, y, l15, q);
     if (q != 0 || !live) return;
     io.values[row] = y[0] + P[L::cb3];
   }
@@ -206,13 +274,13 @@ struct GradLds {
 // Each wave owns distinct output tiles, so the tile accumulators go straight
 // to the partial row; the per-wave db2 / dW3 / db3 / KL sums are folded in a
 // fixed order ((w0 + w2) + (w1 + w3)).
-template <int D, int NET>
+template <int D, int NET, int PREC>
 __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* __restrict__ W, float* lds,
                                                float* __restrict__ out) {
   using L = Lay<D>;
   using G = Geo<D>;
   using S = GradLds<D>;
-  constexpr int NOUT = NET ? 1 : kNA, KS1 = G::KS1, NT1 = G::NT1;
+  constexpr int NOUT = NET ? 1 : kNA, NT1 = G::NT1, XN = G::template XN<PREC>;
   constexpr int oW1 = NET ? L::cW1 : L::aW1, ob1 = NET ? L::cb1 : L::ab1, oW2 = NET ? L::cW2 : L::aW2,
                 ob2 = NET ? L::cb2 : L::ab2, oW3 = NET ? L::cW3 : L::aW3, ob3 = NET ? L::cb3 : L::ab3;
   const rx_ppo_batch& b = a.b;
@@ -260,7 +328,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   // inputs of a row, loaded one pass ahead (the perm index two passes ahead):
   // the dependent gathers perm -> obs / actions / ... never stall a pass
   struct RowIn {
-    float x[KS1], s0, s1, s2, s3;  // actor: action 0/1, old log-prob, advantage; critic: return, value
+    float x[XN], s0, s1, s2, s3;  // actor: action 0/1, old log-prob, advantage; critic: return, value
   };
   auto src_of = [&](int64_t base) -> int64_t {
     const int64_t r_mb = base + rr;
@@ -272,8 +340,8 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     RowIn in;
     const bool ok = src >= 0;
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      const int d = 4 * s + q;
+    for (int s = 0; s < XN; ++s) {
+      const int d = G::template d_of<PREC>(s, q);
       in.x[s] = (ok && d < D) ? b.obs[src * D + d] : 0.0f;
     }
     if (NET == 0) {
@@ -295,15 +363,15 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     const int64_t src_nn = src_of(base + 2 * kRP);
     const RowIn nxt = load_row(src_n);
     const bool live = src >= 0;
-    float x[KS1];
+    float x[XN];
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      const int d = 4 * s + q;
+    for (int s = 0; s < XN; ++s) {
+      const int d = G::template d_of<PREC>(s, q);
       x[s] = cur.x[s];
-      sX[rr * G::XS + d] = d == D ? 1.0f : x[s];  // the ones column (d = D) carries db1
+      if (d <= D) sX[rr * G::XS + d] = d == D ? 1.0f : x[s];  // the ones column (d = D) carries db1
     }
     f4 H1[4], H2[4], y;
-    mlp_forward<D, NOUT>(w, x, H1, H2, y, l15, q);
+    mlp_forward<D, NOUT, PREC>(w, x, H1, H2, y, l15, q);
     float g[NOUT];  // d loss / d head pre-activation, row rr (every lane of the row)
     if (NET == 0) {
       float mu[kNA], diff[kNA], logp = 0.0f;
@@ -354,29 +422,55 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     }
     __syncthreads();
     // ================================================================ B
-    // dW2[16 wv + i][16 nt + c] += sum_rows dZ2 x H1 (k = row 4s + q)
+    // dW2[16 wv + i][16 nt + c] += sum_rows dZ2 x H1 (k = row 4s + q; bf16: row 32s + 8q + j)
+    if constexpr (PREC == kBF16) {
+#pragma unroll
+      for (int s = 0; s < kRP / 32; ++s) {
+        const bf8 av = rows8(sZ + (16 * wv + l15) * kTS + 32 * s + 8 * q);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma16(av, rows8(sH + (16 * nt + l15) * kTS + 32 * s + 8 * q), acc2[nt]);
+      }
+    } else {
 #pragma unroll 4
-    for (int s = 0; s < kRP / 4; ++s) {
-      const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
-      float bv[4];
+      for (int s = 0; s < kRP / 4; ++s) {
+        const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
+        float bv[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bv[nt] = sH[(16 * nt + l15) * kTS + 4 * s + q];
+        for (int nt = 0; nt < 4; ++nt) bv[nt] = sH[(16 * nt + l15) * kTS + 4 * s + q];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma(av, bv[nt], acc2[nt]);
+        for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma(av, bv[nt], acc2[nt]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) db2 += sZ[lane * kTS + 16 * wv + k];  // lane = hidden unit, own rows
     // dH1 = W2^T dZ2 (k = output unit o = 16t + 4q + r), dZ1 = dH1 * (1 - H1^2) in registers
     f4 dZ1[4];
+    if constexpr (PREC == kBF16) {
+      const bf8 bz[2] = {to_bf8(dZ[0], dZ[1]), to_bf8(dZ[2], dZ[3])};
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int mt = 0; mt < 4; ++mt) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int s = 0; s < 2; ++s) {
+          float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) z = mma(w.w2(16 * t + 4 * q + r, 16 * mt + l15), dZ[t][r], z);
+          for (int jj = 0; jj < 8; ++jj) v[jj] = w.w2(32 * s + 16 * (jj >> 2) + 4 * q + (jj & 3), 16 * mt + l15);
+          z = mma16(to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])), bz[s], z);
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
+        for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z = mma(w.w2(16 * t + 4 * q + r, 16 * mt + l15), dZ[t][r], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
+      }
     }
     __syncthreads();
     // ================================================================ C
@@ -391,17 +485,33 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     __syncthreads();
     // ================================================================ D
     // dW1[16 wv + i][d] (+ db1 at d = D) += sum_rows dZ1 x [X | 1]
-#pragma unroll 4
-    for (int s = 0; s < kRP / 4; ++s) {
-      const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
-      float bv[NT1];
+    if constexpr (PREC == kBF16) {
 #pragma unroll
-      for (int nt = 0; nt < NT1; ++nt) {
-        const int d = 16 * nt + l15;
-        bv[nt] = d <= D ? sX[(4 * s + q) * G::XS + d] : 0.0f;
+      for (int s = 0; s < kRP / 32; ++s) {
+        const bf8 av = rows8(sZ + (16 * wv + l15) * kTS + 32 * s + 8 * q);
+#pragma unroll
+        for (int nt = 0; nt < NT1; ++nt) {
+          const int d = 16 * nt + l15;
+          float v[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) v[jj] = d <= D ? sX[(32 * s + 8 * q + jj) * G::XS + d] : 0.0f;
+          acc1[nt] = mma16(av, to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])),
+                           acc1[nt]);
+        }
       }
+    } else {
+#pragma unroll 4
+      for (int s = 0; s < kRP / 4; ++s) {
+        const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
+        float bv[NT1];
 #pragma unroll
-      for (int nt = 0; nt < NT1; ++nt) acc1[nt] = mma(av, bv[nt], acc1[nt]);
+        for (int nt = 0; nt < NT1; ++nt) {
+          const int d = 16 * nt + l15;
+          bv[nt] = d <= D ? sX[(4 * s + q) * G::XS + d] : 0.0f;
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT1; ++nt) acc1[nt] = mma(av, bv[nt], acc1[nt]);
+      }
     }
     // dW3 / db3 of own rows (lane = hidden unit / output)
 #pragma unroll
@@ -463,16 +573,16 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
 
 // blockIdx.y = trunk (0 actor, 1 critic: their losses share no parameter, so
 // they write disjoint ranges of the same partial row); blockIdx.x = row group.
-template <int D>
+template <int D, int PREC>
 __global__ __launch_bounds__(kT, RX_PPO_MINW) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
                                                     float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
   __shared__ __attribute__((aligned(16))) float lds[GradLds<D>::TOTAL];
   float* out = partial + (size_t)blockIdx.x * Lay<D>::Pp;
   if (blockIdx.y == 0)
-    ppo_grad_trunk<D, 0>(a, W, lds, out);
+    ppo_grad_trunk<D, 0, PREC>(a, W, lds, out);
   else
-    ppo_grad_trunk<D, 1>(a, W, lds, out);
+    ppo_grad_trunk<D, 1, PREC>(a, W, lds, out);
 }
 
 // grad[p] = sum_w partial[w][p] in a fixed order.  One workgroup owns 64
@@ -698,11 +808,18 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
   const int n_wg = (b->mb + rp - 1) / rp;
   ppo_args a{*b, m, rp, stop, klp};
   int P, Pp;
+  const bool bf = b->precision == kBF16;
   if (b->obs_dim == 15) {
-    hipLaunchKernelGGL(k_ppo_grad<15>, dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+    if (bf)
+      hipLaunchKernelGGL((k_ppo_grad<15, kBF16>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+    else
+      hipLaunchKernelGGL((k_ppo_grad<15, kF32>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
-    hipLaunchKernelGGL(k_ppo_grad<19>, dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+    if (bf)
+      hipLaunchKernelGGL((k_ppo_grad<19, kBF16>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+    else
+      hipLaunchKernelGGL((k_ppo_grad<19, kF32>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
   norm_args na{};
@@ -720,9 +837,17 @@ extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
   // one wave per 16 rows and trunk, 4 waves per workgroup
   const int64_t waves = 2 * ((io->n + 15) / 16);
   const int n_wg = (int)((waves + 3) / 4);
-  if (io->obs_dim == 15)
-    hipLaunchKernelGGL(k_policy_act<15>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
-  else
-    hipLaunchKernelGGL(k_policy_act<19>, dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+  const bool bf = io->precision == kBF16;
+  if (io->obs_dim == 15) {
+    if (bf)
+      hipLaunchKernelGGL((k_policy_act<15, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    else
+      hipLaunchKernelGGL((k_policy_act<15, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+  } else {
+    if (bf)
+      hipLaunchKernelGGL((k_policy_act<19, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    else
+      hipLaunchKernelGGL((k_policy_act<19, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+  }
   return (int)hipGetLastError();
 }

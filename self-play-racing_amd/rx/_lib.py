@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -33,6 +33,8 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
+RX_PREC_FP32, RX_PREC_BF16 = 0, 1
+PRECISION = {"fp32": RX_PREC_FP32, "bf16": RX_PREC_BF16}
 
 
 class RxConfig(ctypes.Structure):
@@ -68,7 +70,8 @@ class RxPPOBatch(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("mb", ctypes.c_int32), ("n_rows", ctypes.c_int64)] + \
                [(k, _P) for k in ("obs", "actions", "logprobs", "advantages", "returns", "values", "perm", "params",
                                   "log_std", "adv_stats")] + \
-               [("clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float), ("kl_target", ctypes.c_float)]
+               [("clip_coef", ctypes.c_float), ("vf_coef", ctypes.c_float), ("kl_target", ctypes.c_float),
+                ("precision", ctypes.c_int32)]
 
 
 class RxRolloutIO(ctypes.Structure):
@@ -80,7 +83,7 @@ class RxRolloutIO(ctypes.Structure):
 class RxPolicyIO(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("n", ctypes.c_int64)] + \
                [(k, _P) for k in ("obs", "eps", "params", "log_std", "actions", "logprobs", "values")] + \
-               [("obs_stride", ctypes.c_int64), ("act_stride", ctypes.c_int64)]
+               [("obs_stride", ctypes.c_int64), ("act_stride", ctypes.c_int64), ("precision", ctypes.c_int32)]
 
 
 class RxError(RuntimeError):

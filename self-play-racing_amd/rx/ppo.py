@@ -145,16 +145,18 @@ class PPO:
 
     def _fused_policy(self, obs):
         """rx_policy_act driver when config["fused_policy"] (default on) and the
-        policy is the reference layout in flat fp32 buffers; else None."""
+        policy is the reference layout in flat fp32 buffers; else None.  With
+        config["policy_dtype"] = "bf16" the kernel runs its products on the bf16
+        matrix cores (f32 accumulation)."""
         from . import ppo_fused
         c = self.config
-        if (not c.get("fused_policy", True) or c.get("policy_dtype", "fp32") != "fp32"
-                or getattr(self, "_flat", None) is None or obs.dim() != 3
+        if (not c.get("fused_policy", True) or getattr(self, "_flat", None) is None or obs.dim() != 3
                 or not ppo_fused.policy_supported(self.agent, obs.shape[2])):
             return None
+        prec = ppo_fused.precision(c)
         pa = self.__dict__.get("_policy_act")
-        if pa is None or pa.n != obs.shape[1] or pa.obs_dim != obs.shape[2]:
-            pa = self._policy_act = ppo_fused.PolicyAct(self.agent, self._flat, obs.shape[1], obs.shape[2])
+        if pa is None or pa.n != obs.shape[1] or pa.obs_dim != obs.shape[2] or pa.prec != prec:
+            pa = self._policy_act = ppo_fused.PolicyAct(self.agent, self._flat, obs.shape[1], obs.shape[2], prec)
         return pa
 
     def _rollout_body(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):

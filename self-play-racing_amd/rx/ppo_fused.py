@@ -13,6 +13,15 @@ import torch
 from . import _lib
 
 
+def precision(config):
+    """Matrix-core precision of the fused policy kernels: config["policy_dtype"]
+    "fp32" (exact f32 MFMA, default) or "bf16" (bf16 operands, f32 accumulation)."""
+    dt = config.get("policy_dtype", "fp32")
+    if dt not in _lib.PRECISION:
+        raise ValueError(f"policy_dtype={dt!r}: 'fp32' or 'bf16'")
+    return _lib.PRECISION[dt]
+
+
 def supported(agent, b, mb):
     """True when the fused kernel covers this policy / batch: the reference
     Agent layout (64-wide tanh trunks, 2 actions, D in {15, 19}), float32,
@@ -45,7 +54,8 @@ class FusedMinibatchGrad:
         self.batch = _lib.RxPPOBatch(D, mb, B, _lib.ptr(obs), _lib.ptr(actions), _lib.ptr(logprobs),
                                      _lib.ptr(advantages), _lib.ptr(returns), _lib.ptr(values), _lib.ptr(perm),
                                      _lib.ptr(flat.flat_param), _lib.ptr(agent.log_std), _lib.ptr(self.stats),
-                                     float(config["clip_coef"]), float(config["vf_coef"]), float(config["kl_target"]))
+                                     float(config["clip_coef"]), float(config["vf_coef"]), float(config["kl_target"]),
+                                     precision(config))
 
     def adv_stats(self, stream=None):
         _lib.check(self.L.rx_ppo_adv_stats(self.batch, self.n_mb, _lib.ptr(self.stats), _lib.stream_ptr(stream)),
@@ -109,9 +119,10 @@ class PolicyAct:
     (torch.normal(mu, std) = normal_() * std + mu), so the sampling stream is
     unchanged; mu / value differ from the torch forward by float rounding."""
 
-    def __init__(self, agent, flat, n, obs_dim):
+    def __init__(self, agent, flat, n, obs_dim, prec=_lib.RX_PREC_FP32):
         self.L = _lib.load()
         self.agent, self.flat, self.n, self.obs_dim = agent, flat, int(n), int(obs_dim)
+        self.prec = int(prec)
         dev = flat.flat_param.device
         self.eps = torch.empty((self.n, 2), dtype=torch.float32, device=dev)
         self._lp = torch.empty(self.n, dtype=torch.float32, device=dev)  # sinks when the caller
@@ -143,7 +154,8 @@ class PolicyAct:
             self._io_cache["shapes"] = (obs.shape, obs.stride(), actions_out.stride())
             io = self._io_cache[key] = _lib.RxPolicyIO(
                 self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(self.eps), _lib.ptr(self.flat.flat_param),
-                _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out), _lib.ptr(lp), _lib.ptr(val), os_, as_)
+                _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out), _lib.ptr(lp), _lib.ptr(val), os_, as_,
+                self.prec)
         self.eps.normal_()
         _lib.check(self.L.rx_policy_act(io, _lib.stream_ptr(stream)), "rx_policy_act")
         return actions_out

@@ -44,15 +44,16 @@ class SelfPlayVectorEnv:
         self._act = torch.zeros((self.num_envs, 2, 2), dtype=torch.float32, device=self.device)
         self.buf = {"obs": self.venv.buf["obs"][:, agent_idx]}
 
-    def set_opponent(self, policy, flat=None):
+    def set_opponent(self, policy, flat=None, prec=0):
         """policy: an Agent (or None = random actions).  With ``flat`` (an
         rx.optim.FlatParams of that policy) the opponent's forward + sampling is
-        one rx_policy_act launch reading the two-car obs buffer in place."""
+        one rx_policy_act launch reading the two-car obs buffer in place
+        (``prec``: RX_PREC_FP32 / RX_PREC_BF16 matrix-core precision)."""
         from . import ppo_fused
         self.opponent_policy = policy
         self._opp_fused = None
         if policy is not None and flat is not None and ppo_fused.policy_supported(policy, self.venv.D):
-            self._opp_fused = ppo_fused.PolicyAct(policy, flat, self.num_envs, self.venv.D)
+            self._opp_fused = ppo_fused.PolicyAct(policy, flat, self.num_envs, self.venv.D, prec)
 
     def _opponent_actions(self):
         o = self._act[:, self.opp_idx]
@@ -154,8 +155,9 @@ class SelfPlayPPO(PPO):
             with torch.no_grad():
                 for dst, src in zip(self._opp_static.state_dict().values(), self.curr_opponent.state_dict().values()):
                     dst.copy_(src)
-            fused = self.config.get("fused_policy", True) and self.config.get("policy_dtype", "fp32") == "fp32"
-            self.envs.set_opponent(self._opp_static, self._opp_flat if fused else None)
+            from . import ppo_fused
+            fused = self.config.get("fused_policy", True)
+            self.envs.set_opponent(self._opp_static, self._opp_flat if fused else None, ppo_fused.precision(self.config))
         self.envs.reset_device()
 
     def collect_rollout(self, *bufs):
