@@ -18,7 +18,7 @@
  *  - Agents: A = 1 (environment/racing_env.py RacingEnv) or A = 2
  *    (environment/multi_racing_env.py MultiRacingEnv with 2 cars).
  *    Observation width D = n_sensors + 4 + 4*(A-1)   (racing_env.py:37-42,
- *    multi_racing_env.py:204).
+ *    multi_racing_env.py:38).
  *  - All env arithmetic is binary64 in the reference's operation order; see
  *    DESIGN.md §Parity for the two libm calls (sin/cos, pow(x,2)) whose
  *    results may differ from glibc's by 1 ulp.
@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 14
+#define RX_ABI_VERSION 15
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -48,7 +48,7 @@ extern "C" {
 #define RX_F_CP25 4u         /* checkpoints[0.25]                racing_env.py:21-25 */
 #define RX_F_CP50 8u         /* checkpoints[0.50] */
 #define RX_F_CP75 16u        /* checkpoints[0.75] */
-#define RX_F_HAS_CRASHED 32u /* agents_data['has_crashed']       multi_racing_env.py:313,358-360 */
+#define RX_F_HAS_CRASHED 32u /* agents_data['has_crashed']       multi_racing_env.py:147,192-194 */
 /* env flag bits (rx_state.env_flags, per env) */
 #define RX_EF_PENDING_RESET 1u /* episode ended last step: next-step autoreset */
 
@@ -62,7 +62,7 @@ extern "C" {
 #define RX_INFO_SPEED 0          /* info['speed']          racing_env.py:80 */
 #define RX_INFO_PROGRESS 1       /* info['progress'] (1.0 once finished) :81,158-159 */
 #define RX_INFO_PROGRESS_DELTA 2 /* info['progress_delta'] :157 (single-agent) */
-#define RX_INFO_PLACEMENT 3      /* info['placement'] (0 = none) multi_racing_env.py:425 */
+#define RX_INFO_PLACEMENT 3      /* info['placement'] (0 = none) multi_racing_env.py:210-211,252-259 */
 
 typedef struct rx_env rx_env;
 
@@ -77,14 +77,16 @@ typedef struct {
   double sensor_half_cone; /* pi/3 (racing_env.py:45) or pi/2 (multi_racing_env.py:50) */
   double speed_weight;     /* RacingEnv.speed_weight, 8.0 (racing_env.py:9,26) */
   int32_t cull_chunk;      /* raycast culling: segments per chunk (16 recommended; 0 = test every segment) */
-  int32_t sort_interval;   /* re-sort envs by track position every k dynamics launches (0 = never) */
+  int32_t sort_interval;   /* re-sort envs by track position every k dynamics launches (0 = never): a
+                              counting sort by (slot, waypoint bin), rx_sort.hip; scheduling only.  Skipped
+                              when the pool has more than 65,536 slots (at most ~1 env per slot). */
   int32_t ray_order;       /* raycast lane order: 0 = (env, agent, ray), 11 rays of ~6 envs per wave;
                               1 = ray-major: one (agent, ray) of 64 consecutive envs per wave -- with
                               sort_interval > 0 those envs are track neighbours, so a wave's rays are
                               nearly parallel and share culling chunks; 2 = sorted ray tasks: every
-                              sort_interval steps all (env, agent, ray) tasks are radix-sorted by
-                              (slot, waypoint bucket, absolute-direction sector), so a wave holds rays
-                              with nearby origins and nearly equal directions from any envs.
+                              step the dynamics kernel orders the A*R tasks of each 64-env wave by the
+                              absolute direction of the ray (64 sectors, LDS counting sort), so a ray
+                              wave holds rays with nearby origins and nearly equal directions.
                               Scheduling only: same results. */
   int32_t cull_super;      /* two-level raycast culling: chunks per super-chunk box (0 = one level) */
 } rx_config;
@@ -92,7 +94,7 @@ typedef struct {
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
  * agent-minor: element e*A + a.  Mirrors Car (car.py:15-24), RacingEnv
  * (racing_env.py:17-26), MultiRacingEnv.agents_data (multi_racing_env.py:
- * 186-191) and RecordEpisodeStatistics' episode counters. */
+ * 142-148) and RecordEpisodeStatistics' episode counters. */
 typedef struct {
   double* x;             /* [N*A] */
   double* y;             /* [N*A] */
@@ -141,6 +143,14 @@ int rx_destroy(rx_env* h);
 /* Host copy of the sensor angle offsets the kernels use: [n_sensors] =
  * np.linspace(-half_cone, half_cone, n_sensors) (racing_env.py:45). */
 int rx_sensor_angles(const rx_env* h, double* out);
+
+/* Diagnostics (ABI v15): the env id at each position of the current wave
+ * order (envs grouped by slot, re-sorted by track position every
+ * sort_interval dynamics launches), host array [n_envs]; synchronises the
+ * device.  *sort_bins / *sort_shift (either may be NULL) receive the spatial
+ * sort's bin count and waypoints-per-bin shift (0 bins = no re-sort).  The
+ * reference has no counterpart (its SyncVectorEnv steps envs in order). */
+int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort_shift);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env
  * Track.__init__ geometry (environment/track.py:61-148): slot k has

@@ -97,11 +97,12 @@ struct rx_env {
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
-  DevBuf<uint32_t> keys_in, keys_out;
-  DevBuf<int32_t> vals_in;
-  DevBuf<char> sort_tmp;
-  size_t sort_tmp_bytes = 0;
-  int sort_bits = 16;
+  DevBuf<uint32_t> keys_in;              // [N] bin per perm position (REWARD half)
+  DevBuf<int32_t> vals_in;               // [N] env id per perm position
+  DevBuf<uint32_t> sort_hist, sort_cursor;  // [sort_bins]
+  DevBuf<int32_t> sort_base;             // [n_tracks] first bin of each slot
+  int32_t sort_bins = 0, sort_shift = 0;
+  bool sort_on = false;
   uint64_t dyn_calls = 0;
   // ray_order 2: direction-sorted (agent, ray) task ids, rewritten by k_dyn every step
   DevBuf<int32_t> tasks;
@@ -322,6 +323,17 @@ int rx_sensor_angles(const rx_env* h, double* out) {
   return RX_OK;
 }
 
+int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort_shift) {
+  if (!h || !perm_out) return fail(RX_EINVAL, "rx_env_order: null argument");
+  if (!h->assigned) return fail(RX_ESTATE, "rx_env_order before rx_assign");
+  RX_HIP(hipSetDevice(h->cfg.device));
+  RX_HIP(hipDeviceSynchronize());
+  RX_HIP(hipMemcpy(perm_out, h->perm[h->cur].p, (size_t)h->cfg.n_envs * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (sort_bins) *sort_bins = h->sort_on ? h->sort_bins : 0;
+  if (sort_shift) *sort_shift = h->sort_shift;
+  return RX_OK;
+}
+
 int rx_destroy(rx_env* h) {
   if (!h) return RX_OK;
   (void)hipSetDevice(h->cfg.device);
@@ -339,8 +351,9 @@ int rx_destroy(rx_env* h) {
   h->dyn_waves.release();
   h->ray_waves.release();
   h->keys_in.release();
-  h->keys_out.release();
-  h->sort_tmp.release();
+  h->sort_hist.release();
+  h->sort_cursor.release();
+  h->sort_base.release();
   delete h;
   return RX_OK;
 }
@@ -394,6 +407,11 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if (const char* ev = getenv("RX_WIDE_N")) wide_n = atoi(ev);  // A/B knob
   if (A == 1 && N <= wide_n) h->dyn_lpe = 64;
   if (const char* ev = getenv("RX_ARGMIN_WINDOW")) h->argmin_window = std::max(0, std::min(32, atoi(ev)));  // A/B knob
+  {  // the window [prev - H, prev + H] is wrapped into [0, W) by one +-W: needs H <= W of every slot
+    int min_w = 1 << 30;
+    for (int k = 0; k < h->n_tracks; ++k) min_w = std::min(min_w, h->wp_off_h[k + 1] - h->wp_off_h[k]);
+    h->argmin_window = std::min(h->argmin_window, min_w);
+  }
   if (const char* ev = getenv("RX_DYN1_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
     const int v = atoi(ev);
     if (A == 1 && (v == 1 || v == 2 || v == 4 || v == 64)) h->dyn_lpe = v;
@@ -454,21 +472,35 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     std::vector<uint32_t> z(N, 0u);
     if ((rc = upload(h->resets, z.data(), z.size()))) return rc;
   }
-  if (h->cfg.sort_interval > 0) {  // spatial sort buffers (keys: slot << 16 | waypoint)
-    if ((rc = upload(h->vals_in, perm.data(), perm.size()))) return rc;
-    std::vector<uint32_t> zk(N, 0u);
-    if ((rc = upload(h->keys_in, zk.data(), zk.size()))) return rc;
-    if ((rc = upload(h->keys_out, zk.data(), zk.size()))) return rc;
-    int bits = 16;
-    while ((1 << (bits - 16)) < h->n_tracks) ++bits;
-    h->sort_bits = bits;
-    size_t tmp = 0;
-    RX_HIP((hipError_t)rx_sort_pairs(nullptr, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[1].p, N,
-                                     bits, nullptr));
-    h->sort_tmp.release();
-    if (hipMalloc(&h->sort_tmp.p, std::max<size_t>(tmp, 16)) != hipSuccess) return fail(RX_ENOMEM, "sort temp alloc");
-    h->sort_tmp.n = std::max<size_t>(tmp, 16);
-    h->sort_tmp_bytes = tmp;
+  h->sort_on = false;
+  if (h->cfg.sort_interval > 0) {
+    // spatial sort bins: slot k owns (W_k >> shift) + 1 consecutive bins from
+    // sort_base[k]; the smallest shift that keeps all bins <= RX_SORT_MAX_BINS.
+    // More slots than that (at most ~1 env per slot): nothing to regroup, no sort.
+    int shift = 0;
+    long long total = 0;
+    for (;; ++shift) {
+      total = 0;
+      for (int k = 0; k < h->n_tracks; ++k) total += ((h->wp_off_h[k + 1] - h->wp_off_h[k]) >> shift) + 1;
+      if (total <= RX_SORT_MAX_BINS || shift >= 30) break;
+    }
+    if (total <= RX_SORT_MAX_BINS) {
+      std::vector<int32_t> base(h->n_tracks);
+      int32_t run = 0;
+      for (int k = 0; k < h->n_tracks; ++k) {
+        base[k] = run;
+        run += ((h->wp_off_h[k + 1] - h->wp_off_h[k]) >> shift) + 1;
+      }
+      std::vector<uint32_t> zk(std::max<size_t>((size_t)N, (size_t)total), 0u);
+      if ((rc = upload(h->sort_base, base.data(), base.size()))) return rc;
+      if ((rc = upload(h->vals_in, perm.data(), perm.size()))) return rc;
+      if ((rc = upload(h->keys_in, zk.data(), (size_t)N))) return rc;
+      if ((rc = upload(h->sort_hist, zk.data(), (size_t)total))) return rc;
+      if ((rc = upload(h->sort_cursor, zk.data(), (size_t)total))) return rc;
+      h->sort_bins = (int32_t)total;
+      h->sort_shift = shift;
+      h->sort_on = true;
+    }
   }
   if (h->cfg.ray_order == 2) {  // task ids before the first k_dyn: (agent, ray) minor within each env
     const size_t nt = (size_t)N * A * R;
@@ -559,16 +591,16 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.tasks = h->tasks.p;
   a.tasks_out = (h->cfg.ray_order == 2 && !a.wide) ? h->tasks.p : nullptr;
   a.cs_scratch = h->cs_scratch.p;
+  a.sort_base = h->sort_base.p;
+  a.sort_shift = h->sort_shift;
   static const int quad = [] {  // A/B knob
     const char* e = getenv("RX_BOX_QUAD");
     return e ? atoi(e) : 1;
   }();
   a.box_quadrants = quad;
-  static const int no_ep = [] {  // measurement knob: drop the episode-statistics atomics
-    const char* e = getenv("RX_NO_EPSTATS");
-    return e ? atoi(e) : 0;
-  }();
-  if (no_ep) a.io.ep_stats = nullptr;
+#ifdef RX_AB_NO_EPSTATS  // A/B build only (tools/build_rev.py): drop the episode-statistics atomics
+  a.io.ep_stats = nullptr;
+#endif
 }
 
 static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
@@ -595,7 +627,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
                      h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
   if (split) {
     const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
-    const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
+    const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
     if (dyn) {
       prof_arm(h, a, RX_KERNEL_KIN);
       if ((rc = rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
@@ -617,10 +649,9 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     }
     a.prof_ts = nullptr;
     if (sort) {  // keys written by k_step2: the new env order applies from the next step
-      size_t tmp = h->sort_tmp_bytes;
       const int nxt = 1 - h->cur;
-      if ((rc = rx_sort_pairs(h->sort_tmp.p, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[nxt].p,
-                              h->cfg.n_envs, h->sort_bits, s)) != 0)
+      if ((rc = rx_sort_envs(h->keys_in.p, h->vals_in.p, h->cfg.n_envs, h->sort_hist.p, h->sort_cursor.p,
+                             h->sort_bins, h->perm[nxt].p, s)) != 0)
         return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
       h->cur = nxt;
     }
@@ -628,7 +659,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   }
   if (phases & RX_PHASE_DYNAMICS) {
     // re-sort the env order every sort_interval dynamics launches (scheduling only)
-    const bool sort = h->cfg.sort_interval > 0 && h->sort_tmp.p && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
+    const bool sort = h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
     if (sort) {
       a.sort_keys = h->keys_in.p;
       a.sort_vals = h->vals_in.p;
@@ -638,10 +669,9 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
       return fail(RX_EHIP, "k_dyn launch failed: %s", hipGetErrorString((hipError_t)rc));
     a.prof_ts = nullptr;
     if (sort) {
-      size_t tmp = h->sort_tmp_bytes;
       const int nxt = 1 - h->cur;
-      if ((rc = rx_sort_pairs(h->sort_tmp.p, &tmp, h->keys_in.p, h->keys_out.p, h->vals_in.p, h->perm[nxt].p,
-                              h->cfg.n_envs, h->sort_bits, s)) != 0)
+      if ((rc = rx_sort_envs(h->keys_in.p, h->vals_in.p, h->cfg.n_envs, h->sort_hist.p, h->sort_cursor.p,
+                             h->sort_bins, h->perm[nxt].p, s)) != 0)
         return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
       h->cur = nxt;
       a.perm = h->perm[nxt].p;

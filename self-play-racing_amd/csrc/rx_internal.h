@@ -71,8 +71,10 @@ struct rx_kargs {
   const int32_t* perm;        // env order the kernels read (sorted by slot, then position)
   const double* rel_angles;   // [n_sensors]
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
-  uint32_t* sort_keys;        // [N] k_dyn writes (slot << 16 | waypoint) at its perm position, or nullptr
+  uint32_t* sort_keys;        // [N] k_dyn writes the sort bin (sort_base[slot] + (waypoint >> sort_shift)) at its perm position, or nullptr
   int32_t* sort_vals;         // [N] k_dyn writes the env id at its perm position
+  const int32_t* sort_base;   // [n_tracks] first sort bin of each slot (ascending with the slot id)
+  int32_t sort_shift;         // waypoints per sort bin = 1 << sort_shift
   // ray_order 2: k_dyn writes the direction-sorted (agent, ray) task ids of
   // each dynamics wave's envs to tasks_out[perm_start*A*R ..]; k_rays reads
   // tasks[task_start + lane] (the same buffer)
@@ -129,5 +131,8 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
 extern "C" int rx_ppo_reduce_blocks(int obs_dim);
 extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                                     const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s);
-extern "C" int rx_sort_pairs(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
-                             int32_t* vout, int n, int end_bit, hipStream_t s);
+// spatial re-sort (rx_sort.hip): counting sort of the perm positions by the
+// bin keys the REWARD half wrote; hist must be zero on entry and is left zero
+#define RX_SORT_MAX_BINS 65536
+extern "C" int rx_sort_envs(const uint32_t* keys, const int32_t* vals, int n, uint32_t* hist, uint32_t* cursor,
+                            int nbins, int32_t* perm_out, hipStream_t s);

@@ -379,16 +379,16 @@ __device__ __forceinline__ bool corner_out(const double2* __restrict__ wp, const
 
 __device__ __forceinline__ double speed_of(double vx, double vy) { return __builtin_sqrt(rx_sq(vx) + rx_sq(vy)); }
 
-// Spatial-coherence key for the next wave assignment: (slot, waypoint of the
-// car).  Sorting by it (rx_sort_pairs) keeps slot groups in place and puts
-// cars that are near each other on the track into the same wavefronts, which
-// is what makes k_rays' per-wave chunk culling effective.  Pure scheduling:
-// results never depend on the order.
+// Spatial-coherence key for the next wave assignment: the sort bin of (slot,
+// waypoint of the car).  Sorting by it (rx_sort_envs) keeps slot groups in
+// place and puts cars that are near each other on the track into the same
+// wavefronts, which is what makes k_rays' per-wave chunk culling effective.
+// Pure scheduling: results never depend on the order.
 __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k, int e, double progress, int W) {
   if (!a.sort_keys) return;
   int w = (int)(progress * (double)W + 0.5);
-  w = w < 0 ? 0 : (w > 0xffff ? 0xffff : w);
-  a.sort_keys[pos] = ((uint32_t)k << 16) | (uint32_t)w;
+  w = w < 0 ? 0 : (w > W ? W : w);
+  a.sort_keys[pos] = (uint32_t)(a.sort_base[k] + (w >> a.sort_shift));
   a.sort_vals[pos] = e;
 }
 

@@ -1,13 +1,108 @@
-// rx_sort.hip -- radix sort of (spatial key, env id) pairs that re-groups the
-// envs into spatially coherent wavefronts between k_dyn and k_rays
-// (scheduling only; no result depends on the order).  rocPRIM via hipCUB.
+// rx_sort.hip -- the spatial re-sort of the env order (every sort_interval
+// dynamics launches): envs regrouped into track-coherent wavefronts.
+// Scheduling only: no result depends on the order (test_culling_and_sort_are_exact).
+//
+// The key the REWARD half writes per perm position is a BIN: the slot's bin
+// base (bases ascend with the slot id) + (closest waypoint >> shift), so bins
+// of one slot are contiguous, slot groups keep their place in the perm, and
+// the whole key space is <= RX_SORT_MAX_BINS (rx_assign picks the shift).  A
+// counting sort over that small key space, three launches:
+//   k_sort_hist     per wave: lanes grouped by bin (ballot), one atomic per group
+//   k_sort_scan     one workgroup: exclusive scan of the histogram -> cursors,
+//                   histogram cleared for the next sort
+//   k_sort_scatter  per wave: the same grouping, one cursor atomic per group,
+//                   lane rank within its group -> perm_out[base + rank] = env
+// The envs of a wave are track neighbours (the previous sort), so a wave sees
+// only a handful of bins: a few atomics per wave.  Order inside a bin follows
+// the atomic order of the waves (not fixed run to run; nothing depends on it).
 #include <hip/hip_runtime.h>
-
-#include <hipcub/hipcub.hpp>
 
 #include "rx_internal.h"
 
-extern "C" int rx_sort_pairs(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
-                             int32_t* vout, int n, int end_bit, hipStream_t s) {
-  return (int)hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, n, 0, end_bit, s);
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// popcount of the bits of m below this lane
+__device__ __forceinline__ int rank_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_hist(const uint32_t* __restrict__ keys, int n,
+                                                       uint32_t* __restrict__ hist) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const bool v = i < n;
+  const uint32_t b = v ? keys[i] : 0u;
+  unsigned long long pending = __ballot(v);
+  while (pending) {  // wave-uniform loop: one iteration per distinct bin of the wave
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+    const unsigned long long m = __ballot(v && b == lb);
+    if (lane_id() == leader) atomicAdd(&hist[lb], (uint32_t)__builtin_popcountll(m));
+    pending &= ~m;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_sort_scan(uint32_t* __restrict__ hist,
+                                                             uint32_t* __restrict__ cursor, int nbins) {
+  __shared__ uint32_t part[kScanThreads];
+  const int t = threadIdx.x;
+  const int per = (nbins + kScanThreads - 1) / kScanThreads;
+  const int b0 = t * per, b1 = min(nbins, b0 + per);
+  uint32_t s = 0;
+  for (int b = b0; b < b1; ++b) s += hist[b];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < kScanThreads; off <<= 1) {  // Hillis-Steele inclusive scan of the thread sums
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;  // exclusive
+  for (int b = b0; b < b1; ++b) {
+    const uint32_t c = hist[b];
+    cursor[b] = run;
+    run += c;
+    hist[b] = 0u;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
+                                                          const int32_t* __restrict__ vals, int n,
+                                                          uint32_t* __restrict__ cursor,
+                                                          int32_t* __restrict__ perm_out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const bool v = i < n;
+  const uint32_t b = v ? keys[i] : 0u;
+  const int32_t e = v ? vals[i] : 0;
+  unsigned long long pending = __ballot(v);
+  uint32_t dst = 0;
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+    const unsigned long long m = __ballot(v && b == lb);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(&cursor[lb], (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (v && b == lb) dst = base + (uint32_t)rank_below(m);
+    pending &= ~m;
+  }
+  if (v) perm_out[dst] = e;
+}
+
+}  // namespace
+
+extern "C" int rx_sort_envs(const uint32_t* keys, const int32_t* vals, int n, uint32_t* hist, uint32_t* cursor,
+                            int nbins, int32_t* perm_out, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (nbins <= 0 || nbins > RX_SORT_MAX_BINS) return (int)hipErrorInvalidValue;
+  const int grid = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist);
+  hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanThreads), 0, s, hist, cursor, nbins);
+  hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(kBlock), 0, s, keys, vals, n, cursor, perm_out);
+  return (int)hipGetLastError();
 }

@@ -17,6 +17,7 @@ step after a terminal one ignores the action, resets the env and reports
 reward 0, terminated = truncated = False (unpinned, gymnasium
 is not installed here).
 """
+import ctypes
 import time
 
 import numpy as np
@@ -262,6 +263,15 @@ class RacingVectorEnv:
         if reset:
             self.buf["ep_stats"].zero_()
         return float(s[0]), float(s[1]), int(s[2])
+
+    def env_order(self):
+        """(perm, sort_bins, sort_shift): the env id at each position of the current
+        wave order (diagnostics; synchronises the device)."""
+        perm = np.empty(self.num_envs, np.int32)
+        bins, shift = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(self.L.rx_env_order(self._h, perm.ctypes.data, ctypes.byref(bins), ctypes.byref(shift)),
+                   "rx_env_order")
+        return perm, bins.value, shift.value
 
     def get_state(self):
         return {k: v.cpu().numpy() for k, v in self.state.items() if v is not None}

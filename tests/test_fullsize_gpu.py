@@ -205,3 +205,34 @@ def test_8192_two_car_subset_bit_exact_vs_oracle(oracle_dev):
                 assert np.array_equal(g[k].reshape(N, 2)[idx], st[k]), (t, k)
     assert ended > 200
     v.close()
+
+
+@pytest.mark.parametrize("n_agents,N", [(1, 65536), (2, 8192)])
+def test_spatial_sort_orders_envs_by_track_bin(n_agents, N):
+    """The hand-written counting sort (rx_sort.hip) at the bench's sizes: right
+    after a re-sort step the wave order is a permutation of the envs, every slot
+    group keeps exactly its slot's envs, and inside a group the envs ascend by
+    sort bin = (closest waypoint of car 0 = trunc(progress * W + 0.5)) >> shift."""
+    from rx.vector_env import RacingVectorEnv
+    pool, widths = _seed1_pool(N)
+    v = RacingVectorEnv(pool, widths, n_agents=n_agents, device="cuda", autoreset="next_step", sort_interval=16)
+    v.reset_device()
+    rng = np.random.default_rng(21)
+    for t in range(33):  # dynamics launches 0, 16, 32 re-sort: the order now follows step 33's keys
+        v.step_device(torch.from_numpy(_actions(rng, N, n_agents)).cuda())
+    perm, bins, shift = v.env_order()
+    assert bins > 0 and shift == 0
+    assert np.array_equal(np.sort(perm), np.arange(N))
+    slots = v.track_of_env
+    off = v.tracks.arrays()["wp_off"]
+    W = (off[1:] - off[:-1]).astype(np.int64)
+    prog = v.get_state()["progress"].reshape(N, n_agents)[:, 0]
+    w = np.clip(np.trunc(prog * W[slots] + 0.5).astype(np.int64), 0, W[slots]) >> shift
+    base = np.concatenate([[0], np.cumsum((W >> shift) + 1)[:-1]])
+    key = base[slots] + w
+    k_perm = slots[perm]
+    assert np.all(np.diff(k_perm) >= 0), "slot groups moved"
+    assert np.array_equal(np.bincount(k_perm, minlength=len(W)), np.bincount(slots, minlength=len(W)))
+    assert np.all(np.diff(key[perm]) >= 0), "envs not ascending by sort bin"
+    assert len(np.unique(key)) > 100  # the cars have spread over the tracks
+    v.close()
