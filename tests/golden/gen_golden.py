@@ -25,6 +25,10 @@ Sets:
   schedules.npz   A21 PPO.train / SelfPlayPPO.train per-update schedules
                       (lr, log_std, speed weight, snapshot pool, opponent
                       draws, checkpoint cadence).
+  eval_metrics.npz (f)#3 utils/metrics.py:39-78 eval_single_agent on the
+                      evaluate.py pool (seed 42, widths by run), driven by a
+                      scripted agent; the actions it issued are recorded so
+                      the device evaluator can replay them open loop.
 
 Metadata (numpy/scipy/torch versions, libm behaviour notes, CPU model) is stored
 in every file under ``meta_*`` keys.
@@ -761,9 +765,56 @@ def gen_schedules():
     _save("schedules.npz", **out)
 
 
+def gen_eval_metrics(track, racing_env):
+    """(f)#3: the reference's per-episode evaluation metrics.  Episodes follow
+    rx.evaluate.eval_pool(4, 2): np.random.seed(0), gen_tracks(4, seed=42),
+    run r uses width RandomState(42 + r).randint(4, 10) (evaluate.py:26-31
+    indexes widths by run).  The agent is a scripted pure-pursuit driver
+    (varied gains / caps / noise so episodes finish, crash and time out)."""
+    import torch
+    sys.path.insert(0, REF)
+    from utils.metrics import eval_single_agent
+    np.random.seed(0)
+    pool = track.gen_tracks(num_tracks=4, seed=42)
+    widths = [np.random.RandomState(42 + i).randint(4, 10) for i in range(4)]
+    plans = {(0, 0): (3.0, 18.0, 0.05), (0, 1): (3.0, 22.0, 0.05), (1, 0): (2.5, 14.0, 0.02),
+             (1, 1): (12.0, 40.0, 0.6), (2, 0): (3.0, 16.0, 0.02), (2, 1): (3.0, 2.5, 0.0),
+             (3, 0): (3.0, 12.0, 0.01), (3, 1): (0.0, 2.0, 0.0)}
+    rng = np.random.default_rng(909)
+    keys = ("total_reward", "steps", "progress", "finished", "crashed", "speed", "total_distance", "distance_per_step")
+    out = {k: [] for k in keys}
+    acts, off = [], [0]
+
+    class Scripted:
+        def __init__(self, env, plan):
+            self.env, self.plan, self.log = env, plan, []
+
+        def get_action_and_value(self, obs_tensor):
+            a = _controller(self.env, rng, *self.plan)
+            self.log.append(a)
+            return torch.from_numpy(a[None]), None, None, None
+
+    for t in range(4):
+        for r in range(2):
+            env = racing_env.RacingEnv(num_sensors=11, track_pool=pool, track_id=t, track_width=widths[r])
+            agent = Scripted(env, plans[(t, r)])
+            m = eval_single_agent(env, agent, "cpu", max_steps=2000)
+            for k in keys:
+                out[k].append(m[k])
+            acts.extend(agent.log)
+            off.append(len(acts))
+            print(f"eval track {t} run {r}: steps {m['steps']} finished {m['finished']} crashed {m['crashed']}")
+    res = {k: np.array(v, dtype=np.float64 if k not in ("steps", "finished", "crashed") else
+                       (np.int64 if k == "steps" else np.uint8)) for k, v in out.items()}
+    res["actions"] = np.array(acts, dtype=np.float32)
+    res["off"] = np.array(off, dtype=np.int64)
+    res["widths"] = np.array(widths, dtype=np.int64)
+    _save("eval_metrics.npz", **res)
+
+
 def main(argv):
     want = set(argv[1:]) or {"geometry", "raycast", "step_single", "traj_single", "step_multi", "gae", "agent",
-                             "ppo_update", "schedules"}
+                             "ppo_update", "schedules", "eval_metrics"}
     if want <= {"ppo_update", "schedules"}:
         sys.path.insert(0, os.path.join(HERE, "_gym_stub"))
         if "ppo_update" in want:
@@ -791,6 +842,8 @@ def main(argv):
         gen_ppo_update()
     if "schedules" in want:
         gen_schedules()
+    if "eval_metrics" in want:
+        gen_eval_metrics(track, racing_env)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,12 @@ from rx.vector_env import RacingVectorEnv  # noqa: E402
 N, A = int(sys.argv[1]), int(sys.argv[2])
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 400
 pool, widths = seed1_pool(N)
-env = RacingVectorEnv(pool, widths, n_agents=A, device="cuda")
+if os.environ.get("PROBE_CONTIG") == "1":  # envs of one slot contiguous: the wave order is the env order
+    key = [hash((pool[i].tobytes(), int(widths[i]))) for i in range(N)]
+    order = sorted(range(N), key=lambda i: key[i])
+    pool, widths = [pool[i] for i in order], [widths[i] for i in order]
+env = RacingVectorEnv(pool, widths, n_agents=A, device="cuda",
+                      sort_interval=int(os.environ.get("PROBE_SORT", "16")))
 env.reset_device()
 lo = torch.tensor([-1.0, 0.0] if A == 1 else [-1.0, -1.0], device="cuda")
 bank = torch.rand((64, N, A, 2) if A == 2 else (64, N, 2), device="cuda") * 2 - 1
@@ -36,5 +41,5 @@ for k in range(steps):
         env.profile(0)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(json.dumps({"N": N, "agents": A, "env_steps_per_s": round(N * steps / dt), "us_per_step": round(dt / steps * 1e6, 1),
+print(json.dumps({"contig": os.environ.get("PROBE_CONTIG", "0"), "sort": os.environ.get("PROBE_SORT", "16"), "N": N, "agents": A, "env_steps_per_s": round(N * steps / dt), "us_per_step": round(dt / steps * 1e6, 1),
                   "kernels_us": {k: round(v[0] * 1e3, 1) for k, v in env.profile_read().items()}}))
