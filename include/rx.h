@@ -94,7 +94,11 @@ typedef struct {
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
  * agent-minor: element e*A + a.  Mirrors Car (car.py:15-24), RacingEnv
  * (racing_env.py:17-26), MultiRacingEnv.agents_data (multi_racing_env.py:
- * 142-148) and RecordEpisodeStatistics' episode counters. */
+ * 142-148) and RecordEpisodeStatistics' episode counters.
+ * The engine steps a working copy of these arrays kept in wave order (ABI
+ * v15: coalesced state traffic; see rx_state_import / rx_state_export): the
+ * bound arrays are read at rx_bind_state / rx_assign and otherwise only
+ * synchronised on request.  track and speed_weight are read in place. */
 typedef struct {
   double* x;             /* [N*A] */
   double* y;             /* [N*A] */
@@ -170,8 +174,22 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
  * track (segment loads become scalar/broadcast). */
 int rx_assign(rx_env* h, const int32_t* track_of_env);
 
-/* Bind the caller-owned device state (pointers are kept until re-bound). */
+/* Bind the caller-owned device state (pointers are kept until re-bound).
+ * Once both rx_bind_state and rx_assign have run, the engine copies the bound
+ * arrays into its working copy (blocking). */
 int rx_bind_state(rx_env* h, const rx_state* st);
+
+/* ABI v15.  The engine keeps the env state in wave order (position p holds
+ * env rx_env_order()[p]) so its kernels read and write it coalesced, and
+ * moves it with each spatial re-sort.  rx_state_export writes the working
+ * copy to the bound arrays (env order) -- call before reading them;
+ * rx_state_import reads the bound arrays into the working copy -- call after
+ * writing them (state injection).  Both are enqueued on `stream` (a
+ * hipStream_t, NULL = legacy default) without a host sync.  The reference
+ * keeps this state in per-env Python objects (car.py:15-24, racing_env.py:
+ * 17-26), always current. */
+int rx_state_import(rx_env* h, void* stream);
+int rx_state_export(rx_env* h, void* stream);
 
 int rx_set_speed_weight(rx_env* h, double speed_weight);
 

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -86,8 +87,7 @@ struct rx_env {
   int32_t n_chunk_boxes = 0, n_super_boxes = 0;
   // assignment
   bool assigned = false;
-  DevBuf<int32_t> perm[2];  // current env order and the sort target (double-buffered)
-  int cur = 0;
+  DevBuf<int32_t> perm[2];  // the env order (perm[0]: env id at each position) and the re-sort's shadow
   DevBuf<rx_wave> dyn_waves, ray_waves;
   DevBuf<int32_t> slot_n;   // envs per slot (ray-major decode)
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
@@ -98,7 +98,7 @@ struct rx_env {
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
   DevBuf<uint32_t> keys_in;              // [N] bin per perm position (REWARD half)
-  DevBuf<int32_t> vals_in;               // [N] env id per perm position
+  bool sort_pending = false;             // keys written, the re-sort runs after this step's raycast
   DevBuf<uint32_t> sort_hist, sort_cursor;  // [sort_bins]
   DevBuf<int32_t> sort_base;             // [n_tracks] first bin of each slot
   int32_t sort_bins = 0, sort_shift = 0;
@@ -113,9 +113,13 @@ struct rx_env {
   bool prof = false;
   DevBuf<unsigned long long> prof_buf;
   std::vector<int> prof_kinds;
-  // state
+  // state: the caller's arrays (env order, rx_bind_state) and the engine's
+  // working copy in wave order (position p = env perm[p]; the kernels read and
+  // write it coalesced) plus the shadow the re-sort moves rows into
   bool bound = false;
   rx_state st{};
+  rx_state work{}, work_tmp{};
+  std::vector<void*> work_mem;
 };
 
 namespace {
@@ -328,7 +332,7 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
   if (!h->assigned) return fail(RX_ESTATE, "rx_env_order before rx_assign");
   RX_HIP(hipSetDevice(h->cfg.device));
   RX_HIP(hipDeviceSynchronize());
-  RX_HIP(hipMemcpy(perm_out, h->perm[h->cur].p, (size_t)h->cfg.n_envs * sizeof(int32_t), hipMemcpyDeviceToHost));
+  RX_HIP(hipMemcpy(perm_out, h->perm[0].p, (size_t)h->cfg.n_envs * sizeof(int32_t), hipMemcpyDeviceToHost));
   if (sort_bins) *sort_bins = h->sort_on ? h->sort_bins : 0;
   if (sort_shift) *sort_shift = h->sort_shift;
   return RX_OK;
@@ -341,7 +345,7 @@ int rx_destroy(rx_env* h) {
                   &h->wsuper_box, &h->rel_angles})
     b->release();
   for (auto* b : {&h->wp_off, &h->chunk_off, &h->wchunk_off, &h->super_off, &h->wsuper_off, &h->perm[0], &h->perm[1],
-                  &h->vals_in, &h->slot_n, &h->tasks})
+                  &h->slot_n, &h->tasks})
     b->release();
   h->cs_scratch.release();
   h->prof_buf.release();
@@ -350,6 +354,8 @@ int rx_destroy(rx_env* h) {
   h->super_box_f.release();
   h->dyn_waves.release();
   h->ray_waves.release();
+  for (void* m : h->work_mem) (void)hipFree(m);
+  h->work_mem.clear();
   h->keys_in.release();
   h->sort_hist.release();
   h->sort_cursor.release();
@@ -385,6 +391,8 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
   h->assigned = false;  // slots may have changed meaning: require rx_assign again
   return RX_OK;
 }
+
+static int sync_state(rx_env* h, int to_user, void* stream = nullptr, bool blocking = true);
 
 int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if (!h) return fail(RX_EINVAL, "null handle");
@@ -467,7 +475,6 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   if ((rc = upload(h->slot_n, slot_n.data(), slot_n.size()))) return rc;
   if ((rc = upload(h->perm[0], perm.data(), perm.size()))) return rc;
   if ((rc = upload(h->perm[1], perm.data(), perm.size()))) return rc;
-  h->cur = 0;
   if (A == 2) {
     std::vector<uint32_t> z(N, 0u);
     if ((rc = upload(h->resets, z.data(), z.size()))) return rc;
@@ -493,7 +500,6 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       }
       std::vector<uint32_t> zk(std::max<size_t>((size_t)N, (size_t)total), 0u);
       if ((rc = upload(h->sort_base, base.data(), base.size()))) return rc;
-      if ((rc = upload(h->vals_in, perm.data(), perm.size()))) return rc;
       if ((rc = upload(h->keys_in, zk.data(), (size_t)N))) return rc;
       if ((rc = upload(h->sort_hist, zk.data(), (size_t)total))) return rc;
       if ((rc = upload(h->sort_cursor, zk.data(), (size_t)total))) return rc;
@@ -520,7 +526,22 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->n_dyn_waves = (int32_t)dyn.size();
   h->n_ray_waves = (int32_t)ray.size();
   h->assigned = true;
+  h->sort_pending = false;
   if (h->bound && h->st.track) RX_HIP(hipMemcpy(h->st.track, track_of_env, N * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (h->bound) return sync_state(h, 0);  // the new wave order: re-read the caller's arrays
+  return RX_OK;
+}
+
+// working copy <-> the caller's arrays (env order); blocking = finish before
+// returning (bind / assign), else enqueued on the caller's stream
+static int sync_state(rx_env* h, int to_user, void* stream, bool blocking) {
+  if (!h->bound || !h->assigned) return fail(RX_ESTATE, "state sync needs rx_bind_state and rx_assign");
+  RX_HIP(hipSetDevice(h->cfg.device));
+  rx_state user = h->st, work = h->work;
+  if (!user.finished_step) work.finished_step = nullptr;  // A == 1 without the array: nothing to move
+  int rc = rx_state_sync(&work, &user, h->perm[0].p, h->cfg.n_envs, h->cfg.n_agents, to_user, (hipStream_t)stream);
+  if (rc) return fail(RX_EHIP, "state sync failed: %s", hipGetErrorString((hipError_t)rc));
+  if (blocking) RX_HIP(hipDeviceSynchronize());
   return RX_OK;
 }
 
@@ -532,8 +553,41 @@ int rx_bind_state(rx_env* h, const rx_state* st) {
     return fail(RX_EINVAL, "rx_bind_state: every state array except finished_step is required");
   if (h->cfg.n_agents == 2 && !st->finished_step) return fail(RX_EINVAL, "rx_bind_state: finished_step required for 2 agents");
   h->st = *st;
+  if (!h->work.x) {  // working copy + shadow, same shapes as the caller's arrays
+    const size_t N = (size_t)h->cfg.n_envs, NA = N * (size_t)h->cfg.n_agents;
+    for (rx_state* w : {&h->work, &h->work_tmp}) {
+      auto alloc = [&](auto** ptr, size_t bytes) -> int {
+        void* m = nullptr;
+        if (hipMalloc(&m, std::max<size_t>(bytes, 16)) != hipSuccess) return fail(RX_ENOMEM, "working state alloc");
+        RX_HIP(hipMemset(m, 0, std::max<size_t>(bytes, 16)));
+        h->work_mem.push_back(m);
+        *ptr = reinterpret_cast<std::remove_reference_t<decltype(*ptr)>>(m);
+        return RX_OK;
+      };
+      int rc;
+      for (double** f : {&w->x, &w->y, &w->angle, &w->vx, &w->vy, &w->progress, &w->last_progress, &w->last_steering})
+        if ((rc = alloc(f, NA * sizeof(double)))) return rc;
+      if ((rc = alloc(&w->flags, NA))) return rc;
+      if ((rc = alloc(&w->finished_step, NA * sizeof(int32_t)))) return rc;
+      if ((rc = alloc(&w->steps, N * sizeof(int32_t)))) return rc;
+      if ((rc = alloc(&w->env_flags, N))) return rc;
+      if ((rc = alloc(&w->ep_return, N * sizeof(double)))) return rc;
+      if ((rc = alloc(&w->ep_length, N * sizeof(int32_t)))) return rc;
+    }
+  }
   h->bound = true;
+  if (h->assigned) return sync_state(h, 0);
   return RX_OK;
+}
+
+int rx_state_import(rx_env* h, void* stream) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  return sync_state(h, 0, stream, false);
+}
+
+int rx_state_export(rx_env* h, void* stream) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  return sync_state(h, 1, stream, false);
 }
 
 int rx_set_speed_weight(rx_env* h, double w) {
@@ -563,11 +617,13 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
                        h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
                        h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes};
-  a.st = h->st;
+  a.st = h->work;
+  a.st.track = h->st.track;                // read-only, env order
+  a.st.speed_weight = h->st.speed_weight;  // read-only, env order (or nullptr)
   a.io = *io;
   a.dyn_waves = h->dyn_waves.p;
   a.ray_waves = h->ray_waves.p;
-  a.perm = h->perm[h->cur].p;
+  a.perm = h->perm[0].p;
   a.rel_angles = h->rel_angles.p;
   a.reset_mask = mask;
   a.n_dyn_waves = h->n_dyn_waves;
@@ -625,65 +681,53 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   const int A = h->cfg.n_agents;
   const bool split = h->split && mode == RX_MODE_STEP && (A == 2 || h->dyn_lpe == 1) &&
                      h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
+  // Spatial re-sort, every sort_interval dynamics launches: that launch's
+  // REWARD half (or k_dyn) writes the sort keys; the sort -- which moves the
+  // working-state rows -- runs after the step's raycast (the ray tasks name
+  // positions), so the new order applies from the next step.
+  const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
+  if (dyn && h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0) {
+    a.sort_keys = h->keys_in.p;
+    h->sort_pending = true;
+  }
   if (split) {
-    const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
-    const bool sort = dyn && h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
+    uint32_t* keys = a.sort_keys;
     if (dyn) {
+      a.sort_keys = nullptr;
       prof_arm(h, a, RX_KERNEL_KIN);
       if ((rc = rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
         return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
-    }
-    a.tasks_out = nullptr;
-    if (sort) {
-      a.sort_keys = h->keys_in.p;
-      a.sort_vals = h->vals_in.p;
-    }
-    if (dyn) {
+      a.tasks_out = nullptr;
+      a.sort_keys = keys;
       prof_arm(h, a, phases == 3 ? RX_KERNEL_STEP2 : RX_KERNEL_REWARD);
       if ((rc = rx_launch_split(&a, A, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
         return fail(RX_EHIP, "k_step2 launch failed: %s", hipGetErrorString((hipError_t)rc));
     } else {
+      a.tasks_out = nullptr;
       prof_arm(h, a, RX_KERNEL_RAYS);
       if ((rc = rx_launch_step(&a, A, RX_PHASE_RAYS, s)) != 0)
         return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
-    a.prof_ts = nullptr;
-    if (sort) {  // keys written by k_step2: the new env order applies from the next step
-      const int nxt = 1 - h->cur;
-      if ((rc = rx_sort_envs(h->keys_in.p, h->vals_in.p, h->cfg.n_envs, h->sort_hist.p, h->sort_cursor.p,
-                             h->sort_bins, h->perm[nxt].p, s)) != 0)
-        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
-      h->cur = nxt;
+  } else {
+    if (dyn) {
+      prof_arm(h, a, RX_KERNEL_DYN);
+      if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_DYNAMICS, s)) != 0)
+        return fail(RX_EHIP, "k_dyn launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
-    return RX_OK;
-  }
-  if (phases & RX_PHASE_DYNAMICS) {
-    // re-sort the env order every sort_interval dynamics launches (scheduling only)
-    const bool sort = h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0;
-    if (sort) {
-      a.sort_keys = h->keys_in.p;
-      a.sort_vals = h->vals_in.p;
-    }
-    prof_arm(h, a, RX_KERNEL_DYN);
-    if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_DYNAMICS, s)) != 0)
-      return fail(RX_EHIP, "k_dyn launch failed: %s", hipGetErrorString((hipError_t)rc));
-    a.prof_ts = nullptr;
-    if (sort) {
-      const int nxt = 1 - h->cur;
-      if ((rc = rx_sort_envs(h->keys_in.p, h->vals_in.p, h->cfg.n_envs, h->sort_hist.p, h->sort_cursor.p,
-                             h->sort_bins, h->perm[nxt].p, s)) != 0)
-        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
-      h->cur = nxt;
-      a.perm = h->perm[nxt].p;
+    if (phases & RX_PHASE_RAYS) {
+      a.sort_keys = nullptr;
+      a.tasks_out = nullptr;
+      prof_arm(h, a, RX_KERNEL_RAYS);
+      if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_RAYS, s)) != 0)
+        return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
   }
-  if (phases & RX_PHASE_RAYS) {
-    a.sort_keys = nullptr;
-    a.sort_vals = nullptr;
-    a.tasks_out = nullptr;
-    prof_arm(h, a, RX_KERNEL_RAYS);
-    if ((rc = rx_launch_step(&a, h->cfg.n_agents, RX_PHASE_RAYS, s)) != 0)
-      return fail(RX_EHIP, "k_rays launch failed: %s", hipGetErrorString((hipError_t)rc));
+  if (h->sort_pending && (phases & RX_PHASE_RAYS)) {
+    h->sort_pending = false;
+    rx_state work = h->work, tmp = h->work_tmp;
+    if ((rc = rx_sort_envs(h->keys_in.p, h->cfg.n_envs, A, h->sort_hist.p, h->sort_cursor.p, h->sort_bins,
+                           h->perm[0].p, h->perm[1].p, &work, &tmp, s)) != 0)
+      return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
   }
   return RX_OK;
 }
@@ -779,7 +823,6 @@ int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream)
   rx_kargs a{};
   make_kargs(h, io, RX_MODE_STEP, nullptr, a);
   a.sort_keys = nullptr;
-  a.sort_vals = nullptr;
   a.tasks_out = nullptr;
   a.prof_ts = nullptr;
   int rc;

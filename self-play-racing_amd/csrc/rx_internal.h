@@ -64,7 +64,8 @@ struct rx_track_view {
 
 struct rx_kargs {
   rx_track_view tr;
-  rx_state st;
+  rx_state st;                // the engine's working state, position order (element A*p + q is agent q of
+                              // env perm[p]); track and speed_weight are the caller's (env order)
   rx_io io;
   const rx_wave* dyn_waves;
   const rx_wave* ray_waves;
@@ -72,7 +73,6 @@ struct rx_kargs {
   const double* rel_angles;   // [n_sensors]
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
   uint32_t* sort_keys;        // [N] k_dyn writes the sort bin (sort_base[slot] + (waypoint >> sort_shift)) at its perm position, or nullptr
-  int32_t* sort_vals;         // [N] k_dyn writes the env id at its perm position
   const int32_t* sort_base;   // [n_tracks] first sort bin of each slot (ascending with the slot id)
   int32_t sort_shift;         // waypoints per sort bin = 1 << sort_shift
   // ray_order 2: k_dyn writes the direction-sorted (agent, ray) task ids of
@@ -134,5 +134,10 @@ extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* 
 // spatial re-sort (rx_sort.hip): counting sort of the perm positions by the
 // bin keys the REWARD half wrote; hist must be zero on entry and is left zero
 #define RX_SORT_MAX_BINS 65536
-extern "C" int rx_sort_envs(const uint32_t* keys, const int32_t* vals, int n, uint32_t* hist, uint32_t* cursor,
-                            int nbins, int32_t* perm_out, hipStream_t s);
+// and moves the working state rows with their envs (perm, work -> perm_tmp,
+// tmp -> back); rx_state_sync: working copy <-> the caller's arrays
+extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
+                            int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
+                            hipStream_t s);
+extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const int32_t* perm, int n, int A,
+                             int to_user, hipStream_t s);

@@ -384,12 +384,11 @@ __device__ __forceinline__ double speed_of(double vx, double vy) { return __buil
 // place and puts cars that are near each other on the track into the same
 // wavefronts, which is what makes k_rays' per-wave chunk culling effective.
 // Pure scheduling: results never depend on the order.
-__device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k, int e, double progress, int W) {
+__device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k, double progress, int W) {
   if (!a.sort_keys) return;
   int w = (int)(progress * (double)W + 0.5);
   w = w < 0 ? 0 : (w > W ? W : w);
   a.sort_keys[pos] = (uint32_t)(a.sort_base[k] + (w >> a.sort_shift));
-  a.sort_vals[pos] = e;
 }
 
 // ray_order 2: the (agent, ray) tasks of a dynamics wave's envs (64 track
@@ -398,12 +397,13 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
 // holds nearly parallel rays from nearby origins, whichever env they belong to.
 // A per-wave counting sort in LDS: ds_add_rtn ranks every task in its sector,
 // a 64-lane scan turns the sector counts into offsets, and the task ids are
-// written to tasks_out[perm_start*A*R ..].  Runs every step with all 64 lanes
-// of the wave (env lanes have e >= 0).  The direction is the car's new angle
+// written to tasks_out[perm_start*A*R ..] as (A*p + q)*R + r with p the
+// env's position.  Runs every step with all 64 lanes of the wave (env lanes
+// have p >= 0).  The direction is the car's new angle
 // (the one k_rays casts from).  Scheduling only: no result depends on it.
 constexpr int kTaskSectors = 64;
 template <int A>
-__device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int e, const double* ang,
+__device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
                                                  int32_t* cnt) {
   constexpr int kMaxT = 16 * A;  // rx_assign enforces n_sensors <= 16 for ray_order 2
   const int R = a.n_sensors, AR = A * R;
@@ -412,7 +412,7 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
   int pk[kMaxT];  // (rank << 6) | sector per task
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  if (e >= 0) {
+  if (p >= 0) {
 #pragma unroll
     for (int t = 0; t < kMaxT; ++t)
       if (t < AR) {
@@ -434,11 +434,11 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
   cnt[lane] = c - c0;  // exclusive offset of sector `lane`
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  if (e >= 0) {
+  if (p >= 0) {
     int32_t* out = a.tasks_out + (size_t)perm_start * AR;
 #pragma unroll
     for (int t = 0; t < kMaxT; ++t)
-      if (t < AR) out[cnt[pk[t] & 63] + (pk[t] >> 6)] = A * e * R + t;  // task id (A*e + q)*R + r
+      if (t < AR) out[cnt[pk[t] & 63] + (pk[t] >> 6)] = A * p * R + t;  // task id (A*p + q)*R + r
   }
 }
 
@@ -523,25 +523,28 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   const double* __restrict__ meta = a.tr.meta + 8 * k;
   const double width = meta[3];
   if (lane >= we.count) return;
-  const int e = a.perm[we.perm_start + lane];
+  // p = the env's position in the wave order: the engine's working state is
+  // stored in that order (coalesced); e = the env id, the row of every io buffer
+  const int p = we.perm_start + lane;
+  const int e = a.perm[p];
 
   const rx_state& S = a.st;
-  uint8_t ef = S.env_flags[e];
-  uint8_t fl = S.flags[e];
-  Car c{S.x[e], S.y[e], S.angle[e], S.vx[e], S.vy[e], S.progress[e], (fl & RX_F_CRASHED) != 0};
-  double last_steering = REW ? 0.0 : S.last_steering[e];
+  uint8_t ef = S.env_flags[p];
+  uint8_t fl = S.flags[p];
+  Car c{S.x[p], S.y[p], S.angle[p], S.vx[p], S.vy[p], S.progress[p], (fl & RX_F_CRASHED) != 0};
+  double last_steering = REW ? 0.0 : S.last_steering[p];
   // every per-env load up front, so their latencies overlap (not one round trip per use)
   const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
   const float2 act =
       (step_mode && !REW) ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
-  const double last_progress = KIN ? 0.0 : S.last_progress[e];
-  const double ep_ret0 = KIN ? 0.0 : S.ep_return[e];
-  const int ep_len0 = KIN ? 0 : S.ep_length[e];
-  const double speed_w = KIN ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);
-  int steps = S.steps[e];  // REWARD: already advanced by KIN
+  const double last_progress = KIN ? 0.0 : S.last_progress[p];
+  const double ep_ret0 = KIN ? 0.0 : S.ep_return[p];
+  const int ep_len0 = KIN ? 0 : S.ep_length[p];
+  const double speed_w = KIN ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);  // caller's, env order
+  int steps = S.steps[p];  // REWARD: already advanced by KIN
   double cs[2] = {0.0, 0.0};
   if (REW) {
-    const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[e];
+    const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[p];
     cs[0] = sc.x;
     cs[1] = sc.y;
   }
@@ -616,23 +619,23 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   double epr = 0.0, epl_d = 0.0;
   if (!REW && stepping) steps += 1;
   if (!KIN && stepping) {
-    const double p = c.progress;
-    pd = p - last_progress;  // racing_env.py:112-116
-    if (last_progress > 0.9 && p < 0.1)
-      pd = (1.0 - last_progress) + p;
-    else if (last_progress < 0.1 && p > 0.9)
-      pd = -((1.0 - p) + last_progress);
+    const double pg = c.progress;
+    pd = pg - last_progress;  // racing_env.py:112-116
+    if (last_progress > 0.9 && pg < 0.1)
+      pd = (1.0 - last_progress) + pg;
+    else if (last_progress < 0.1 && pg > 0.9)
+      pd = -((1.0 - pg) + last_progress);
     double r = pd * 200;
-    if (!(fl & RX_F_CP25) && 0.25 <= p && p < 0.35) { fl |= RX_F_CP25; r += 20; }
-    if ((fl & RX_F_CP25) && !(fl & RX_F_CP50) && 0.50 <= p && p < 0.60) { fl |= RX_F_CP50; r += 20; }
-    if ((fl & RX_F_CP50) && !(fl & RX_F_CP75) && 0.75 <= p && p < 0.85) { fl |= RX_F_CP75; r += 20; }
+    if (!(fl & RX_F_CP25) && 0.25 <= pg && pg < 0.35) { fl |= RX_F_CP25; r += 20; }
+    if ((fl & RX_F_CP25) && !(fl & RX_F_CP50) && 0.50 <= pg && pg < 0.60) { fl |= RX_F_CP50; r += 20; }
+    if ((fl & RX_F_CP50) && !(fl & RX_F_CP75) && 0.75 <= pg && pg < 0.85) { fl |= RX_F_CP75; r += 20; }
     if (!c.crashed && pd > 0) {  // :137-140
       double ratio = rx_clip(speed_of(c.vx, c.vy) / RX_MAX_SPEED, 0.0, 1.0);
       r += ratio * speed_w;
     }
     if (c.crashed) r -= 60;
     const uint8_t all_cp = RX_F_CP25 | RX_F_CP50 | RX_F_CP75;
-    if ((fl & all_cp) == all_cp && last_progress > 0.9 && p < 0.1 && pd > 0) {  // :145-150
+    if ((fl & all_cp) == all_cp && last_progress > 0.9 && pg < 0.1 && pd > 0) {  // :145-150
       fl |= RX_F_FINISHED;
       r += 100;
       double tb = 200 - ((double)steps / 10);
@@ -646,8 +649,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     epr = ep_ret0 + r;
     const int epl = ep_len0 + 1;
     epl_d = (double)epl;
-    S.ep_return[e] = epr;
-    S.ep_length[e] = epl;
+    S.ep_return[p] = epr;
+    S.ep_length[p] = epl;
     ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
@@ -677,8 +680,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     last_steering = 0.0;
     ef &= (uint8_t)~RX_EF_PENDING_RESET;
     if (KIN) ef |= RX_EF_RESET_NOW;
-    S.ep_return[e] = 0.0;
-    S.ep_length[e] = 0;
+    S.ep_return[p] = 0.0;
+    S.ep_length[p] = 0;
     if (a.io.info && (a.mode == RX_MODE_RESET || a.autoreset == RX_AUTORESET_NEXT_STEP)) {
       double* inf = a.io.info + (size_t)e * RX_INFO_W;
       inf[RX_INFO_SPEED] = 0.0;
@@ -689,41 +692,41 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
   if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
   if (FULL && (stepping || do_reset)) {
-    S.x[e] = c.x;
-    S.y[e] = c.y;
-    S.angle[e] = c.angle;
-    S.vx[e] = c.vx;
-    S.vy[e] = c.vy;
-    S.progress[e] = c.progress;
-    S.last_progress[e] = c.progress;  // racing_env.py:165 (0.0 after reset)
-    S.last_steering[e] = last_steering;
-    S.steps[e] = steps;
-    S.flags[e] = fl;
-    S.env_flags[e] = ef;
+    S.x[p] = c.x;
+    S.y[p] = c.y;
+    S.angle[p] = c.angle;
+    S.vx[p] = c.vx;
+    S.vy[p] = c.vy;
+    S.progress[p] = c.progress;
+    S.last_progress[p] = c.progress;  // racing_env.py:165 (0.0 after reset)
+    S.last_steering[p] = last_steering;
+    S.steps[p] = steps;
+    S.flags[p] = fl;
+    S.env_flags[p] = ef;
   }
   if (KIN && (stepping || do_reset)) {
-    S.x[e] = c.x;
-    S.y[e] = c.y;
-    S.angle[e] = c.angle;
-    S.vx[e] = c.vx;
-    S.vy[e] = c.vy;
-    S.last_steering[e] = last_steering;
-    S.steps[e] = steps;
-    if (moving) reinterpret_cast<double2*>(a.cs_scratch)[e] = make_double2(cs[0], cs[1]);
+    S.x[p] = c.x;
+    S.y[p] = c.y;
+    S.angle[p] = c.angle;
+    S.vx[p] = c.vx;
+    S.vy[p] = c.vy;
+    S.last_steering[p] = last_steering;
+    S.steps[p] = steps;
+    if (moving) reinterpret_cast<double2*>(a.cs_scratch)[p] = make_double2(cs[0], cs[1]);
     if (do_reset) {
-      S.progress[e] = 0.0;
-      S.last_progress[e] = 0.0;
-      S.flags[e] = fl;
-      S.env_flags[e] = ef;
+      S.progress[p] = 0.0;
+      S.last_progress[p] = 0.0;
+      S.flags[p] = fl;
+      S.env_flags[p] = ef;
     }
   }
   if (REW && (stepping || do_reset)) {
     if (stepping) {
-      S.progress[e] = c.progress;
-      S.last_progress[e] = c.progress;  // racing_env.py:165
-      S.flags[e] = fl;
+      S.progress[p] = c.progress;
+      S.last_progress[p] = c.progress;  // racing_env.py:165
+      S.flags[p] = fl;
     }
-    S.env_flags[e] = ef;
+    S.env_flags[p] = ef;
   }
   RX_STAMP(7);
   // ---------------------------------------------------------------- outputs
@@ -755,10 +758,10 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     o[2] = (float)rx_clip(0.0 / 3.0, -1.0, 1.0);  // angular_velocity is always 0
     o[3] = (float)last_steering;
   }
-  if (!KIN) write_sort_key(a, we.perm_start + lane, k, e, c.progress, W);
+  if (!KIN) write_sort_key(a, p, k, c.progress, W);
   if (!REW) {
     ang_out[0] = c.angle;
-    e_out = e;
+    e_out = p;  // the ray tasks name the position (k_rays reads the state there, writes obs row perm[p])
   }
   if (ended) {  // RecordEpisodeStatistics: summed per wave by the caller
     ep_out[0] = epr;
@@ -921,17 +924,18 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   const double width = meta[3];
   const double maxd = meta[4];
   if (lane >= we.count) return;
-  const int e = a.perm[we.perm_start + lane];
+  const int p = we.perm_start + lane;  // working-state position (see dyn1_env)
+  const int e = a.perm[p];             // env id: io rows, the start-slot draw
   const rx_state& S = a.st;
 
-  uint8_t ef = S.env_flags[e];
+  uint8_t ef = S.env_flags[p];
   Car c[2];
   uint8_t fl[2];
   double last_steering[2];
   double csr[2][2];  // REWARD: cos / sin of each stepped car's angle (KIN's cs_scratch)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int i = 2 * e + q;
+    const int i = 2 * p + q;
     fl[q] = S.flags[i];
     c[q] = Car{S.x[i], S.y[i], S.angle[i], S.vx[i], S.vy[i], S.progress[i], (fl[q] & RX_F_CRASHED) != 0};
     last_steering[q] = REW ? 0.0 : S.last_steering[i];
@@ -949,7 +953,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   else
     do_reset = (a.autoreset == RX_AUTORESET_NEXT_STEP) && (ef & RX_EF_PENDING_RESET);
   const bool stepping = (a.mode == RX_MODE_STEP) && !do_reset;
-  int steps = S.steps[e];  // REWARD: already advanced by KIN
+  int steps = S.steps[p];  // REWARD: already advanced by KIN
   double rw[2] = {0.0, 0.0};
   int place[2] = {0, 0};
   bool term = false, trunc = false;
@@ -979,7 +983,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
           cn[q] = cs[q][0];
           sn[q] = cs[q][1];
           have_sc[q] = true;
-          if (KIN) reinterpret_cast<double2*>(a.cs_scratch)[2 * e + q] = make_double2(cs[q][0], cs[q][1]);
+          if (KIN) reinterpret_cast<double2*>(a.cs_scratch)[2 * p + q] = make_double2(cs[q][0], cs[q][1]);
         }
       } else if (mv[q]) {  // car.py:26-43 of the stepped pose
         corners(c[q].x, c[q].y, csr[q][0], csr[q][1], cx[q], cy[q]);
@@ -1056,7 +1060,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   if (!KIN && stepping) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int i = 2 * e + q;
+      const int i = 2 * p + q;
       fl[q] = (uint8_t)((fl[q] & ~RX_F_CRASHED) | (c[q].crashed ? RX_F_CRASHED : 0));
       int32_t fs = S.finished_step[i];
       double r = multi_reward(c[q], fl[q], fs, S.last_progress[i], steps);
@@ -1071,7 +1075,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
       double sc[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int fs = S.finished_step[2 * e + q];
+        const int fs = S.finished_step[2 * p + q];
         double v = (double)((fl[q] & RX_F_FINISHED) ? 10000 : 0) + c[q].progress * 100;
         v = v + (double)(c[q].crashed ? 0 : 10);
         v = v + 1.0 / (double)(fs > 0 ? fs : 10000);
@@ -1082,10 +1086,10 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
       place[1 - first] = 2;
       rw[first] += 250;
     }
-    double epr = S.ep_return[e] + rw[0];
-    int epl = S.ep_length[e] + 1;
-    S.ep_return[e] = epr;
-    S.ep_length[e] = epl;
+    double epr = S.ep_return[p] + rw[0];
+    int epl = S.ep_length[p] + 1;
+    S.ep_return[p] = epr;
+    S.ep_length[p] = epl;
     const bool ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
     if (ended) {  // RecordEpisodeStatistics: summed per wave by the caller
@@ -1125,19 +1129,19 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
       c[q].crashed = false;
       fl[q] = 0;
       last_steering[q] = 0.0;
-      S.finished_step[2 * e + q] = -1;
+      S.finished_step[2 * p + q] = -1;
     }
     steps = 0;
     ef &= (uint8_t)~(RX_EF_PENDING_RESET | RX_EF_TOUCH);
     if (KIN) ef |= RX_EF_RESET_NOW;
-    S.ep_return[e] = 0.0;
-    S.ep_length[e] = 0;
+    S.ep_return[p] = 0.0;
+    S.ep_length[p] = 0;
   }
   if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
   if (FULL && (stepping || do_reset)) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int i = 2 * e + q;
+      const int i = 2 * p + q;
       S.x[i] = c[q].x;
       S.y[i] = c[q].y;
       S.angle[i] = c[q].angle;
@@ -1148,13 +1152,13 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
       S.last_steering[i] = last_steering[q];
       S.flags[i] = fl[q];
     }
-    S.steps[e] = steps;
-    S.env_flags[e] = ef;
+    S.steps[p] = steps;
+    S.env_flags[p] = ef;
   }
   if (KIN && (stepping || do_reset)) {  // the pose the raycast and REWARD read
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int i = 2 * e + q;
+      const int i = 2 * p + q;
       S.x[i] = c[q].x;
       S.y[i] = c[q].y;
       S.angle[i] = c[q].angle;
@@ -1167,20 +1171,20 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
         S.flags[i] = fl[q];
       }
     }
-    S.steps[e] = steps;
-    S.env_flags[e] = ef;
+    S.steps[p] = steps;
+    S.env_flags[p] = ef;
   }
   if (REW && (stepping || do_reset)) {
     if (stepping) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int i = 2 * e + q;
+        const int i = 2 * p + q;
         S.progress[i] = c[q].progress;
         S.last_progress[i] = c[q].progress;
         S.flags[i] = fl[q];
       }
     }
-    S.env_flags[e] = ef;
+    S.env_flags[p] = ef;
   }
   // outputs: reset-by-NEXT_STEP / explicit reset gives reward 0, term = trunc = False
   if (FULL || (REW && stepping) || (KIN && !stepping)) {
@@ -1225,11 +1229,11 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
     ob[6] = (float)rx_clip(lvx / RX_MAX_SPEED, -1.0, 1.0);
     ob[7] = (float)rx_clip(lvy / RX_MAX_SPEED, -1.0, 1.0);
   }
-  if (!KIN) write_sort_key(a, we.perm_start + lane, k, e, c[0].progress, W);
+  if (!KIN) write_sort_key(a, p, k, c[0].progress, W);
   if (!REW) {
     ang_out[0] = c[0].angle;
     ang_out[1] = c[1].angle;
-    e_out = e;
+    e_out = p;
   }
 }
 
@@ -1343,7 +1347,7 @@ __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx
 }
 
 template <int A>
-__device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int q, int ray, double ox, double oy,
+__device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, int ray, double ox, double oy,
                                            double v3x, double v3y, double best);
 
 // chunk_needed_f for a wave whose lanes all cast into one direction quadrant:
@@ -1442,13 +1446,13 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (lane >= we.count) return;
   const int R = a.n_sensors;
   const int task = we.task_start + lane;
-  int env_local = 0, q, ray, e;
+  int env_local = 0, q, ray, pos;
   if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
     const int t = a.tasks[task];
     const int iq = t / R;
     ray = t - iq * R;
-    e = iq / A;
-    q = iq - e * A;
+    pos = iq / A;
+    q = iq - pos * A;
   } else if (a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
     env_local = task / (A * R);
     const int rem = task - env_local * (A * R);
@@ -1461,8 +1465,8 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
     q = qr / R;
     ray = qr - q * R;
   }
-  if (a.ray_order != 2) e = a.perm[we.perm_start + env_local];
-  const int i = A * e + q;
+  if (a.ray_order != 2) pos = we.perm_start + env_local;
+  const int i = A * pos + q;  // working state (position order); the obs row is A * perm[pos] + q
   const double ox = a.st.x[i], oy = a.st.y[i];
   const double theta = a.st.angle[i] + a.rel_angles[ray];  // racing_env.py:50
   double sn, cs;
@@ -1513,7 +1517,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
   }
-  ray_finish<A>(a, i, e, q, ray, ox, oy, v3x, v3y, best);
+  ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);
 }
 
 // The observation of one ray from the wall minimum `best` (inf = no hit):
@@ -1521,11 +1525,11 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
 // the other car's edges for A = 2 (MultiTrack.raycast_with_cars,
 // multi_track.py:5-44), float32 division by 50 (racing_env.py:46,51,53).
 template <int A>
-__device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int q, int ray, double ox, double oy,
+__device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, int ray, double ox, double oy,
                                            double v3x, double v3y, double best) {
   double dist = (best == __builtin_inf()) ? RX_MAX_RANGE : best;
   if (A == 2) {
-    const int o = A * e + (1 - q);
+    const int o = A * pos + (1 - q);  // the other car (working state)
     const double ocx = a.st.x[o], ocy = a.st.y[o];
     const double dx = ocx - ox, dy = ocy - oy;
     double min_car = RX_MAX_RANGE;
@@ -1548,7 +1552,8 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int i, int e, int 
     }
     dist = (min_car < dist) ? min_car : dist;
   }
-  a.io.obs[(size_t)i * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
+  const int e = a.perm[pos];
+  a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 
 template <int A>
@@ -1566,8 +1571,8 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
 // exact t of hits is order-independent, hence bit-identical to k_rays.
 template <int A>
 __device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray, const double4* seg_lds = nullptr) {
-  const int e = iq / A, q = iq - e * A;
-  const int k = uniform(a.st.track[e]);
+  const int pos = iq / A, q = iq - pos * A;  // iq = A * position + agent (working state)
+  const int k = uniform(a.st.track[a.perm[pos]]);
   const int wp0 = uniform(a.tr.wp_off[k]);
   const int S_ = 2 * (uniform(a.tr.wp_off[k + 1]) - wp0);
   const double4* __restrict__ seg = seg_lds ? seg_lds : reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
@@ -1588,7 +1593,7 @@ __device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray, con
   for (; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
-  if ((threadIdx.x & 63) == 0) ray_finish<A>(a, iq, e, q, ray, ox, oy, v3x, v3y, best);
+  if ((threadIdx.x & 63) == 0) ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);
 }
 
 template <int A>
@@ -1684,7 +1689,8 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
   const int b = blockIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t n = a.n_dyn_waves;  // = envs (one per dynamics wave)
-  const int e = a.perm[a.dyn_waves[b].perm_start];
+  const int pos = a.dyn_waves[b].perm_start;  // working-state position of this workgroup's env
+  const int e = a.perm[pos];                   // its env id: the rollout buffers' row
   const float* __restrict__ P = r.params;
   for (int i = threadIdx.x; i < D * H; i += blockDim.x) {
     const int j = i / D, d = i - j * D;
@@ -1798,7 +1804,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         add_episode_stats(at, ep);
         RX_RSTAMP(4);
       } else {
-        for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, e, ray, sl.seg);
+        for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, pos, ray, sl.seg);
         if (w == 1) RX_RSTAMP(5);
       }
     } else {  // same-step autoreset: the whole step first (k_dyn1's order)
@@ -1807,7 +1813,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         add_episode_stats(at, ep);
       }
       __syncthreads();
-      for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, e, ray, sl.seg);
+      for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, pos, ray, sl.seg);
     }
     __syncthreads();  // obs[t+1] complete before the next policy step
     if (w == 0) RX_RSTAMP(3);

@@ -1,20 +1,27 @@
 // rx_sort.hip -- the spatial re-sort of the env order (every sort_interval
-// dynamics launches): envs regrouped into track-coherent wavefronts.
+// dynamics launches), which also MOVES the engine's working state: the env
+// state lives in wave order (position p holds env perm[p]), so the kernels'
+// state reads and writes are coalesced, and a re-sort permutes it.
 // Scheduling only: no result depends on the order (test_culling_and_sort_are_exact).
 //
 // The key the REWARD half writes per perm position is a BIN: the slot's bin
 // base (bases ascend with the slot id) + (closest waypoint >> shift), so bins
 // of one slot are contiguous, slot groups keep their place in the perm, and
 // the whole key space is <= RX_SORT_MAX_BINS (rx_assign picks the shift).  A
-// counting sort over that small key space, three launches:
+// counting sort over that small key space, four launches:
 //   k_sort_hist     per wave: lanes grouped by bin (ballot), one atomic per group
 //   k_sort_scan     one workgroup: exclusive scan of the histogram -> cursors,
 //                   histogram cleared for the next sort
 //   k_sort_scatter  per wave: the same grouping, one cursor atomic per group,
-//                   lane rank within its group -> perm_out[base + rank] = env
+//                   lane rank within its group -> new position; the env id and
+//                   its whole state row move there (into the shadow copy)
+//   k_state_copy    shadow -> working copy (coalesced), so every launch keeps
+//                   reading the same buffers (HIP-graph replay safe)
 // The envs of a wave are track neighbours (the previous sort), so a wave sees
 // only a handful of bins: a few atomics per wave.  Order inside a bin follows
 // the atomic order of the waves (not fixed run to run; nothing depends on it).
+//
+// rx_state_sync: the caller's bound arrays (env order) <-> the working copy.
 #include <hip/hip_runtime.h>
 
 #include "rx_internal.h"
@@ -71,14 +78,38 @@ __global__ __launch_bounds__(kScanThreads) void k_sort_scan(uint32_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
-                                                          const int32_t* __restrict__ vals, int n,
+// one env's state row: working-state element i (position) -> j
+template <int A>
+__device__ __forceinline__ void move_row(const rx_state& src, int i, const rx_state& dst, int j) {
+#pragma unroll
+  for (int q = 0; q < A; ++q) {
+    const int si = A * i + q, di = A * j + q;
+    dst.x[di] = src.x[si];
+    dst.y[di] = src.y[si];
+    dst.angle[di] = src.angle[si];
+    dst.vx[di] = src.vx[si];
+    dst.vy[di] = src.vy[si];
+    dst.progress[di] = src.progress[si];
+    dst.last_progress[di] = src.last_progress[si];
+    dst.last_steering[di] = src.last_steering[si];
+    dst.flags[di] = src.flags[si];
+    if (src.finished_step) dst.finished_step[di] = src.finished_step[si];
+  }
+  dst.steps[j] = src.steps[i];
+  dst.env_flags[j] = src.env_flags[i];
+  dst.ep_return[j] = src.ep_return[i];
+  dst.ep_length[j] = src.ep_length[i];
+}
+
+template <int A>
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restrict__ keys, int n,
                                                           uint32_t* __restrict__ cursor,
-                                                          int32_t* __restrict__ perm_out) {
+                                                          const int32_t* __restrict__ perm,
+                                                          int32_t* __restrict__ perm_tmp, rx_state work,
+                                                          rx_state tmp) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const bool v = i < n;
   const uint32_t b = v ? keys[i] : 0u;
-  const int32_t e = v ? vals[i] : 0;
   unsigned long long pending = __ballot(v);
   uint32_t dst = 0;
   while (pending) {
@@ -91,18 +122,63 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restr
     if (v && b == lb) dst = base + (uint32_t)rank_below(m);
     pending &= ~m;
   }
-  if (v) perm_out[dst] = e;
+  if (!v) return;
+  perm_tmp[dst] = perm[i];
+  move_row<A>(work, i, tmp, (int)dst);
+}
+
+template <int A>
+__global__ __launch_bounds__(kBlock) void k_state_copy(int n, const int32_t* __restrict__ perm_tmp,
+                                                        int32_t* __restrict__ perm, rx_state tmp, rx_state work) {
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  perm[j] = perm_tmp[j];
+  move_row<A>(tmp, j, work, j);
+}
+
+// to_user: working row p -> the caller's row perm[p]; else the reverse
+template <int A>
+__global__ __launch_bounds__(kBlock) void k_state_sync(int n, const int32_t* __restrict__ perm, rx_state work,
+                                                        rx_state user, int to_user) {
+  const int p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n) return;
+  const int e = perm[p];
+  if (to_user)
+    move_row<A>(work, p, user, e);
+  else
+    move_row<A>(user, e, work, p);
 }
 
 }  // namespace
 
-extern "C" int rx_sort_envs(const uint32_t* keys, const int32_t* vals, int n, uint32_t* hist, uint32_t* cursor,
-                            int nbins, int32_t* perm_out, hipStream_t s) {
+extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
+                            int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
+                            hipStream_t s) {
   if (n <= 0) return 0;
-  if (nbins <= 0 || nbins > RX_SORT_MAX_BINS) return (int)hipErrorInvalidValue;
+  if (nbins <= 0 || nbins > RX_SORT_MAX_BINS || (A != 1 && A != 2)) return (int)hipErrorInvalidValue;
   const int grid = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist);
   hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanThreads), 0, s, hist, cursor, nbins);
-  hipLaunchKernelGGL(k_sort_scatter, dim3(grid), dim3(kBlock), 0, s, keys, vals, n, cursor, perm_out);
+  if (A == 1) {
+    hipLaunchKernelGGL(k_sort_scatter<1>, dim3(grid), dim3(kBlock), 0, s, keys, n, cursor, perm, perm_tmp, *work,
+                       *tmp);
+    hipLaunchKernelGGL(k_state_copy<1>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
+  } else {
+    hipLaunchKernelGGL(k_sort_scatter<2>, dim3(grid), dim3(kBlock), 0, s, keys, n, cursor, perm, perm_tmp, *work,
+                       *tmp);
+    hipLaunchKernelGGL(k_state_copy<2>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const int32_t* perm, int n, int A,
+                             int to_user, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (A != 1 && A != 2) return (int)hipErrorInvalidValue;
+  const int grid = (n + kBlock - 1) / kBlock;
+  if (A == 1)
+    hipLaunchKernelGGL(k_state_sync<1>, dim3(grid), dim3(kBlock), 0, s, n, perm, *work, *user, to_user);
+  else
+    hipLaunchKernelGGL(k_state_sync<2>, dim3(grid), dim3(kBlock), 0, s, n, perm, *work, *user, to_user);
   return (int)hipGetLastError();
 }

@@ -71,6 +71,7 @@ class Evaluator:
             else:
                 a = agent.get_action_and_value(obs)[0]
             obs, _, done = v.step_device(a, full_info=True)
+            st = v.state  # writes the stepped state back into x, y, flags (rx_state_export)
             r64 = v.buf["reward64"]
             info = v.buf["info"][:, 0]
             total_reward += torch.where(active, r64, torch.zeros_like(r64))
@@ -81,7 +82,7 @@ class Evaluator:
             px.copy_(x)
             py.copy_(y)
             steps += active.long()
-            fl = v.state["flags"]
+            fl = st["flags"]
             fin = torch.where(active, (fl & 2) != 0, fin)
             crash = torch.where(active, (fl & 1) != 0, crash)
             prog = torch.where(active, info[:, 1], prog)
@@ -161,6 +162,7 @@ class MultiEvaluator:
         for t in range(self.max_steps):
             a = agent.get_action_and_value(obs.reshape(2 * N, D))[0].reshape(N, 2, 2)
             obs, _, done = v.step_device(a, full_info=True)
+            st = v.state  # writes the stepped state back into x, y, flags (rx_state_export)
             act2 = active.unsqueeze(1)
             total_reward += torch.where(act2, v.buf["reward64"], torch.zeros_like(total_reward))
             if not first:
@@ -171,7 +173,7 @@ class MultiEvaluator:
             py.copy_(y)
             steps += active.long()
             info_last = torch.where(act2.unsqueeze(2), v.buf["info"], info_last)
-            flags_last = torch.where(act2, v.state["flags"].view(N, 2), flags_last)
+            flags_last = torch.where(act2, st["flags"].view(N, 2), flags_last)
             active &= ~done.bool()
             if t % 50 == 49 and not bool(active.any()):
                 break

@@ -90,15 +90,18 @@ class RacingVectorEnv:
         dev = self.device
         with torch.cuda.device(dev):
             f64 = dict(dtype=torch.float64, device=dev)
-            self.state = {k: torch.zeros(N * A, **f64) for k in ("x", "y", "angle", "vx", "vy", "progress",
-                                                               "last_progress", "last_steering")}
-            self.state["finished_step"] = torch.full((N * A,), -1, dtype=torch.int32, device=dev)
-            self.state["flags"] = torch.zeros(N * A, dtype=torch.uint8, device=dev)
-            self.state["steps"] = torch.zeros(N, dtype=torch.int32, device=dev)
-            self.state["track"] = torch.from_numpy(slots).to(dev)
-            self.state["env_flags"] = torch.zeros(N, dtype=torch.uint8, device=dev)
-            self.state["ep_return"] = torch.zeros(N, **f64)
-            self.state["ep_length"] = torch.zeros(N, dtype=torch.int32, device=dev)
+            # the bound state arrays (env order); the engine steps a working copy in
+            # wave order and writes these back on demand (the `state` property)
+            self._dev_newer = False
+            self._st = {k: torch.zeros(N * A, **f64) for k in ("x", "y", "angle", "vx", "vy", "progress",
+                                                             "last_progress", "last_steering")}
+            self._st["finished_step"] = torch.full((N * A,), -1, dtype=torch.int32, device=dev)
+            self._st["flags"] = torch.zeros(N * A, dtype=torch.uint8, device=dev)
+            self._st["steps"] = torch.zeros(N, dtype=torch.int32, device=dev)
+            self._st["track"] = torch.from_numpy(slots).to(dev)
+            self._st["env_flags"] = torch.zeros(N, dtype=torch.uint8, device=dev)
+            self._st["ep_return"] = torch.zeros(N, **f64)
+            self._st["ep_length"] = torch.zeros(N, dtype=torch.int32, device=dev)
             obs_shape = (N, self.D) if A == 1 else (N, A, self.D)
             self.buf = dict(
                 actions=torch.zeros((N, A, 2), dtype=torch.float32, device=dev),
@@ -119,7 +122,7 @@ class RacingVectorEnv:
             _lib.check(self.L.rx_create(cfg, h), "rx_create")
             self._h = h
             self._upload_tracks()
-            self.state["speed_weight"] = None  # per-env weights: set_speed_weights()
+            self._st["speed_weight"] = None  # per-env weights: set_speed_weights()
             st = self._state_struct()
             _lib.check(self.L.rx_bind_state(self._h, st), "rx_bind_state")
             _lib.check(self.L.rx_assign(self._h, _lib.ptr(np.ascontiguousarray(slots))), "rx_assign")
@@ -198,15 +201,37 @@ class RacingVectorEnv:
                 "wp_chunks_scanned": int(c[3])}
 
     def _state_struct(self):
-        return _lib.RxState(*[_lib.ptr(self.state[k]) for k in _lib.STATE_FIELDS])
+        return _lib.RxState(*[_lib.ptr(self._st[k]) for k in _lib.STATE_FIELDS])
+
+    @property
+    def state(self):
+        """The env state tensors in env order (x, y, angle, ... [N*A]; steps, ... [N]).
+        The engine steps a working copy in wave order (rx.h, ABI v15); reading
+        this property first writes it back here (rx_state_export, enqueued on
+        the current stream) if a launch changed it.  After writing the tensors,
+        call ``state_changed()`` (set_state does)."""
+        if self._dev_newer and not self._closed:
+            _lib.check(self.L.rx_state_export(self._h, _lib.stream_ptr()), "rx_state_export")
+            self._dev_newer = False
+        return self._st
+
+    def state_changed(self, stream=None):
+        """The state tensors were written: reload the engine's working copy."""
+        _lib.check(self.L.rx_state_import(self._h, _lib.stream_ptr(stream)), "rx_state_import")
+        self._dev_newer = False
+
+    def _launched(self):
+        self._dev_newer = True
 
     def set_speed_weights(self, w):
         """Per-env RacingEnv.speed_weight ([N] array), or None to use the uniform value."""
+        st = self.state  # current values in the bound arrays: re-binding re-reads them
         if w is None:
-            self.state["speed_weight"] = None
+            st["speed_weight"] = None
         else:
-            self.state["speed_weight"] = torch.as_tensor(np.asarray(w, dtype=np.float64).reshape(self.num_envs)).to(
+            st["speed_weight"] = torch.as_tensor(np.asarray(w, dtype=np.float64).reshape(self.num_envs)).to(
                 self.device).contiguous()
+        torch.cuda.current_stream(self.device).synchronize()
         _lib.check(self.L.rx_bind_state(self._h, self._state_struct()), "rx_bind_state")
 
     def set_speed_weight(self, w):
@@ -237,6 +262,7 @@ class RacingVectorEnv:
             m = mask.to(self.device, torch.uint8).contiguous()
         io = self._io(obs=obs_out, full=True)
         _lib.check(self.L.rx_reset(self._h, _lib.ptr(m), io, _lib.stream_ptr(stream)), "rx_reset")
+        self._dev_newer = True
         return obs_out if obs_out is not None else self.buf["obs"]
 
     def step_device(self, actions, obs_out=None, reward_out=None, done_out=None, full_info=False, stream=None,
@@ -252,6 +278,7 @@ class RacingVectorEnv:
             _lib.check(self.L.rx_step(self._h, io, _lib.stream_ptr(stream)), "rx_step")
         else:
             _lib.check(self.L.rx_step_phases(self._h, io, int(phases), _lib.stream_ptr(stream)), "rx_step_phases")
+        self._dev_newer = True
         return (obs_out if obs_out is not None else self.buf["obs"],
                 reward_out if reward_out is not None else self.buf["reward"],
                 done_out if done_out is not None else self.buf["done_f32"])
@@ -278,9 +305,11 @@ class RacingVectorEnv:
 
     def set_state(self, **arrays):
         """State injection (parity tests): overwrite state arrays from host arrays."""
+        st = self.state
         for k, v in arrays.items():
-            t = self.state[k]
+            t = st[k]
             t.copy_(torch.as_tensor(np.ascontiguousarray(v).reshape(t.shape)).to(t.device, t.dtype))
+        self.state_changed()
 
     # ------------------------------------------------------------ numpy surface
     def reset(self, seed=None, options=None):
