@@ -526,22 +526,27 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   // p = the env's position in the wave order: the engine's working state is
   // stored in that order (coalesced); e = the env id, the row of every io buffer
   const int p = we.perm_start + lane;
-  const int e = a.perm[p];
+  int e = REW ? -1 : a.perm[p];  // REWARD: loaded after the argmins
 
   const rx_state& S = a.st;
   uint8_t ef = S.env_flags[p];
   uint8_t fl = S.flags[p];
-  Car c{S.x[p], S.y[p], S.angle[p], S.vx[p], S.vy[p], S.progress[p], (fl & RX_F_CRASHED) != 0};
+  // every per-env load up front, so their latencies overlap (not one round
+  // trip per use) -- except in the REWARD half, which runs under the raycast
+  // at the raycast's 64-VGPR budget: its values not needed by the argmins
+  // (velocity, last progress, episode counters, steps) load after them, so
+  // they are not live across the argmin loops (fewer spills)
+  Car c{S.x[p], S.y[p], REW ? 0.0 : S.angle[p], REW ? 0.0 : S.vx[p], REW ? 0.0 : S.vy[p], S.progress[p],
+        (fl & RX_F_CRASHED) != 0};
   double last_steering = REW ? 0.0 : S.last_steering[p];
-  // every per-env load up front, so their latencies overlap (not one round trip per use)
   const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
   const float2 act =
       (step_mode && !REW) ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
-  const double last_progress = KIN ? 0.0 : S.last_progress[p];
-  const double ep_ret0 = KIN ? 0.0 : S.ep_return[p];
-  const int ep_len0 = KIN ? 0 : S.ep_length[p];
-  const double speed_w = KIN ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);  // caller's, env order
-  int steps = S.steps[p];  // REWARD: already advanced by KIN
+  double last_progress = (KIN || REW) ? 0.0 : S.last_progress[p];
+  double ep_ret0 = (KIN || REW) ? 0.0 : S.ep_return[p];
+  int ep_len0 = (KIN || REW) ? 0 : S.ep_length[p];
+  double speed_w = (KIN || REW) ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);  // caller's, env order
+  int steps = REW ? 0 : S.steps[p];  // REWARD: already advanced by KIN
   double cs[2] = {0.0, 0.0};
   if (REW) {
     const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[p];
@@ -615,6 +620,16 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
   RX_STAMP(6);
   if (sub != 0) return;  // one lane per env from here on
+  if (REW) {  // the REWARD half's late loads (see above)
+    e = a.perm[p];
+    c.vx = S.vx[p];
+    c.vy = S.vy[p];
+    last_progress = S.last_progress[p];
+    ep_ret0 = S.ep_return[p];
+    ep_len0 = S.ep_length[p];
+    speed_w = S.speed_weight ? S.speed_weight[e] : a.speed_weight;
+    steps = S.steps[p];
+  }
   bool ended = false;
   double epr = 0.0, epl_d = 0.0;
   if (!REW && stepping) steps += 1;

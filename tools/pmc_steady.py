@@ -34,8 +34,8 @@ PASSES = [
     ["TCC_HIT_sum", "TCC_MISS_sum", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_WAVES",
      "SQ_BUSY_CYCLES", "SQ_INST_LEVEL_VMEM", "GRBM_GUI_ACTIVE"],
 ]
-KERNELS = ("k_step2", "k_kin1", "k_kin2", "k_rays", "k_dyn1", "k_dyn2", "k_gae", "k_sort", "k_ppo_grad",
-           "k_policy_act")
+KERNELS = ("k_step2", "k_kin1", "k_kin2", "k_rays", "k_dyn1", "k_dyn2", "k_gae", "k_sort_hist", "k_sort_scan",
+           "k_sort_scatter", "k_state_copy", "k_state_sync", "k_ppo_grad", "k_policy_act")
 
 
 def short(name):
