@@ -85,6 +85,7 @@ struct rx_env {
   DevBuf<double> wsuper_box;
   DevBuf<float> chunk_box_f, super_box_f;  // outward-rounded float32 copies (raycast box tests) + 4 quadrant blocks
   int32_t n_chunk_boxes = 0, n_super_boxes = 0;
+  DevBuf<float> seg_f;  // [2*Wtot][4] float32 (start.x, start.y, v2.x, v2.y): the raycast's segment pre-filter
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // the env order (perm[0]: env id at each position) and the re-sort's shadow
@@ -352,6 +353,7 @@ int rx_destroy(rx_env* h) {
   h->resets.release();
   h->chunk_box_f.release();
   h->super_box_f.release();
+  h->seg_f.release();
   h->dyn_waves.release();
   h->ray_waves.release();
   for (void* m : h->work_mem) (void)hipFree(m);
@@ -384,6 +386,11 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
   if ((rc = upload(h->wp, wp, 2 * Wt))) return rc;
   if ((rc = upload(h->nrm, nrm, 2 * Wt))) return rc;
   if ((rc = upload(h->seg, seg, 8 * Wt))) return rc;
+  {  // float32 copy of the segments (nearest rounding; the kernel's error bound covers it)
+    std::vector<float> sf(8 * (size_t)Wt);
+    for (size_t i = 0; i < sf.size(); ++i) sf[i] = (float)seg[i];
+    if ((rc = upload(h->seg_f, sf.data(), sf.size()))) return rc;
+  }
   if ((rc = upload(h->meta, meta, 8 * (size_t)n_tracks))) return rc;
   if ((rc = build_chunks(h, n_tracks, wp_off, wp, seg))) return rc;
   h->wp_off_h.assign(wp_off, wp_off + n_tracks + 1);
@@ -616,7 +623,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
                        h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
-                       h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes};
+                       h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes, h->seg_f.p};
   a.st = h->work;
   a.st.track = h->st.track;                // read-only, env order
   a.st.speed_weight = h->st.speed_weight;  // read-only, env order (or nullptr)
@@ -654,6 +661,8 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
     return e ? atoi(e) : 1;
   }();
   a.box_quadrants = quad;
+  const char* pf = getenv("RX_SEG_FILTER");  // A/B knob, read per launch so tests can run both paths
+  a.seg_filter = pf ? atoi(pf) : 1;
 #ifdef RX_AB_NO_EPSTATS  // A/B build only (tools/build_rev.py): drop the episode-statistics atomics
   a.io.ep_stats = nullptr;
 #endif

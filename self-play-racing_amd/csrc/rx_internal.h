@@ -43,6 +43,7 @@ struct rx_track_view {
   const float* super_box_f;  // then 4 quadrant blocks of (near.x, near.y, far.x, far.y) (rx_api.cpp)
   int32_t n_chunk_boxes;     // boxes per block
   int32_t n_super_boxes;
+  const float* seg_f;        // [2*Wtot][4] float32 copy of seg (culled raycast: segment pre-filter)
 };
 
 #ifndef RX_WP_CHUNK
@@ -102,6 +103,7 @@ struct rx_kargs {
   uint64_t seed;
   uint32_t* reset_count;  // [N] (2-car envs), advanced by k_dyn2 at every reset
   int32_t box_quadrants;  // k_rays: single-quadrant waves use the quadrant-ordered box tables (RX_BOX_QUAD=0: off)
+  int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

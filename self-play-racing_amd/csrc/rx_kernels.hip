@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 #include <stdint.h>
 
 #include "rx.h"
@@ -1310,12 +1311,54 @@ __device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, 
   }
 }
 
+typedef float rx_f2 __attribute__((ext_vector_type(2)));
+
+// Segment pre-filter (float32, one lane's ray).  With a = (o - start) . v3
+// (the reference's `dot`) and p = v2 . v3 (`dotp`), s = a / p lies in [0, 1]
+// iff a and a - p do not share a strict sign, i.e. iff
+// |2a - p| - |p| <= 0.  Computed in float32 from the float32 segment table,
+// the left side is within 2^-22 (3.5 M1 + 4.2 L) of its value on the f64
+// operands (M1 = |ox| + |oy| + |sx| + |sy|, L = the slot's longest segment),
+// and those differ from the exact one by ~2^-50 (M1 + L).  So a segment this
+// test rejects, with e2 = 2^-17 (M1 + L + 1) >= 8x that bound, has a and a - p
+// of one strict sign by a margin >= 2^-18 (M1 + L): the f64 test then sees
+// N < 0 or fl(N - D) > D 2^-53 and reports no hit.  Rejecting it changes
+// nothing; the wave runs the exact test on a segment iff some lane may hit it.
+struct seg_pref {
+  const float4* __restrict__ segf;  // the slot's float32 segments
+  rx_f2 of, v3f;                    // origin, (-sin, cos) in float32
+  float e2;                         // 2^-17 (|ox| + |oy| + max(|sx| + |sy|) + L + 1)
+};
+__device__ __forceinline__ bool seg_may_hit(const float4 f, const seg_pref& pf) {
+  const rx_f2 pa = (pf.of - rx_f2{f.x, f.y}) * pf.v3f;
+  const rx_f2 pd = rx_f2{f.z, f.w} * pf.v3f;
+  const float aa = pa.x + pa.y, dp = pd.x + pd.y;
+  return !(__builtin_fabsf(__builtin_fmaf(2.0f, aa, -dp)) - __builtin_fabsf(dp) > pf.e2);
+}
+
 // Segments [j0, j1) of a wave-uniform slot, four scalar loads in flight at a
 // time (each test ends in a divergent branch, so a plain loop would wait for
-// every s_load on its own).
+// every s_load on its own).  FILT: the exact test of a segment runs only if
+// the float32 pre-filter passes for some lane.
+template <bool FILT>
 __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
-                                             double v3x, double v3y, double& best, float& bestf) {
+                                             double v3x, double v3y, double& best, float& bestf, const seg_pref& pf) {
   int j = j0;
+  if constexpr (FILT) {
+    for (; j + 4 <= j1; j += 4) {
+      const float4 f0 = ldu(pf.segf + j), f1 = ldu(pf.segf + j + 1), f2 = ldu(pf.segf + j + 2),
+                   f3 = ldu(pf.segf + j + 3);
+      const bool h0 = __any(seg_may_hit(f0, pf)), h1 = __any(seg_may_hit(f1, pf)), h2 = __any(seg_may_hit(f2, pf)),
+                 h3 = __any(seg_may_hit(f3, pf));
+      if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
+      if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best, bestf);
+      if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best, bestf);
+      if (h3) seg_test(ldu(seg + j + 3), ox, oy, v3x, v3y, best, bestf);
+    }
+    for (; j < j1; ++j)
+      if (__any(seg_may_hit(ldu(pf.segf + j), pf))) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
+    return;
+  }
   for (; j + 4 <= j1; j += 4) {
     const double4 g0 = ldu(seg + j), g1 = ldu(seg + j + 1), g2 = ldu(seg + j + 2), g3 = ldu(seg + j + 3);  // uniform -> s_load
     seg_test(g0, ox, oy, v3x, v3y, best, bestf);
@@ -1348,7 +1391,6 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
 // empty-interval test and the entry distance absorbs it; bestf >= best.  An
 // f32 direction component of 0 gives +-inf slab bounds (NaN when the origin
 // sits on the slab plane, which fmin/fmax drop: the axis is then unconstrained).
-typedef float rx_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 nlo, rx_f2 nhi, rx_f2 id2,
                                                float mtf, float bestf) {
   const float4 b = ldu(reinterpret_cast<const float4*>(box));
@@ -1389,11 +1431,11 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
 // `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far);
 // otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi).
-template <bool FAST>
+template <bool FAST, bool FILT>
 __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
                                           int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
                                           double oy, double v3x, double v3y, double& best, float& bestf, int& tested,
-                                          int& scanned) {
+                                          int& scanned, const seg_pref& pf) {
   const int G = a.cull_chunk;
   const float* __restrict__ fboxes =
       a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uniform(a.tr.chunk_off[k]));
@@ -1411,7 +1453,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (__any(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
+          ray_segments<FILT>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf,
+                             pf);
         }
       }
     }
@@ -1441,7 +1484,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (__any(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          ray_segments(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf);
+          ray_segments<FILT>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf,
+                             pf);
         }
       }
     }
@@ -1491,7 +1535,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   float bestf = __builtin_inff();
   const int G = a.cull_chunk;
   if (G <= 0) {
-    ray_segments(seg, 0, S_, ox, oy, v3x, v3y, best, bestf);
+    ray_segments<false>(seg, 0, S_, ox, oy, v3x, v3y, best, bestf, seg_pref{});
   } else {
     const int nch = (W + G - 1) / G;  // chunks per side
     const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
@@ -1519,14 +1563,26 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
     const int quad = (int)(__float_as_uint(csf) >> 31) | (int)((__float_as_uint(snf) >> 31) << 1);
     const int quad0 = uniform(quad);
     int scanned = 0, tested = 0;
-    if (a.box_quadrants && __all(quad == quad0)) {
-      const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
-      const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
-      cull_scan<true>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
-                      scanned);
-    } else {
-      cull_scan<false>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested, scanned);
-    }
+    // segment pre-filter operands (seg_may_hit): |sx| + |sy| <= |cx| + |cy| + 2 rad for every boundary point
+    const seg_pref pf{reinterpret_cast<const float4*>(a.tr.seg_f) + 2 * wp0, rx_f2{oxf, oyf}, rx_f2{-snf, csf},
+                      (float)((__builtin_fabs(ox) + __builtin_fabs(oy) + __builtin_fabs(cx) + __builtin_fabs(cy) +
+                               2.0 * rad + L + 1.0) * 0x1p-17)};
+    auto scan = [&](auto filt) {
+      constexpr bool F = decltype(filt)::value;
+      if (a.box_quadrants && __all(quad == quad0)) {
+        const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
+        const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
+        cull_scan<true, F>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
+                           scanned, pf);
+      } else {
+        cull_scan<false, F>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
+                            scanned, pf);
+      }
+    };
+    if (a.seg_filter && a.tr.seg_f)
+      scan(std::true_type{});
+    else
+      scan(std::false_type{});
     if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
       atomicAdd(&a.io.counters[0], (unsigned long long)tested);
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);

@@ -315,6 +315,35 @@ def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
         assert torch.equal(ob, oc) and torch.equal(rb, rc) and torch.equal(db, dc), t
 
 
+@pytest.mark.parametrize("n_agents,N", [(1, 1536), (1, 8256), (2, 512)])
+def test_segment_prefilter_is_exact(rx, golden, monkeypatch, n_agents, N):
+    """The float32 segment pre-filter (seg_may_hit) only skips exact segment
+    tests that cannot report a hit: with (RX_SEG_FILTER=1, the default) and
+    without it, obs, rewards and dones are bit-identical over 300 steps of
+    random play (both culled; culled == brute force is checked above).  8,256
+    envs run the split step (k_step2), fewer the one-kernel path (k_rays)."""
+    tracks = np.arange(N) % golden.n_tracks
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step")
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step")
+    monkeypatch.setenv("RX_SEG_FILTER", "0")
+    ra0 = va.reset_device().clone()
+    monkeypatch.setenv("RX_SEG_FILTER", "1")
+    assert torch.equal(ra0, vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(12)
+    shape = (N, 2) if n_agents == 1 else (N, 2, 2)
+    for t in range(300):
+        a = torch.rand(shape, device="cuda", generator=g) * 2 - 1
+        if n_agents == 1:
+            a[:, 1].abs_()
+        monkeypatch.setenv("RX_SEG_FILTER", "0")
+        oa, ra, da = (x.clone() for x in va.step_device(a))
+        monkeypatch.setenv("RX_SEG_FILTER", "1")
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    va.close()
+    vb.close()
+
+
 def test_culled_raycast_on_golden_kats(rx, golden):
     """Track.raycast golden KATs (incl. no-hit, > 50 uncapped, grazing, far
     origins) through the culled kernel: sensor 5 (relative angle exactly 0)
