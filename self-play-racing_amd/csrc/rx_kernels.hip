@@ -948,18 +948,15 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   Car c[2];
   uint8_t fl[2];
   double last_steering[2];
-  double csr[2][2];  // REWARD: cos / sin of each stepped car's angle (KIN's cs_scratch)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int i = 2 * p + q;
     fl[q] = S.flags[i];
-    c[q] = Car{S.x[i], S.y[i], S.angle[i], S.vx[i], S.vy[i], S.progress[i], (fl[q] & RX_F_CRASHED) != 0};
+    // REWARD needs no angle, and loads the velocity only after the argmins
+    // (fewer live registers through them: k_step2<2> runs at 80 VGPRs)
+    c[q] = REW ? Car{S.x[i], S.y[i], 0.0, 0.0, 0.0, S.progress[i], (fl[q] & RX_F_CRASHED) != 0}
+               : Car{S.x[i], S.y[i], S.angle[i], S.vx[i], S.vy[i], S.progress[i], (fl[q] & RX_F_CRASHED) != 0};
     last_steering[q] = REW ? 0.0 : S.last_steering[i];
-    if (REW) {
-      const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[i];
-      csr[q][0] = sc.x;
-      csr[q][1] = sc.y;
-    }
   }
   bool do_reset;
   if (REW)
@@ -991,7 +988,8 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // multi_racing_env.py:215-220
       mv[q] = !c[q].crashed;
-      if (!REW) {
+      if (REW) continue;  // REWARD: corners per car in its argmin pass below
+      {
         last_steering[q] = (double)clipf(av[2 * q], -1.0f, 1.0f);
         const float thr = clipf((av[2 * q + 1] + 1.0f) / 2.0f, 0.0f, 1.0f);
         if (mv[q]) {
@@ -1001,11 +999,47 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
           have_sc[q] = true;
           if (KIN) reinterpret_cast<double2*>(a.cs_scratch)[2 * p + q] = make_double2(cs[q][0], cs[q][1]);
         }
-      } else if (mv[q]) {  // car.py:26-43 of the stepped pose
-        corners(c[q].x, c[q].y, csr[q][0], csr[q][1], cx[q], cy[q]);
       }
     }
-    if (!KIN && (mv[0] || mv[1])) {
+    if (REW && (mv[0] || mv[1])) {
+      // one pass per car (as FULL's culled passes below): corners of the stepped
+      // pose (car.py:26-43, KIN's cos / sin), the 5 closest waypoints, wall
+      // collision; only this car's corners are live during its pass
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (!__any(mv[q])) continue;
+        const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[2 * p + q];
+        double px[5], py[5];
+        px[0] = c[q].x;
+        py[0] = c[q].y;
+        corners(c[q].x, c[q].y, sc.x, sc.y, px + 1, py + 1);
+        int idx[5];
+        if (a.cull_chunk > 0) {
+          const int prev[1] = {prev_waypoint(c[q].progress, W)};
+          const double ccx[1] = {c[q].x}, ccy[1] = {c[q].y};
+          argmin_culled<5, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
+                              a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, ccx, ccy,
+                              a.argmin_window, idx, a.io.counters, nullptr, mv[q]);
+        } else {
+          argmin_pts<5>(wp, W, px, py, idx);
+        }
+        if (mv[q]) {
+          c[q].progress = (double)idx[0] / (double)W;
+          bool out = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) out = out || corner_out(wp, nrm, idx[1 + j], px[1 + j], py[1 + j], width);
+          c[q].crashed = out;
+        }
+      }
+    }
+    if (REW) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        c[q].vx = S.vx[2 * p + q];
+        c[q].vy = S.vy[2 * p + q];
+      }
+    }
+    if (FULL && (mv[0] || mv[1])) {
       double px[10], py[10];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {

@@ -1,6 +1,7 @@
 """Build librx.so from another git revision's sources, for same-session A/B runs.
 
-    python tools/build_rev.py REV NAME     -> self-play-racing_amd/rx/lib/librx_NAME.so
+    python tools/build_rev.py REV NAME [-DFLAG=V ...]  -> self-play-racing_amd/rx/lib/librx_NAME.so
+    (REV "." = the working tree; extra arguments are added to the hipcc flags)
     RX_LIB_PATH=.../librx_NAME.so python bench.py ...   (on the GPU box)
 
 Only the C/HIP sources and headers are taken from REV; the Python side must
@@ -23,12 +24,15 @@ def main():
     inc = os.path.join(tmp, "include")
     os.makedirs(csrc)
     os.makedirs(inc)
+    def read(path):
+        if rev == ".":
+            return open(os.path.join(ROOT, path), "rb").read()
+        return subprocess.check_output(["git", "-C", ROOT, "show", f"{rev}:{path}"])
     for f in _build.SOURCES + _build.HEADERS:
-        data = subprocess.check_output(["git", "-C", ROOT, "show", f"{rev}:self-play-racing_amd/csrc/{f}"])
-        open(os.path.join(csrc, f), "wb").write(data)
-    open(os.path.join(inc, "rx.h"), "wb").write(subprocess.check_output(["git", "-C", ROOT, "show", f"{rev}:include/rx.h"]))
+        open(os.path.join(csrc, f), "wb").write(read(f"self-play-racing_amd/csrc/{f}"))
+    open(os.path.join(inc, "rx.h"), "wb").write(read("include/rx.h"))
     out = os.path.join(_build.LIBDIR, f"librx_{name}.so")
-    flags = [x for x in _build.FLAGS if not x.startswith("-I")] + ["-I" + csrc, "-I" + inc]
+    flags = [x for x in _build.FLAGS if not x.startswith("-I")] + ["-I" + csrc, "-I" + inc] + sys.argv[3:]
     objs = []
     for src in _build.SOURCES:
         obj = os.path.join(tmp, os.path.splitext(src)[0] + ".o")
