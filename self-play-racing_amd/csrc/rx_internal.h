@@ -55,9 +55,12 @@ struct rx_track_view {
 
 // lanes per env in k_dyn1 (a dynamics wave holds 64 / lpe envs): 4 when there
 // are few envs (latency-bound: more lanes per env shorten the chain), 1 when
-// the chip is full (issue-bound: the replicated dynamics would cost more)
+// the chip is fuller.  One lane per env also selects the split step (k_kin1 +
+// k_step2: the REWARD half beside the raycast), which beats k_dyn1<4> + k_rays
+// from 4,096 envs on (41.4 vs 52.8 us at 4,096, 42.7 vs 54.3 at 8,192; equal
+// at 2,048, where the wide kernels run anyway: tools/gpu_lpe_ab.sh)
 #define RX_DYN1_LPE_SMALL 4
-#define RX_DYN1_SMALL_N 8192
+#define RX_DYN1_SMALL_N 2048
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them

@@ -405,9 +405,10 @@ def test_ray_major_two_car_is_exact(rx, golden, order):
 
 
 def test_dyn_lanes_per_env_paths_agree(rx, golden):
-    """k_dyn1 runs 4 lanes per env below 8,192 envs and 1 above: envs are
-    independent, so the first envs of a large vector env must step exactly
-    like a small one with the same tracks and actions."""
+    """Small vector envs run the wide kernels (<= 2,048 envs), larger ones the
+    split step at one lane per env: envs are independent, so the first envs of
+    a large vector env must step exactly like a small one with the same tracks
+    and actions."""
     n_small, n_big = 1024, 8256
     tracks = np.arange(n_big) % golden.n_tracks
     big = _venv(rx, golden, tracks, autoreset="next_step")
