@@ -37,7 +37,10 @@ using rx_policy::kH;   // hidden width (agent/ppo.py:20-29)
 using rx_policy::kNA;  // action dims
 constexpr int kT = 256;      // threads per workgroup (4 waves)
 constexpr int kRP = 64;      // rows per workgroup pass (16 per wave)
-constexpr int kMaxWG = 256;  // row workgroups per minibatch and trunk (rows per workgroup grow beyond that)
+#ifndef RX_PPO_MAXWG
+#define RX_PPO_MAXWG 256
+#endif
+constexpr int kMaxWG = RX_PPO_MAXWG;  // row workgroups per minibatch and trunk (rows per workgroup grow beyond that)
 constexpr int kWS = 68;      // LDS row stride of W2 [o][i] (float4-aligned; transposed reads conflict-free)
 constexpr int kTS = 66;      // LDS row stride of the [hidden][row] transposes (operand reads conflict-free)
 #ifndef RX_PPO_MINW

@@ -10,7 +10,7 @@ for rep in 1 2; do
 for set in "${SETS[@]}"; do
   IFS='|' read -r label lib args <<< "$set"
   libpath=""; [ -n "$lib" ] && libpath=$LIBDIR/librx_$lib.so
-  RX_LIB_PATH=$libpath timeout -k 10 200 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 $args > $OUT/ab_$label.log 2>&1 || { tail -20 $OUT/ab_$label.log; exit 1; }
+  RX_LIB_PATH=$libpath timeout -k 10 200 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 --no-time-to-90 $args > $OUT/ab_$label.log 2>&1 || { tail -20 $OUT/ab_$label.log; exit 1; }
   tail -1 $OUT/ab_$label.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$label', round(d['value']/1e6,1), d['kernels_ms'])"
 done
 done
