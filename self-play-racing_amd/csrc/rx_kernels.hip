@@ -1826,8 +1826,35 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
   }
   const rx_slot_lds sl{reinterpret_cast<const double2*>(sSlot + 2 * W),
                        reinterpret_cast<const double2*>(sSlot + 2 * W) + W, sSlot};
+  // The env's working-state row, KIN's cos / sin and its observation row live
+  // in LDS for the whole rollout (read back at the end): the device functions
+  // index state by position p = pos and obs by env id e, so they get pointers
+  // offset by -pos / -e*D into LDS (generic addressing) and every per-step
+  // state round trip is an LDS access instead of an L2 / HBM one.  The obs row
+  // is copied to the rollout buffer once per step, off the critical path.
+  __shared__ double sStD[9];   // x, y, angle, vx, vy, progress, last_progress, last_steering, ep_return
+  __shared__ double2 sCs;      // KIN -> REWARD: cos / sin of the stepped angle
+  __shared__ int32_t sStI[3];  // finished_step, steps, ep_length
+  __shared__ uint8_t sStB[2];  // flags, env_flags
+  __shared__ float sObs[D];
+  const rx_state& G = a.st;
+  if (threadIdx.x == 0) {
+    sStD[0] = G.x[pos], sStD[1] = G.y[pos], sStD[2] = G.angle[pos], sStD[3] = G.vx[pos], sStD[4] = G.vy[pos];
+    sStD[5] = G.progress[pos], sStD[6] = G.last_progress[pos], sStD[7] = G.last_steering[pos];
+    sStD[8] = G.ep_return[pos];
+    sStI[0] = G.finished_step ? G.finished_step[pos] : -1;
+    sStI[1] = G.steps[pos], sStI[2] = G.ep_length[pos];
+    sStB[0] = G.flags[pos], sStB[1] = G.env_flags[pos];
+  }
   __syncthreads();
   rx_kargs at = a;
+  at.st.x = sStD + 0 - pos, at.st.y = sStD + 1 - pos, at.st.angle = sStD + 2 - pos, at.st.vx = sStD + 3 - pos;
+  at.st.vy = sStD + 4 - pos, at.st.progress = sStD + 5 - pos, at.st.last_progress = sStD + 6 - pos;
+  at.st.last_steering = sStD + 7 - pos, at.st.ep_return = sStD + 8 - pos;
+  at.st.finished_step = G.finished_step ? sStI + 0 - pos : nullptr;
+  at.st.steps = sStI + 1 - pos, at.st.ep_length = sStI + 2 - pos;
+  at.st.flags = sStB + 0 - pos, at.st.env_flags = sStB + 1 - pos;
+  at.cs_scratch = reinterpret_cast<double*>(&sCs) - 2 * (ptrdiff_t)pos;
   // next-step / no autoreset: the split step's KIN / REWARD halves (as k_kin1 /
   // k_step2), so the argmins and the reward run beside the 11 raycast waves
   const bool split = a.autoreset != RX_AUTORESET_SAME_STEP;
@@ -1843,7 +1870,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     const int64_t row = (int64_t)t * n + e;
     if (w < 2) {  // ---- policy (k_policy_act's operations, one row)
       const int tr = w;  // 0 = actor, 1 = critic
-      if (lane < D) sX[tr][lane] = r.obs[row * D + lane];
+      if (lane < D) sX[tr][lane] = t == 0 ? r.obs[row * D + lane] : sObs[lane];
       wave_sync();
       // k_policy_act's MFMA chains (rx_ppo.hip): inputs d = 0 .. D-1 then the
       // zero padding to a multiple of 4; hidden units in the order t, r, q
@@ -1895,7 +1922,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     __syncthreads();  // actions[t] -> the dynamics wave
     if (w == 0) RX_RSTAMP(1);
     at.io.actions = r.actions + (size_t)t * n * NA;
-    at.io.obs = last ? r.next_obs : r.obs + (size_t)(t + 1) * n * D;
+    at.io.obs = sObs - (ptrdiff_t)e * D;  // obs[t+1] row in LDS, copied out below
     at.io.reward = r.rewards + (size_t)t * n;
     at.io.done_f32 = last ? r.next_done : r.dones + (size_t)(t + 1) * n;
     double ang[1], ep[3] = {0.0, 0.0, 0.0};
@@ -1921,7 +1948,17 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
       for (int ray = w; ray < a.n_sensors; ray += kRollWaves) ray_wide<1>(at, pos, ray, sl.seg);
     }
     __syncthreads();  // obs[t+1] complete before the next policy step
+    if (w == 2 && lane < D) (last ? r.next_obs : r.obs + (size_t)(t + 1) * n * D)[(size_t)e * D + lane] = sObs[lane];
     if (w == 0) RX_RSTAMP(3);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the working state back to HBM
+    G.x[pos] = sStD[0], G.y[pos] = sStD[1], G.angle[pos] = sStD[2], G.vx[pos] = sStD[3], G.vy[pos] = sStD[4];
+    G.progress[pos] = sStD[5], G.last_progress[pos] = sStD[6], G.last_steering[pos] = sStD[7];
+    G.ep_return[pos] = sStD[8];
+    if (G.finished_step) G.finished_step[pos] = sStI[0];
+    G.steps[pos] = sStI[1], G.ep_length[pos] = sStI[2];
+    G.flags[pos] = sStB[0], G.env_flags[pos] = sStB[1];
   }
 }
 

@@ -12,7 +12,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
 sys.path.insert(0, ROOT)
-LIB = os.path.join(ROOT, "self-play-racing_amd", "rx", "lib", "librx_rstamps.so")
+LIB = os.environ.get("RSTAMPS_LIB") or os.path.join(ROOT, "self-play-racing_amd", "rx", "lib", "librx_rstamps.so")
 if not os.path.exists(LIB):
     from rx import _build
     _build.build(out=LIB, defines=["RX_ROLL_STAMPS"], verbose=False)
