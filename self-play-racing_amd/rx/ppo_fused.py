@@ -137,10 +137,16 @@ class PolicyAct:
                              f"stride, got {tuple(t.shape)} / {t.stride()}")
         return t.stride(0)
 
-    def __call__(self, obs, actions_out, logprobs_out=None, values_out=None, stream=None):
+    def __call__(self, obs, actions_out, logprobs_out=None, values_out=None, stream=None, eps=None):
+        """``eps``: a caller-drawn float32 [n, 2] N(0, 1) block (e.g. one slice of
+        a rollout's noise drawn up front); default: draw into the own buffer."""
         lp = self._lp if logprobs_out is None else logprobs_out
         val = self._val if values_out is None else values_out
-        key = (obs.data_ptr(), actions_out.data_ptr(), lp.data_ptr(), val.data_ptr())
+        if eps is not None and (tuple(eps.shape) != (self.n, 2) or eps.dtype != torch.float32
+                                or not eps.is_contiguous()):
+            raise ValueError("rx_policy_act: eps must be a contiguous float32 [n, 2] block")
+        e = self.eps if eps is None else eps
+        key = (obs.data_ptr(), actions_out.data_ptr(), lp.data_ptr(), val.data_ptr(), e.data_ptr())
         io = self._io_cache.get(key) if self._io_cache.get("shapes") == (obs.shape, obs.stride(),
                                                                          actions_out.stride()) else None
         if io is None:  # validate once per buffer set (a rollout reuses the same rows every update)
@@ -153,10 +159,11 @@ class PolicyAct:
                 self._io_cache.clear()
             self._io_cache["shapes"] = (obs.shape, obs.stride(), actions_out.stride())
             io = self._io_cache[key] = _lib.RxPolicyIO(
-                self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(self.eps), _lib.ptr(self.flat.flat_param),
+                self.obs_dim, self.n, _lib.view_ptr(obs), _lib.ptr(e), _lib.ptr(self.flat.flat_param),
                 _lib.ptr(self.agent.log_std), _lib.view_ptr(actions_out), _lib.ptr(lp), _lib.ptr(val), os_, as_,
                 self.prec)
-        self.eps.normal_()
+        if eps is None:
+            self.eps.normal_()
         _lib.check(self.L.rx_policy_act(io, _lib.stream_ptr(stream)), "rx_policy_act")
         return actions_out
 
