@@ -515,12 +515,10 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       h->sort_on = true;
     }
   }
-  if (h->cfg.ray_order == 2) {  // task ids before the first k_dyn: (agent, ray) minor within each env
+  if (h->cfg.ray_order == 2) {  // task ids before the first sort: position-major, (agent, ray) minor -- a valid order
     const size_t nt = (size_t)N * A * R;
     std::vector<int32_t> t0(nt);
-    size_t o = 0;
-    for (int i = 0; i < N; ++i)
-      for (int qr = 0; qr < A * R; ++qr) t0[o++] = perm[i] * A * R + qr;
+    for (size_t o = 0; o < nt; ++o) t0[o] = (int32_t)o;  // task id (A*p + q)*R + r at slot p*A*R + q*R + r
     if ((rc = upload(h->tasks, t0.data(), nt))) return rc;
   }
   {
