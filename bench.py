@@ -12,7 +12,7 @@ one env step of every env (random actions + rx_step) through ONE env handle
 on one stream -- the configuration the PPO rollout uses, and the one whose
 per-launch kernel timing the roofline is computed from.  --stream-groups G
 steps the envs as G independent groups on G HIP streams instead (as an
-asynchronous rollout would); the JSON also reports that throughput for G = 4
+asynchronous rollout would); the JSON also reports that throughput for G = 2
 as "async_stream_groups", timed after the main region, and PPO training
 throughput ("ppo_train": rollout + GAE + the 10 x 16 minibatch update, 4,096
 envs per GPU; at N GPUs the update all-reduces one gradient+KL bucket per
@@ -316,7 +316,7 @@ def main():
     ap.add_argument("--cull-super", type=int, default=8, help="chunks per super-chunk box (0 = one-level culling)")
     ap.add_argument("--stream-groups", type=int, default=1,
                     help="independent env groups, one HIP stream each (1 = one handle on one stream)")
-    ap.add_argument("--async-probe-groups", type=int, default=4,
+    ap.add_argument("--async-probe-groups", type=int, default=2,
                     help="after the timed region, also time the same workload as this many stream groups "
                          "(reported as 'async_stream_groups'; 0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=128,
@@ -376,7 +376,9 @@ def main():
                                 sort_interval=args.sort_interval, ray_order=args.ray_order,
                                 cull_super=args.cull_super)
                 for g in range(G)]
-        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(G - 1)]
+        # several groups: every group on a stream of its own (torch's current stream is the
+        # null stream, which would serialise against the others)
+        streams = [torch.cuda.current_stream(dev)] if G == 1 else [torch.cuda.Stream(device=dev) for _ in range(G)]
         # synthetic inputs resident in HBM before the timed region: a bank of uniform random
         # actions (steer ~ U(-1, 1), throttle ~ U(0, 1)), one [n, 2] slice per step, cycled
         # when the run is longer than the bank (<= 512 MB per GPU)
