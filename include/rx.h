@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 15
+#define RX_ABI_VERSION 16
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -362,6 +362,13 @@ int rx_ppo_adv_finalize(const double* moments, int32_t n_mb, int64_t count, floa
 int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, float* ws_f32, double* ws_f64,
                                 float* grad, float* kl_out, const uint8_t* stop, void* stream);
 int rx_ppo_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, void* stream);
+
+/* ABI v16.  The minibatch shuffle of PPO.ppo_update (agent/ppo.py:165-171,
+ * np.random.shuffle(b_inds)) on the device, for config shuffle = "device": out
+ * [n] int64 receives a pseudo-random permutation of 0 .. n-1 keyed by seed
+ * (4-round Feistel network, cycle-walked to [0, n)); one launch, no host
+ * round trip.  Same seed, same permutation. */
+int rx_random_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream);
 
 /* Rollout policy step (agent/ppo.py:105-110: agent.get_action_and_value(obs)
  * under no_grad) for the same policy layout: per row, actor + critic forward,

@@ -998,6 +998,14 @@ int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, f
   return RX_OK;
 }
 
+int rx_random_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream) {
+  if (n < 0 || n > (1ll << 62)) return fail(RX_EINVAL, "rx_random_permutation: n = %lld out of range", (long long)n);
+  if (n > 0 && !out) return fail(RX_EINVAL, "rx_random_permutation: null output");
+  const int rc = rx_launch_permutation(n, seed, out, (hipStream_t)stream);
+  if (rc) return fail(RX_EHIP, "rx_random_permutation launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
 int rx_ppo_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, void* stream) {
   if (!kl || !stop || !kl_at_stop) return fail(RX_EINVAL, "rx_ppo_kl_check: null buffer");
   const int rc = rx_launch_kl_check(kl, kl_target, stop, kl_at_stop, (hipStream_t)stream);

@@ -144,5 +144,6 @@ extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* 
 extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
                             int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
                             hipStream_t s);
+extern "C" int rx_launch_permutation(int64_t n, uint64_t seed, int64_t* out, hipStream_t s);
 extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const int32_t* perm, int n, int A,
                              int to_user, hipStream_t s);

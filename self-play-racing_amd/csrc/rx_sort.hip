@@ -149,6 +149,36 @@ __global__ __launch_bounds__(kBlock) void k_state_sync(int n, const int32_t* __r
     move_row<A>(user, e, work, p);
 }
 
+// rx_random_permutation: a pseudo-random permutation of [0, n) in one
+// launch (the device minibatch shuffle, config["shuffle"] = "device").  A
+// 4-round balanced Feistel network on 2h bits (2^(2h) >= n) is a bijection of
+// [0, 2^(2h)); cycle-walking (apply it again while the value is >= n) turns it
+// into a bijection of [0, n), at most 4 walks on average since 2^(2h) < 4n.
+// Round function: the splitmix64 finalizer of (half ^ round key).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(kBlock) void k_feistel_perm(int64_t n, int h, uint64_t seed, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t mask = (1ull << h) - 1ull;
+  uint64_t x = (uint64_t)i;
+  do {
+    uint64_t l = x >> h, r = x & mask;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t f = mix64(r ^ mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1))) & mask;
+      const uint64_t t = l ^ f;
+      l = r;
+      r = t;
+    }
+    x = (l << h) | r;
+  } while (x >= (uint64_t)n);
+  out[i] = (int64_t)x;
+}
+
 }  // namespace
 
 extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
@@ -180,5 +210,15 @@ extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const i
     hipLaunchKernelGGL(k_state_sync<1>, dim3(grid), dim3(kBlock), 0, s, n, perm, *work, *user, to_user);
   else
     hipLaunchKernelGGL(k_state_sync<2>, dim3(grid), dim3(kBlock), 0, s, n, perm, *work, *user, to_user);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_permutation(int64_t n, uint64_t seed, int64_t* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  int bits = 1;
+  while (bits < 62 && (1ll << bits) < n) ++bits;
+  const int h = (bits + 1) / 2;  // 2h >= bits, so 2^(2h) >= n and < 4n (cycle-walk length)
+  const int64_t grid = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_feistel_perm, dim3((unsigned)grid), dim3(kBlock), 0, s, n, h, seed, out);
   return (int)hipGetLastError();
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -28,7 +28,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_assign", "rx_bind_state", "rx_set_speed_weight", "rx_reset", "rx_step", "rx_step_phases", "rx_gae",
            "rx_gae_scan", "rx_adam_workspace_floats", "rx_adam_clip_step", "rx_ppo_n_params", "rx_ppo_workspace_floats",
            "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act",
-           "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check",
+           "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
@@ -142,6 +142,7 @@ def load(build_if_missing=True):
     L.rx_ppo_minibatch_grad_shard.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, ctypes.c_float, _P, _P, _P,
                                               _P, _P, _P]
     L.rx_ppo_kl_check.argtypes = [_P, ctypes.c_float, _P, _P, _P]
+    L.rx_random_permutation.argtypes = [ctypes.c_int64, ctypes.c_uint64, _P, _P]
     L.rx_ppo_update_workspace_floats.argtypes = [ctypes.c_int32, ctypes.POINTER(RxAdamConfig)]
     L.rx_ppo_update_workspace_floats.restype = ctypes.c_size_t
     L.rx_ppo_minibatch_update.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, ctypes.POINTER(RxAdamConfig)] + \

@@ -34,6 +34,7 @@ import torch
 import torch.nn as nn
 import torch.optim as optim
 
+from . import _lib
 from . import dist as rdist
 from .agent import Agent
 from .gae import compute_gae
@@ -412,6 +413,17 @@ class PPO:
         graphs[key] = ent
         return ent
 
+    def _device_permutation(self, out):
+        """config["shuffle"] = "device": a pseudo-random permutation of the batch
+        rows written straight into ``out`` (int64 [B]) by rx_random_permutation
+        (Feistel network, include/rx.h), keyed by a draw from torch's CPU
+        generator (seeded from config["seed"]) mixed with the rank, so runs
+        repeat and data-parallel ranks shuffle independently."""
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) ^ (rdist.rank() * 0x9E3779B97F4A7C15 % 2 ** 64)
+        L = _lib.load()
+        _lib.check(L.rx_random_permutation(out.numel(), seed, _lib.ptr(out), _lib.stream_ptr(None)),
+                   "rx_random_permutation")
+
     def _update_epochs(self, b, fused, capture):
         c = self.config
         B, mb = b[0].shape[0], self._minibatch_size()
@@ -421,8 +433,8 @@ class PPO:
         nxt = None
         ent.stop.zero_()
         for epoch in range(c["update_epochs"]):
-            if device_shuffle:  # torch.randperm on the device: no host shuffle / H2D copy
-                torch.randperm(B, device=self.device, out=ent.perm)
+            if device_shuffle:  # rx_random_permutation: one launch, no host shuffle / H2D copy
+                self._device_permutation(ent.perm)
             else:
                 if nxt is None:
                     np.random.shuffle(b_inds)
