@@ -94,6 +94,7 @@ struct rx_env {
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   int32_t dyn_lpe = 1;
+  int32_t ray_lpr = 1;  // lanes per ray task (ray_order 2, not wide): 64 / ray_lpr tasks a ray wave
   int32_t argmin_window = 2;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -431,6 +432,16 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     const int v = atoi(ev);
     if (A == 1 && (v == 1 || v == 2 || v == 4 || v == 64)) h->dyn_lpe = v;
   }
+  // few envs: the culled raycast is a latency chain over too few waves to
+  // fill the chip, so 2 or 4 lanes share one ray and split its leaves
+  h->ray_lpr = 1;
+  if (h->cfg.ray_order == 2 && h->dyn_lpe != 64)
+    h->ray_lpr = (long long)N * A <= RX_RAY_LPR4_N ? 4 : ((long long)N * A <= RX_RAY_LPR2_N ? 2 : 1);
+  if (const char* ev = getenv("RX_RAY_LPR")) {  // A/B knob: 1, 2 or 4 lanes per ray
+    const int v = atoi(ev);
+    if ((v == 1 || v == 2 || v == 4) && h->cfg.ray_order == 2 && h->dyn_lpe != 64) h->ray_lpr = v;
+  }
+  const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
   int g0 = 0;
@@ -441,10 +452,10 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     const int ng = g1 - g0;
     const int epw = A == 1 ? 64 / h->dyn_lpe : 64;  // envs per dynamics wave
     for (int s = 0; s < ng; s += epw) dyn.push_back(rx_wave{k, g0 + s, 0, std::min(epw, ng - s)});
-    if (h->cfg.ray_order == 2) {  // per dynamics wave: its envs' A*R tasks (direction-sorted by k_dyn), 64 a wave
+    if (h->cfg.ray_order == 2) {  // per dynamics wave: its envs' A*R tasks (direction-sorted by k_dyn), tpw a wave
       for (int s = 0; s < ng; s += epw) {
         const int cnt = std::min(epw, ng - s), nt = cnt * A * R, ps = g0 + s;
-        for (int j = 0; j < nt; j += 64) ray.push_back(rx_wave{k, ps, ps * A * R + j, std::min(64, nt - j)});
+        for (int j = 0; j < nt; j += tpw) ray.push_back(rx_wave{k, ps, ps * A * R + j, std::min(tpw, nt - j)});
         ray_groups.push_back((int)ray.size());
       }
     } else if (h->cfg.ray_order == 0) {
@@ -645,6 +656,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.reset_count = h->resets.p;
   a.ray_order = h->cfg.ray_order;
   a.dyn_lpe = h->dyn_lpe;
+  a.ray_lpr = h->ray_lpr;
   a.argmin_window = h->argmin_window;
   a.slot_nenv = h->slot_n.p;
   a.wide = h->dyn_lpe == 64;

@@ -61,6 +61,16 @@ struct rx_track_view {
 // at 2,048, where the wide kernels run anyway: tools/gpu_lpe_ab.sh)
 #define RX_DYN1_LPE_SMALL 4
 #define RX_DYN1_SMALL_N 2048
+// Lanes per ray task (ray_order 2): 4 (16 tasks a ray wave) up to
+// RX_RAY_LPR4_N (env, agent) pairs, 2 up to RX_RAY_LPR2_N, 1 above: with few
+// envs the raycast is a latency chain over too few waves to fill the chip
+// ("Lanes per ray"; crossovers measured on MI355X)
+#ifndef RX_RAY_LPR4_N
+#define RX_RAY_LPR4_N 8192
+#endif
+#ifndef RX_RAY_LPR2_N
+#define RX_RAY_LPR2_N 16384
+#endif
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them
@@ -107,6 +117,7 @@ struct rx_kargs {
   uint32_t* reset_count;  // [N] (2-car envs), advanced by k_dyn2 at every reset
   int32_t box_quadrants;  // k_rays: single-quadrant waves use the quadrant-ordered box tables (RX_BOX_QUAD=0: off)
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
+  int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

@@ -1403,6 +1403,44 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
   for (; j < j1; ++j) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
 }
 
+// The four lanes of a quad (lanes 4i .. 4i+3) exchange a double: DPP
+// quad_perm [1,0,3,2] / [2,3,0,1] (every lane of the wave active).
+template <int CTRL>
+__device__ __forceinline__ double quad_dpp(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)u, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(u >> 32), (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// One scanned leaf's segments [j0, j1) for the lanes of a wave.  LPR = 1: each
+// lane tests all of them for its ray (ray_segments).  LPR = 2 or 4 (few envs:
+// the raycast is a latency chain, rx_assign): LPR adjacent lanes of a quad
+// hold the SAME ray and split the leaf (lane sub tests j0 + sub, j0 + sub +
+// LPR, ...), then take the minimum of their bests, so every lane goes on with
+// the ray's best -- the minimum over the leaf's exact hits, whoever tested
+// which segment.
+template <bool FILT, int LPR>
+__device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
+                                              double v3x, double v3y, double& best, float& bestf, const seg_pref& pf) {
+  if constexpr (LPR == 1) {
+    ray_segments<FILT>(seg, j0, j1, ox, oy, v3x, v3y, best, bestf, pf);
+  } else {
+    static_assert(LPR == 2 || LPR == 4, "2 or 4 lanes per ray");
+    const int sub = threadIdx.x & (LPR - 1);
+    for (int jb = j0; jb < j1; jb += LPR) {
+      const int j = jb + sub < j1 ? jb + sub : j0;
+      const double4 g = seg[j];
+      bool may = jb + sub < j1;
+      if constexpr (FILT) may = may && seg_may_hit(pf.segf[j], pf);
+      if (may) seg_test(g, ox, oy, v3x, v3y, best, bestf);
+    }
+    best = __builtin_fmin(best, quad_dpp<0xB1>(best));
+    if constexpr (LPR == 4) best = __builtin_fmin(best, quad_dpp<0x4E>(best));
+    bestf = f32_up(best);
+  }
+}
+
 // Chunk culling (exact; derivation in DESIGN.md §3).  The 2W boundary
 // segments of a slot are cut into chunks of G consecutive segments with
 // axis-aligned boxes of their end points.  A computed hit on segment j means
@@ -1465,7 +1503,7 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
 // `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far);
 // otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi).
-template <bool FAST, bool FILT>
+template <bool FAST, bool FILT, int LPR>
 __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
                                           int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
                                           double oy, double v3x, double v3y, double& best, float& bestf, int& tested,
@@ -1487,8 +1525,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (__any(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          ray_segments<FILT>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf,
-                             pf);
+          leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
+                                   bestf, pf);
         }
       }
     }
@@ -1518,15 +1556,15 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (__any(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          ray_segments<FILT>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best, bestf,
-                             pf);
+          leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
+                                   bestf, pf);
         }
       }
     }
   }
 }
 
-template <int A>
+template <int A, int LPR>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
   const rx_wave we = a.ray_waves[wave];
@@ -1536,9 +1574,16 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
   const int S_ = 2 * W;
   const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
-  if (lane >= we.count) return;
+  const int count = uniform(we.count);  // tasks of this wave (64 / LPR at most)
+  if (count <= 0) return;
+  // LPR lanes per task; lanes past the wave's tasks repeat its last one (their
+  // values equal that task's at every point, so no wave vote or minimum
+  // changes and every lane stays active for the quad exchanges); only the
+  // first lane of an own task writes
+  const int tl = lane / LPR;
+  const bool own = tl < count;
   const int R = a.n_sensors;
-  const int task = we.task_start + lane;
+  const int task = we.task_start + (own ? tl : count - 1);
   int env_local = 0, q, ray, pos;
   if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
     const int t = a.tasks[task];
@@ -1606,11 +1651,11 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
       if (a.box_quadrants && __all(quad == quad0)) {
         const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
         const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
-        cull_scan<true, F>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
-                           scanned, pf);
+        cull_scan<true, F, LPR>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf,
+                                tested, scanned, pf);
       } else {
-        cull_scan<false, F>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf, tested,
-                            scanned, pf);
+        cull_scan<false, F, LPR>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf,
+                                 tested, scanned, pf);
       }
     };
     if (a.seg_filter && a.tr.seg_f)
@@ -1622,7 +1667,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
   }
-  ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);
+  if (own && (lane & (LPR - 1)) == 0) ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);
 }
 
 // The observation of one ray from the wall minimum `best` (inf = no hit):
@@ -1665,7 +1710,12 @@ template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const unsigned long long prof_t0 = prof_start(a);
-  rays_body<A>(a, wave);
+  if (a.ray_lpr == 4)
+    rays_body<A, 4>(a, wave);
+  else if (a.ray_lpr == 2)
+    rays_body<A, 2>(a, wave);
+  else
+    rays_body<A, 1>(a, wave);
   prof_end(a, wave, prof_t0);
 }
 
@@ -1750,8 +1800,12 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     else
       dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
+  } else if (a.ray_lpr == 4) {
+    rays_body<A, 4>(a, b - n_rw);
+  } else if (a.ray_lpr == 2) {
+    rays_body<A, 2>(a, b - n_rw);
   } else {
-    rays_body<A>(a, b - n_rw);
+    rays_body<A, 1>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
 }

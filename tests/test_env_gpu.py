@@ -344,6 +344,34 @@ def test_segment_prefilter_is_exact(rx, golden, monkeypatch, n_agents, N):
     vb.close()
 
 
+@pytest.mark.parametrize("lpr", [2, 4])
+@pytest.mark.parametrize("n_agents,N", [(1, 1536), (1, 8256), (2, 512), (2, 3000)])
+def test_lanes_per_ray_are_exact(rx, golden, monkeypatch, n_agents, N, lpr):
+    """Two or four lanes per ray (RX_RAY_LPR: the lanes split each scanned
+    leaf and take the minimum of their bests; 4 is the default up to
+    RX_RAY_LPR4_N (env, agent) pairs) against one lane per ray: obs, rewards
+    and dones are bit-identical over 300 steps of random play.  Ragged sizes
+    leave partial ray waves (duplicate-task lanes); 8,256 envs run the split
+    step."""
+    tracks = np.arange(N) % golden.n_tracks
+    monkeypatch.setenv("RX_RAY_LPR", "1")
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step")
+    monkeypatch.setenv("RX_RAY_LPR", str(lpr))
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step")
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(13)
+    shape = (N, 2) if n_agents == 1 else (N, 2, 2)
+    for t in range(300):
+        a = torch.rand(shape, device="cuda", generator=g) * 2 - 1
+        if n_agents == 1:
+            a[:, 1].abs_()
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    va.close()
+    vb.close()
+
+
 def test_culled_raycast_on_golden_kats(rx, golden):
     """Track.raycast golden KATs (incl. no-hit, > 50 uncapped, grazing, far
     origins) through the culled kernel: sensor 5 (relative angle exactly 0)
