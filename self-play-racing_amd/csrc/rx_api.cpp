@@ -95,6 +95,7 @@ struct rx_env {
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   int32_t dyn_lpe = 1;
   int32_t ray_lpr = 1;  // lanes per ray task (ray_order 2, not wide): 64 / ray_lpr tasks a ray wave
+  int32_t reward_lpe = 1;  // split step, single-agent: lanes per env in k_step2's REWARD half
   int32_t argmin_window = 2;
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -441,6 +442,13 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     const int v = atoi(ev);
     if ((v == 1 || v == 2 || v == 4) && h->cfg.ray_order == 2 && h->dyn_lpe != 64) h->ray_lpr = v;
   }
+  // few single-agent envs: REWARD (a latency chain of argmins) outlasts the
+  // raycast beside it in k_step2 unless 2 lanes share an env's five points
+  h->reward_lpe = (A == 1 && N <= RX_REWARD_LPE2_N) ? 2 : 1;
+  if (const char* ev = getenv("RX_REWARD_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
+    const int v = atoi(ev);
+    if (v == 1 || v == 2 || v == 4) h->reward_lpe = v;
+  }
   const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
@@ -618,7 +626,7 @@ int rx_set_speed_weight(rx_env* h, double w) {
 static constexpr int kProfMax = 512;  // launches per record
 static int prof_stride(const rx_env* h) {
   const int wide = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;  // k_rays_wide: one wave per ray
-  return std::max((h->n_dyn_waves + 7) / 8 * 8 + h->n_ray_waves, wide) + 8;
+  return std::max(h->reward_lpe * ((h->n_dyn_waves + 7) / 8 * 8) + h->n_ray_waves, wide) + 8;
 }
 static void prof_arm(rx_env* h, rx_kargs& a, int kind) {
   a.prof_ts = nullptr;
@@ -657,6 +665,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.ray_order = h->cfg.ray_order;
   a.dyn_lpe = h->dyn_lpe;
   a.ray_lpr = h->ray_lpr;
+  a.reward_lpe = h->reward_lpe;
   a.argmin_window = h->argmin_window;
   a.slot_nenv = h->slot_n.p;
   a.wide = h->dyn_lpe == 64;

@@ -71,6 +71,12 @@ struct rx_track_view {
 #ifndef RX_RAY_LPR2_N
 #define RX_RAY_LPR2_N 16384
 #endif
+// k_step2<1>'s REWARD half at 2 lanes per env up to this many envs (it is the
+// launch's critical path there once the raycast runs at 4 lanes per ray;
+// from 8,192 envs on it only slows the raycast beside it)
+#ifndef RX_REWARD_LPE2_N
+#define RX_REWARD_LPE2_N 4096
+#endif
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them
@@ -118,6 +124,7 @@ struct rx_kargs {
   int32_t box_quadrants;  // k_rays: single-quadrant waves use the quadrant-ordered box tables (RX_BOX_QUAD=0: off)
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
   int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
+  int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

@@ -1771,9 +1771,6 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 // stepped positions k_kin1 wrote; the raycast reads them and, as an ordering
 // hint only, progress), so they run side by side: the latency-bound argmin
 // hides under the VALU-bound raycast.
-#ifndef RX_REWARD_LPE
-#define RX_REWARD_LPE 1  // lanes per env in the REWARD half (1 or 2: fewer argmin points per lane)
-#endif
 #ifndef RX_REWARD_PRIO
 #define RX_REWARD_PRIO 0
 #endif
@@ -1795,9 +1792,18 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
 #endif
     double ang[A], ep[3] = {0.0, 0.0, 0.0};
     int e = -1;
-    if constexpr (A == 1)
-      dyn1_env<RX_REWARD_LPE, RX_PART_REWARD>(a, b / RX_REWARD_LPE, ang, e, ep, b % RX_REWARD_LPE);
-    else
+    if constexpr (A == 1) {
+      // a.reward_lpe lanes per env (fewer argmin points per lane; few envs):
+      // block b = sub-block * n1 + dynamics wave, so a REWARD wave keeps the
+      // XCD (b % 8) of its k_kin1 wave (n1 = n_dyn_waves rounded up to 8)
+      const int n1 = n_rw / a.reward_lpe, w = b % n1, sb = b / n1;
+      if (a.reward_lpe == 4)
+        dyn1_env<4, RX_PART_REWARD>(a, w, ang, e, ep, sb);
+      else if (a.reward_lpe == 2)
+        dyn1_env<2, RX_PART_REWARD>(a, w, ang, e, ep, sb);
+      else
+        dyn1_env<1, RX_PART_REWARD>(a, w, ang, e, ep, 0);
+    } else
       dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
   } else if (a.ray_lpr == 4) {
@@ -2105,7 +2111,7 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
                          *a, n_rw2);
     return (int)hipGetLastError();
   }
-  const int n_rw = (a->n_dyn_waves * RX_REWARD_LPE + 7) / 8 * 8;
+  const int n_rw = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2

@@ -372,6 +372,35 @@ def test_lanes_per_ray_are_exact(rx, golden, monkeypatch, n_agents, N, lpr):
     vb.close()
 
 
+@pytest.mark.parametrize("lpe", [2, 4])
+@pytest.mark.parametrize("N", [4100, 8256])
+def test_reward_lanes_per_env_are_exact(rx, golden, monkeypatch, N, lpe):
+    """The split step's REWARD half at 2 or 4 lanes per env (RX_REWARD_LPE:
+    the five argmin points spread over the env's lanes, the wall test OR-ed
+    across them) against one lane per env: obs, rewards and dones
+    bit-identical over 300 steps of random play, episode counts exact (ragged last
+    dynamics wave at 4,100 envs; the episode-return sums only to f64
+    rounding, as their atomic order differs)."""
+    tracks = np.arange(N) % golden.n_tracks
+    monkeypatch.setenv("RX_REWARD_LPE", "1")
+    va = _venv(rx, golden, tracks, seed=6, autoreset="next_step")
+    monkeypatch.setenv("RX_REWARD_LPE", str(lpe))
+    vb = _venv(rx, golden, tracks, seed=6, autoreset="next_step")
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(14)
+    for t in range(300):
+        a = torch.rand((N, 2), device="cuda", generator=g) * 2 - 1
+        a[:, 1].abs_()
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    (ra_, la_, ca_), (rb_, lb_, cb_) = va.episode_stats(), vb.episode_stats()
+    assert ca_ == cb_ > 0 and la_ == lb_  # counts and (integer) lengths exact
+    assert abs(ra_ - rb_) <= 1e-9 * max(1.0, abs(ra_))  # f64 atomic sums: order differs across shards
+    va.close()
+    vb.close()
+
+
 def test_culled_raycast_on_golden_kats(rx, golden):
     """Track.raycast golden KATs (incl. no-hit, > 50 uncapped, grazing, far
     origins) through the culled kernel: sensor 5 (relative angle exactly 0)
