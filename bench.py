@@ -244,6 +244,47 @@ def time_to_90(configs):
             "runs": out}
 
 
+# Algorithmic flops of one minibatch row through k_ppo_grad (both trunks,
+# agent/ppo.py:11-62 + the backward of :183-203): forward 2(15*64 + 64*64 +
+# 64*n_out), backward dZ2 / dW3 2*64*n_out each, dW2 / dH1 2*64*64 each, dW1
+# 2*64*15; actor (n_out 2) 29,184 + critic (n_out 1) 28,800.
+PPO_GRAD_FLOP_PER_ROW = 57984
+FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X dense FP32 MFMA
+
+
+def ppo_grad_roofline(t, dev, reps=160):
+    """Live MFMA roofline of the PPO minibatch gradient: ``reps`` back-to-back
+    rx_ppo_minibatch_grad calls (k_ppo_grad + its split-K k_ppo_reduce) over
+    the last update's batch, bracketed by HIP events on the launch stream.
+    k_ppo_reduce is inside the timed launches, so ``frac`` is a lower bound
+    for k_ppo_grad alone (its rocprofv3 share: profiles/r02/ppo_prof_fp32_kernel_stats.csv)."""
+    ents = [e for e in t.__dict__.get("_upd_graphs", {}).values() if e.fused is not None]
+    if not ents:
+        return None
+    f = ents[-1].fused
+    stop = torch.zeros(1, dtype=torch.bool, device=dev)  # KL target 1e9: never raised
+    kl = torch.zeros(1, dtype=torch.float32, device=dev)
+    for m in range(f.n_mb):
+        f.grad(m, stop, kl)
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record(s)
+    for i in range(reps):
+        f.grad(i % f.n_mb, stop, kl)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    tf = PPO_GRAD_FLOP_PER_ROW * f.mb / (ms * 1e-3) / 1e12
+    prec = t.config.get("policy_dtype", "fp32")
+    return {"bound": "mfma", "kernel": "k_ppo_grad + k_ppo_reduce", "precision": prec,
+            "flop_per_row": PPO_GRAD_FLOP_PER_ROW, "rows_per_launch": f.mb, "avg_launch_ms": round(ms, 5),
+            "achieved": round(tf, 2), "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_MATRIX_PEAK_TFLOPS, 4),
+            "note": f"live HIP events over {reps} back-to-back minibatch gradient calls; includes k_ppo_reduce, "
+                    "so frac is a lower bound for k_ppo_grad alone"}
+
+
 def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
     """PPO training throughput (BASELINE.json configs[1] per GPU; configs[4]'s
     data-parallel update at N GPUs): rx.ppo.PPO on envs_per_gpu envs per rank,
@@ -288,8 +329,10 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
     B = T * n
     c = t.config
     n_mb = c["num_minibatches"]
+    grad_rf = ppo_grad_roofline(t, dev) if world == 1 else None
     t.envs.close()
     return {"value": round(B * updates / el, 1), "unit": "train env-steps/s", "updates": updates,
+            "grad_roofline": grad_rf,
             "ms_per_update": round(el / updates * 1e3, 3), "envs_per_gpu": envs_per_gpu, "global_envs": n,
             "num_steps": T, "batch": B, "epochs_x_minibatches": f"{c['update_epochs']}x{n_mb}",
             "update_path": "fused HIP (rx_ppo_minibatch_grad" + ("_shard + bucket all-reduce)" if world > 1 else ")"),

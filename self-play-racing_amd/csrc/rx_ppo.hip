@@ -289,26 +289,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   const rx_ppo_batch& b = a.b;
   const int t0 = threadIdx.x, lane = t0 & 63, l15 = lane & 15, q = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(t0 >> 6);
-  // ---- stage the trunk's weights (zero-padded rows)
-  for (int e = t0; e < 64 * G::DP; e += kT) {
-    const int o = e / G::DP, d = e - o * G::DP;
-    lds[S::W1 + e] = d < D ? W[oW1 + o * D + d] : 0.0f;
-  }
-  for (int e = t0; e < 64 * 64; e += kT) lds[S::W2 + (e >> 6) * kWS + (e & 63)] = W[oW2 + e];
-  for (int e = t0; e < 64; e += kT) {
-    lds[S::B1 + e] = W[ob1 + e];
-    lds[S::B2 + e] = W[ob2 + e];
-  }
-  for (int e = t0; e < NOUT * 64; e += kT) lds[S::W3 + e] = W[oW3 + e];
-  if (t0 < NOUT) lds[S::B3 + t0] = W[ob3 + t0];
-  __syncthreads();
-  const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
-  float* sZ = lds + S::SZ;  // [hidden][row]
-  float* sH = lds + S::SH;  // [hidden][row]
-  float* sX = lds + S::SX;  // [row][d]
-  float* sG = lds + S::SG;  // [row][j]
   const int rr = 16 * wv + l15;  // this lane's row within the pass
-
   const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
   const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
   const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
@@ -359,8 +340,29 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     }
     return in;
   };
+  // the first pass's row gathers are issued before the weight staging, so
+  // the two memory latencies overlap
   int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
   RowIn cur = load_row(src);
+  // ---- stage the trunk's weights (zero-padded rows)
+  for (int e = t0; e < 64 * G::DP; e += kT) {
+    const int o = e / G::DP, d = e - o * G::DP;
+    lds[S::W1 + e] = d < D ? W[oW1 + o * D + d] : 0.0f;
+  }
+  for (int e = t0; e < 64 * 64; e += kT) lds[S::W2 + (e >> 6) * kWS + (e & 63)] = W[oW2 + e];
+  for (int e = t0; e < 64; e += kT) {
+    lds[S::B1 + e] = W[ob1 + e];
+    lds[S::B2 + e] = W[ob2 + e];
+  }
+  for (int e = t0; e < NOUT * 64; e += kT) lds[S::W3 + e] = W[oW3 + e];
+  if (t0 < NOUT) lds[S::B3 + t0] = W[ob3 + t0];
+  __syncthreads();
+  const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
+  float* sZ = lds + S::SZ;  // [hidden][row]
+  float* sH = lds + S::SH;  // [hidden][row]
+  float* sX = lds + S::SX;  // [row][d]
+  float* sG = lds + S::SG;  // [row][j]
+
   for (int64_t base = row0; base < row_end; base += kRP) {
     // ================================================================ A
     const int64_t src_nn = src_of(base + 2 * kRP);
@@ -710,16 +712,32 @@ __device__ __forceinline__ void adv_write(double a, double q, double count, floa
   stats[2 * i + 1] = (float)sqrt(var);
 }
 
+constexpr int kAdvBatch = 16;  // k_adv_stats rows in flight per thread
+
 __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ adv, const int64_t* __restrict__ perm,
                                                     int mb, int64_t n_rows, float* stats, double* moments) {
   __shared__ double red[2][16];
   const int64_t base = (int64_t)blockIdx.x * mb;
   double s = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < mb; i += 1024) {
-    const int64_t k = perm[base + i];
-    const double x = (k >= 0 && k < n_rows) ? adv[k] : 0.0;
-    s += x;
-    s2 += x * x;
+  // thread t adds rows t, t + 1024, ... in order; the perm indices and then the
+  // gathered advantages of kAdvBatch rows are loaded before any is added, so a
+  // batch costs two memory round trips instead of two per row
+  for (int i0 = threadIdx.x; i0 < mb; i0 += 1024 * kAdvBatch) {
+    int64_t k[kAdvBatch];
+#pragma unroll
+    for (int j = 0; j < kAdvBatch; ++j) {
+      const int i = i0 + 1024 * j;
+      k[j] = i < mb ? perm[base + i] : -1;
+    }
+    double x[kAdvBatch];
+#pragma unroll
+    for (int j = 0; j < kAdvBatch; ++j) x[j] = (k[j] >= 0 && k[j] < n_rows) ? adv[k[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < kAdvBatch; ++j)
+      if (i0 + 1024 * j < mb) {
+        s += x[j];
+        s2 += x[j] * x[j];
+      }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o, 64);
