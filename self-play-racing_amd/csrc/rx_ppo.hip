@@ -616,7 +616,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
                                                      float kl_target, float scale, float* grad, uint8_t* stop,
                                                      float* kl_at_stop, float* kl_out, const norm_args* norm_p,
                                                      norm_args norm) {
-  if (*stop) return;
+  const bool stopped = *stop;  // tested after the partial loads are issued (one round trip, not two)
   __shared__ float4 red[kRedSlices][kRedCols];
   const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
   const int p4 = blockIdx.x * (4 * kRedCols) + c * 4;  // first of this thread's 4 parameters
@@ -638,6 +638,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
         s.w += v[k].w;
       }
     }
+  if (stopped) return;  // uniform: KL early stop already hit
   red[sl][c] = s;
   __syncthreads();
   // slices -> 8 groups (group q sums slices q, q+8, ...) -> column total, in order
