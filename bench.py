@@ -16,7 +16,8 @@ asynchronous rollout would); the JSON also reports that throughput for G = 2
 as "async_stream_groups", timed after the main region, and PPO training
 throughput ("ppo_train": rollout + GAE + the 10 x 16 minibatch update, 4,096
 envs per GPU; at N GPUs the update all-reduces one gradient+KL bucket per
-optimizer step over RCCL).  With N GPUs
+optimizer step over RCCL; "ppo_train_bf16" is the same leg with the bf16
+policy kernels, BASELINE configs[1] as named, at N = 1).  With N GPUs
 (torch.distributed.run, one rank per GPU) every rank owns 65,536 envs of a
 N*65,536-env pool (weak scaling, configs[4]); the env step has no collective.
 
@@ -250,6 +251,7 @@ def time_to_90(configs):
 # 2*64*15; actor (n_out 2) 29,184 + critic (n_out 1) 28,800.
 PPO_GRAD_FLOP_PER_ROW = 57984
 FP32_MATRIX_PEAK_TFLOPS = 157.3  # MI355X dense FP32 MFMA
+BF16_MATRIX_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (no sparsity)
 
 
 def ppo_grad_roofline(t, dev, reps=160):
@@ -277,15 +279,15 @@ def ppo_grad_roofline(t, dev, reps=160):
     ms = e0.elapsed_time(e1) / reps
     tf = PPO_GRAD_FLOP_PER_ROW * f.mb / (ms * 1e-3) / 1e12
     prec = t.config.get("policy_dtype", "fp32")
+    peak = BF16_MATRIX_PEAK_TFLOPS if prec == "bf16" else FP32_MATRIX_PEAK_TFLOPS
     return {"bound": "mfma", "kernel": "k_ppo_grad + k_ppo_reduce", "precision": prec,
             "flop_per_row": PPO_GRAD_FLOP_PER_ROW, "rows_per_launch": f.mb, "avg_launch_ms": round(ms, 5),
-            "achieved": round(tf, 2), "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / FP32_MATRIX_PEAK_TFLOPS, 4),
+            "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
             "note": f"live HIP events over {reps} back-to-back minibatch gradient calls; includes k_ppo_reduce, "
                     "so frac is a lower bound for k_ppo_grad alone"}
 
 
-def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
+def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dtype="fp32"):
     """PPO training throughput (BASELINE.json configs[1] per GPU; configs[4]'s
     data-parallel update at N GPUs): rx.ppo.PPO on envs_per_gpu envs per rank,
     each update = T-step rollout with the fused policy in the loop + GAE + the
@@ -298,7 +300,7 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates):
     from rx.ppo import PPO
     from rx.track import gen_tracks
     n = envs_per_gpu * world
-    cfg = base_config(num_envs=n, num_steps=T, kl_target=1e9, shuffle="device")
+    cfg = base_config(num_envs=n, num_steps=T, kl_target=1e9, shuffle="device", policy_dtype=policy_dtype)
     cfg["total_timesteps"] = (updates + 1) * cfg["batch_size"]
     random.seed(1)
     np.random.seed(1)
@@ -513,6 +515,10 @@ def main():
     gae = gae_roofline(E, dev) if rank == 0 else None
     ppo = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
                   args.ppo_updates) if args.ppo_updates > 0 else None
+    # BASELINE configs[1] is named "PPO bf16": the same leg with the bf16 policy kernels
+    # (bf16 MFMA operands, f32 accumulation, f32 master weights / Adam), at N = 1 only
+    ppo_bf16 = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
+                       args.ppo_updates, "bf16") if args.ppo_updates > 0 and world == 1 else None
     tt90 = None
     if world == 1 and not args.no_time_to_90:
         tt90 = time_to_90([(16, 2048, "numpy"), (4096, 128, "device")])
@@ -574,6 +580,7 @@ def main():
             "gae": gae,
             "async_stream_groups": async_probe,
             "ppo_train": ppo,
+            "ppo_train_bf16": ppo_bf16,
             "time_to_90": tt90,
         }
         if cpu is not None:

@@ -424,6 +424,33 @@ class PPO:
         _lib.check(L.rx_random_permutation(out.numel(), seed, _lib.ptr(out), _lib.stream_ptr(None)),
                    "rx_random_permutation")
 
+    def _update_epochs_async(self, ent, n_mb):
+        """Device shuffles on one rank: every epoch (permutation launch + epoch
+        graph) is enqueued without waiting for the previous one's KL verdict.
+        Once the device stop flag is up, every later launch of the update exits
+        at its flag test (k_ppo_grad / k_ppo_reduce / k_adam_apply), so the parameters, the Adam state and
+        the step count end exactly as with a host check after every epoch
+        (agent/ppo.py:178-182 breaks out of the epoch loop).  The stop epoch
+        comes from the optimizer steps taken (a stop in epoch e, minibatch m
+        leaves e * n_mb + m of them), and torch's CPU generator is rewound to
+        just after that epoch's seed draw, so the generator consumes exactly
+        what the per-epoch check would have (config["epoch_sync"] = True keeps
+        that synchronous loop).  One host sync per update instead of one per
+        epoch."""
+        E = self.config["update_epochs"]
+        steps0 = self._flat.step_t.clone()
+        rng = []
+        for _ in range(E):
+            rng.append(torch.get_rng_state())
+            self._device_permutation(ent.perm)
+            ent.run()
+        if bool(ent.stop.item()):
+            taken = int(round(float((self._flat.step_t - steps0).item())))
+            epoch = min(taken // n_mb, E - 1)
+            if epoch + 1 < E:
+                torch.set_rng_state(rng[epoch + 1])
+            self._early_stop_msg(epoch, float(ent.kl.item()))
+
     def _update_epochs(self, b, fused, capture):
         c = self.config
         B, mb = b[0].shape[0], self._minibatch_size()
@@ -432,6 +459,9 @@ class PPO:
         b_inds = np.arange(B)
         nxt = None
         ent.stop.zero_()
+        if device_shuffle and ent.fused is not None and rdist.world() == 1 and not c.get("epoch_sync", False):
+            self._update_epochs_async(ent, B // mb)
+            return
         for epoch in range(c["update_epochs"]):
             if device_shuffle:  # rx_random_permutation: one launch, no host shuffle / H2D copy
                 self._device_permutation(ent.perm)

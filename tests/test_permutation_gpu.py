@@ -71,3 +71,44 @@ def test_ppo_device_shuffle_uses_it(monkeypatch):
     adv, ret = p.compute_advantages(rewards, dones, values, nv, nd)
     p.ppo_update(adv, ret, values, logprobs, actions, obs)
     assert calls == [64 * 32] * cfg["update_epochs"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kl_target", [1e9, 0.02, 0.004, 1e-5])
+def test_async_epochs_equal_per_epoch_sync(kl_target, capsys):
+    """Device shuffles enqueue every epoch without a host KL check in between
+    (rx.ppo.PPO._update_epochs_async); parameters, Adam state, step count, the
+    early-stop message and torch's CPU generator must end exactly as with the
+    synchronous per-epoch check (config["epoch_sync"] = True)."""
+    from rx.configs import base_config
+    from rx.envs import RacingEnv
+    from rx.ppo import PPO
+    from rx.track import gen_tracks
+    out = {}
+    for sync in (True, False):
+        np.random.seed(1)
+        pool = gen_tracks(64, seed=1)
+        cfg = base_config(num_envs=64, num_steps=32, shuffle="device", kl_target=kl_target, epoch_sync=sync)
+        p = PPO(lambda i: RacingEnv(11, pool, i, 8), cfg)
+        bufs = p._buffers()
+        nobs = p.envs.buf["obs"].clone()
+        nd = torch.zeros(p.num_local_envs, device="cuda")
+        obs, actions, logprobs, dones, rewards, values, nobs, nd, _ = p.collect_rollout(*bufs, nobs, nd)
+        with torch.no_grad():
+            nv = p.agent.get_value(nobs).flatten()
+        adv, ret = p.compute_advantages(rewards, dones, values, nv, nd)
+        capsys.readouterr()
+        p.ppo_update(adv, ret, values, logprobs, actions, obs)
+        torch.cuda.synchronize()
+        f = p._flat
+        out[sync] = (f.flat_param.clone(), f.exp_avg.clone(), f.exp_avg_sq.clone(), float(f.step_t.item()),
+                     torch.get_rng_state().clone(), capsys.readouterr().out)
+        p.envs.close()
+    a, b = out[True], out[False]
+    for x, y in zip(a[:3], b[:3]):
+        assert torch.equal(x, y)
+    assert a[3] == b[3]
+    assert torch.equal(a[4], b[4])
+    assert a[5] == b[5]
+    if kl_target < 1e-4:
+        assert "Early stopping" in a[5]

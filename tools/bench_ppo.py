@@ -43,6 +43,8 @@ def main():
              kl_target=1e9,
              shuffle="device" if args.device_shuffle else "numpy")  # no early stop: time the full update
     cfg["total_timesteps"] = (args.updates + 1) * cfg["batch_size"]
+    if os.environ.get("EPOCH_SYNC") is not None:  # A/B: host KL check after every epoch (1) or one per update (0)
+        cfg["epoch_sync"] = os.environ["EPOCH_SYNC"] == "1"
     if os.environ.get("GRAPH_ROLLOUT") is not None:  # A/B: rollout as one captured HIP graph (1) or eager (0)
         cfg["graph_rollout"] = os.environ["GRAPH_ROLLOUT"] == "1"
     random.seed(1)
