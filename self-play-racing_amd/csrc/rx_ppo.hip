@@ -211,17 +211,19 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
 // per row  action = clamp(eps * std + mu, -1, 1)   (Normal.sample() = normal_() * std + mu)
 //          logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs).
 // eps [N][2] is drawn by the caller with torch's normal_() so the sampling
-// stream is torch's.  Wave = 16 rows of one trunk (even waves actor, odd
-// critic), weights straight from the (L2-resident) parameter buffer.
+// stream is torch's.  Wave = 16 rows of one trunk, weights straight from the
+// (L2-resident) parameter buffer.
 template <int D, int PREC>
 __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P) {
   using L = Lay<D>;
   constexpr int XN = Geo<D>::template XN<PREC>;
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
-  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (kT / 64) + (threadIdx.x >> 6));
-  const bool critic = gw & 1;
-  const int64_t row = (int64_t)(gw >> 1) * 16 + l15;
-  if ((int64_t)(gw >> 1) * 16 >= io.n) return;
+  // a workgroup's 4 waves run ONE trunk (even workgroups actor, odd critic) on
+  // 4 consecutive 16-row blocks, so a CU's L1 holds one trunk's 21 KB of weights
+  const bool critic = blockIdx.x & 1;
+  const int64_t rb = (int64_t)(blockIdx.x >> 1) * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row = rb * 16 + l15;
+  if (rb * 16 >= io.n) return;
   const bool live = row < io.n;
   const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
   float x[XN];
@@ -856,9 +858,9 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
 }
 
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
-  // one wave per 16 rows and trunk, 4 waves per workgroup
-  const int64_t waves = 2 * ((io->n + 15) / 16);
-  const int n_wg = (int)((waves + 3) / 4);
+  // one wave per 16 rows and trunk, 4 waves (one trunk) per workgroup
+  const int64_t blocks16 = (io->n + 15) / 16;
+  const int n_wg = (int)(2 * ((blocks16 + 3) / 4));
   const bool bf = io->precision == kBF16;
   if (io->obs_dim == 15) {
     if (bf)
