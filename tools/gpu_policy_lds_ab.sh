@@ -6,7 +6,7 @@ OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_ppo_fused_gpu.py tests/test_rollout_gpu.py tests/test_bf16_gpu.py tests/test_ppo_gpu.py tests/test_ppo_golden.py tests/test_eval_golden_gpu.py > $OUT/plds_pytest.log 2>&1; rc=$?
 tail -1 $OUT/plds_pytest.log; [ $rc -eq 0 ] || exit $rc
 LIBDIR=$(pwd)/self-play-racing_amd/rx/lib
-for rep in 1 2; do for lib in head tree; do
+for rep in 1 2; do for lib in ${LIBS:-head tree}; do
   RX_LIB_PATH=$LIBDIR/librx_$lib.so timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/plds_$lib -o run --output-format csv -- \
     python tools/bench_ppo.py --envs 4096 --steps 128 --device-shuffle --updates 2 > $OUT/plds_$lib.log 2>&1 || { tail -20 $OUT/plds_$lib.log; exit 1; }
   python - $lib $OUT/plds_$lib <<'PY'
@@ -19,7 +19,7 @@ print(sys.argv[1], "k_policy_act_us", round(float(pa["AverageNs"]) / 1e3, 2), "r
       "train_M", round(d["train_env_steps_per_s"] / 1e6, 2))
 PY
 done; done
-for rep in 1 2; do for lib in head tree; do
+for rep in 1 2; do for lib in ${LIBS:-head tree}; do
   RX_LIB_PATH=$LIBDIR/librx_$lib.so timeout -k 10 200 python tools/bench_ppo.py --mode selfplay --envs 8192 --steps 128 --device-shuffle --updates 2 > $OUT/plds_sp.log 2>&1 || { tail -20 $OUT/plds_sp.log; exit 1; }
   grep '^{' $OUT/plds_sp.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$lib selfplay rollout_ms', round(d['rollout_s']*1e3,3), 'train_M', round(d['train_env_steps_per_s']/1e6,2))"
 done; done
