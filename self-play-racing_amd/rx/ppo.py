@@ -440,16 +440,46 @@ class PPO:
         E = self.config["update_epochs"]
         steps0 = self._flat.step_t.clone()
         rng = []
-        for _ in range(E):
+        f = ent.fused
+        B = ent.perm.numel()
+        if ent.__dict__.get("perms") is None:
+            ent.perms = torch.empty((E, B), dtype=torch.int64, device=ent.perm.device)
+            ent.stats_all = torch.empty((E, f.n_mb, 2), dtype=torch.float32, device=ent.perm.device)
+        # every epoch's permutation up front (the same draws, in the same order),
+        # then the advantage statistics of all epochs in ONE launch
+        for e in range(E):
             rng.append(torch.get_rng_state())
-            self._device_permutation(ent.perm)
-            ent.run()
+            self._device_permutation(ent.perms[e])
+        f.epochs_stats(ent.perms, ent.stats_all)
+        run = self._epoch_nostats(ent)
+        for e in range(E):
+            ent.perm.copy_(ent.perms[e])
+            f.stats.copy_(ent.stats_all[e].reshape(-1))
+            run()
         if bool(ent.stop.item()):
             taken = int(round(float((self._flat.step_t - steps0).item())))
             epoch = min(taken // n_mb, E - 1)
             if epoch + 1 < E:
                 torch.set_rng_state(rng[epoch + 1])
             self._early_stop_msg(epoch, float(ent.kl.item()))
+
+    def _epoch_nostats(self, ent):
+        """The epoch's minibatch steps without its advantage-statistics launch
+        (the stats rows are copied in by _update_epochs_async), as a graph when
+        the epoch runner captures one."""
+        run = ent.__dict__.get("run_nostats")
+        if run is None:
+            if ent.graph is not None:
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(ent.perm.device)
+                with torch.cuda.graph(g):
+                    ent.fused.epoch(ent.stop, ent.kl, stats=False)
+                run = g.replay
+                ent.graph_nostats = g
+            else:
+                run = lambda: ent.fused.epoch(ent.stop, ent.kl, stats=False)  # noqa: E731
+            ent.run_nostats = run
+        return run
 
     def _update_epochs(self, b, fused, capture):
         c = self.config

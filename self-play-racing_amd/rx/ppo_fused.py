@@ -105,11 +105,37 @@ class FusedMinibatchGrad:
             _lib.ptr(f.flat_grad), _lib.ptr(f.exp_avg), _lib.ptr(f.exp_avg_sq), _lib.ptr(f.step_t), _lib.ptr(f.lr_t),
             _lib.ptr(stop), _lib.ptr(kl_at_stop), _lib.ptr(ws), _lib.stream_ptr(stream)), "rx_ppo_minibatch_update")
 
-    def epoch(self, stop, kl_at_stop):
-        """All minibatch steps of one epoch over the current perm."""
-        self.adv_stats()
+    def epoch(self, stop, kl_at_stop, stats=True):
+        """All minibatch steps of one epoch over the current perm (``stats``:
+        its advantage statistics first; False when the caller has already put
+        them in ``self.stats``, see epochs_stats)."""
+        if stats:
+            self.adv_stats()
         for m in range(self.n_mb):
             self.update(m, stop, kl_at_stop)
+
+    def epochs_stats(self, perms, stats_out, stream=None):
+        """Advantage statistics of E epochs in ONE rx_ppo_adv_stats launch:
+        ``perms`` int64 [E, B] (one permutation per epoch), ``stats_out``
+        float32 [E, n_mb, 2].  Workgroup e * n_mb + m sums minibatch m of epoch
+        e exactly as the per-epoch launch does (same rows, same order), so the
+        rows equal E separate launches bit for bit; E * n_mb workgroups keep
+        that many CUs gathering instead of n_mb.  The batch view addresses the
+        E * B indices (every index is still < B: they are permutations)."""
+        E, B = perms.shape
+        b = RxPPOBatch_copy(self.batch)
+        b.perm = _lib.ptr(perms)
+        b.n_rows = E * B
+        self._keep_epochs = (perms, stats_out)
+        _lib.check(self.L.rx_ppo_adv_stats(b, E * self.n_mb, _lib.ptr(stats_out), _lib.stream_ptr(stream)),
+                   "rx_ppo_adv_stats")
+
+
+def RxPPOBatch_copy(b):
+    c = _lib.RxPPOBatch()
+    for name, _ in _lib.RxPPOBatch._fields_:
+        setattr(c, name, getattr(b, name))
+    return c
 
 
 class PolicyAct:
