@@ -100,6 +100,18 @@ def compute_roofline(pmc, launch_ms):
     return res
 
 
+_MARKS = os.environ.get("RX_BENCH_MARKS") == "1"
+
+
+def mark(tag):
+    """Diagnostics (RX_BENCH_MARKS=1): host clocks at the edges of a timed region on
+    stderr, to line the region up with a rocprofv3 kernel trace (CLOCK_BOOTTIME
+    and CLOCK_MONOTONIC ns).  Outside the timed interval; changes nothing timed."""
+    if _MARKS:
+        print(f"RX_MARK {tag} boottime_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME)} "
+              f"monotonic_ns={time.monotonic_ns()}", file=sys.stderr, flush=True)
+
+
 def seed1_pool(n_total):
     """train.py:67-80 track pool for n_total envs (rx.track.gen_tracks == reference, memoised)."""
     from rx.track import gen_tracks
@@ -318,12 +330,15 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
     sync()
     gc.collect()
     gc.disable()
+    from rx import dist as rdist
+    ar0 = dict(rdist.COUNTS)
     t0 = time.perf_counter()
     for _ in range(updates):
         next(it)
     sync()
     gc.enable()
     el = time.perf_counter() - t0
+    ar = {k: (rdist.COUNTS[k] - ar0[k]) / updates for k in ar0}
     if dist:
         x = torch.tensor([el], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
@@ -338,9 +353,112 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
             "ms_per_update": round(el / updates * 1e3, 3), "envs_per_gpu": envs_per_gpu, "global_envs": n,
             "num_steps": T, "batch": B, "epochs_x_minibatches": f"{c['update_epochs']}x{n_mb}",
             "update_path": "fused HIP (rx_ppo_minibatch_grad" + ("_shard + bucket all-reduce)" if world > 1 else ")"),
-            "allreduce_per_update": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
+            "allreduce_per_update": ar["all_reduce"], "allreduce_bytes_per_update": ar["bytes"],
+            "allreduce_per_update_expected": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
             "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
             "note": "KL early stop off, device shuffles; timed after one warm-up update"}
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n, argv, poll_s=0.2):
+    """`python bench.py --gpus N` without an external launcher: start N fresh
+    rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1), one per GPU, exactly as `torch.distributed.run --nproc-per-node N`
+    would.  This parent never initialises HIP (it has only parsed arguments), and
+    it starts the ranks as children -- no exec.  Rank 0's JSON line is relayed
+    to this process's stdout; everything else the ranks print (library chatter
+    such as gloo's connection messages included) goes to stderr, so stdout
+    carries the one line.  If any rank fails, the others are terminated (their
+    own PIDs) and its exit code is returned."""
+    import subprocess
+    import threading
+    port = _free_port()
+    me = os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, me] + list(argv), env=env, text=True,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def relay(f):
+        for line in f:
+            (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            print(f"bench.py: a rank exited with {rc}; the others were stopped", file=sys.stderr, flush=True)
+            return rc if rc > 0 else 1
+        if all(c == 0 for c in codes):
+            th.join(timeout=30)
+            return 0
+        time.sleep(poll_s)
+
+
+def gather_dist_info(dist, backend, world, rank, local, dev):
+    """What the process group saw: backend, world size and per rank its host,
+    LOCAL_RANK, device ordinal and PCI location (all_gather_object), plus the
+    RCCL version for the nccl backend."""
+    me = {"rank": rank, "local_rank": local, "host": os.uname().nodename}
+    if dev is not None and torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(dev)
+        me.update(device=dev.index, name=p.name, gcn_arch=getattr(p, "gcnArchName", None),
+                  pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}")
+    else:
+        me.update(device="cpu")
+    allinfo = [None] * world
+    dist.all_gather_object(allinfo, me)
+    out = {"backend": backend, "world_size": world, "ranks": allinfo,
+           "distinct_devices": len({(i.get("host"), i.get("pci", i.get("device"))) for i in allinfo})}
+    if backend == "nccl":
+        try:
+            out["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:  # noqa: BLE001 -- informational only
+            out["rccl_version"] = None
+    return out
+
+
+def launch_selftest(args, world, rank, local):
+    """--launch-selftest: the N-rank plumbing without a GPU -- join the process
+    group (gloo), gather the per-rank info, one all-reduce of a host tensor
+    (the MAX-over-ranks the timed region uses), rank 0 prints one JSON line."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(args.dist_backend)
+        info = gather_dist_info(dist, args.dist_backend, world, rank, local, None)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mx = float(t.item())
+    else:
+        info, mx = None, 1.0
+    if rank == 0:
+        print(json.dumps({"metric": "launch selftest (no measurement)", "value": None, "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dist": info, "max_over_ranks": mx}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def main():
@@ -374,13 +492,22 @@ def main():
     ap.add_argument("--no-time-to-90", action="store_true", help="skip the PPO wall-clock-to-90%% runs")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on one GPU)")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="launcher / process-group check only: every rank joins the group, reports its device and "
+                         "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `python bench.py --gpus N`: this process (which has not touched HIP)
+        # starts the N ranks itself and relays rank 0's JSON line
+        raise SystemExit(self_launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_selftest:
+        return launch_selftest(args, world, rank, local)
     E = args.envs_per_gpu
     G = args.stream_groups
     if G < 1 or E % G:
@@ -398,12 +525,14 @@ def main():
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     dist = None
+    dist_info = None
     if world > 1:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+        dist_info = gather_dist_info(dist, args.dist_backend, world, rank, local, dev)
 
     from rx.vector_env import RacingVectorEnv
     lo = rank * E
@@ -462,6 +591,7 @@ def main():
         sync_all()
         gc.collect()
         gc.disable()  # a full collection over the 65,536-track pool stalls the host for tens of ms
+        mark("t0")
         t0 = time.perf_counter()
         for k in range(steps):
             one_step(events.get(k) if events else None)
@@ -471,6 +601,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        mark("t1")
         if dist:
             t = torch.tensor([el], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -577,6 +708,7 @@ def main():
             "step_roofline": {"kernels": "k_kin1 + k_step2", "avg_step_kernels_ms": round(kin_ms + step2_ms, 5),
                               "bytes_per_env_step": STEP_BYTES_PER_ENV,
                               "achieved_GBs": round(STEP_BYTES_PER_ENV * n / ((kin_ms + step2_ms) * 1e-3) / 1e9, 3)},
+            "dist": dist_info,
             "gae": gae,
             "async_stream_groups": async_probe,
             "ppo_train": ppo,

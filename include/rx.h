@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 16
+#define RX_ABI_VERSION 17
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -89,6 +89,21 @@ typedef struct {
                               wave holds rays with nearby origins and nearly equal directions.
                               Scheduling only: same results. */
   int32_t cull_super;      /* two-level raycast culling: chunks per super-chunk box (0 = one level) */
+  /* ABI v17: launch schedule.  Scheduling only -- every setting gives bit-identical results (the tests
+     force each path) -- so 0 = automatic (the measured best for the env count) everywhere; -1 = off /
+     none where a field has an off state.  Out-of-range values fail rx_create with RX_EINVAL.  These
+     replace the RX_* environment variables earlier versions read: the library reads no environment. */
+  int32_t split;           /* split step (k_kin + k_step2: REWARD beside the raycast): 0 auto (on), 1 on, -1 off */
+  int32_t wide_n;          /* wide kernels (a wave per env / per ray) up to this many single-agent envs:
+                              0 auto (2,048), -1 never, > 0 the threshold */
+  int32_t dyn_lpe;         /* k_dyn1 lanes per env: 0 auto, or 1, 2, 4, 64 */
+  int32_t ray_lpr;         /* lanes per ray task (ray_order 2): 0 auto (4 / 2 / 1 by env count), or 1, 2, 4 */
+  int32_t reward_lpe;      /* k_step2 REWARD lanes per env (single agent): 0 auto (2 up to 4,096 envs), or 1, 2, 4 */
+  int32_t argmin_window;   /* closest-waypoint scan half-width around the previous one: 0 auto (2), -1 none,
+                              1 .. 32 */
+  int32_t seg_filter;      /* float32 pre-filter before each exact segment test: 0 auto (on), 1 on, -1 off */
+  int32_t box_quadrants;   /* quadrant-ordered float32 box tables for single-quadrant ray waves: 0 auto (on),
+                              1 on, -1 off */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are

@@ -287,6 +287,22 @@ int rx_create(const rx_config* cfg, rx_env** out) {
   if (cfg->cull_super < 0 || cfg->cull_super > 64) return fail(RX_EINVAL, "cull_super out of range (%d)", cfg->cull_super);
   if (cfg->autoreset < RX_AUTORESET_NEXT_STEP || cfg->autoreset > RX_AUTORESET_DISABLED)
     return fail(RX_EINVAL, "bad autoreset mode %d", cfg->autoreset);
+  // launch schedule (ABI v17): 0 = auto, -1 = off where there is an off state
+  auto tri = [](int32_t v) { return v == 0 || v == 1 || v == -1; };
+  auto lanes = [](int32_t v, bool wide) { return v == 0 || v == 1 || v == 2 || v == 4 || (wide && v == 64); };
+  if (!tri(cfg->split)) return fail(RX_EINVAL, "split must be 0 (auto), 1 or -1 (got %d)", cfg->split);
+  if (!tri(cfg->seg_filter)) return fail(RX_EINVAL, "seg_filter must be 0 (auto), 1 or -1 (got %d)", cfg->seg_filter);
+  if (!tri(cfg->box_quadrants))
+    return fail(RX_EINVAL, "box_quadrants must be 0 (auto), 1 or -1 (got %d)", cfg->box_quadrants);
+  if (cfg->wide_n < -1) return fail(RX_EINVAL, "wide_n must be >= -1 (got %d)", cfg->wide_n);
+  if (!lanes(cfg->dyn_lpe, true)) return fail(RX_EINVAL, "dyn_lpe must be 0 (auto), 1, 2, 4 or 64 (got %d)", cfg->dyn_lpe);
+  if (!lanes(cfg->ray_lpr, false)) return fail(RX_EINVAL, "ray_lpr must be 0 (auto), 1, 2 or 4 (got %d)", cfg->ray_lpr);
+  if (!lanes(cfg->reward_lpe, false))
+    return fail(RX_EINVAL, "reward_lpe must be 0 (auto), 1, 2 or 4 (got %d)", cfg->reward_lpe);
+  if (cfg->argmin_window < -1 || cfg->argmin_window > 32)
+    return fail(RX_EINVAL, "argmin_window must be 0 (auto), -1 (none) or 1 .. 32 (got %d)", cfg->argmin_window);
+  if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 1))
+    return fail(RX_EINVAL, "dyn_lpe / reward_lpe > 1 are single-agent schedules (n_agents = 2)");
   if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
     return fail(RX_EINVAL, "n_envs * n_agents * n_sensors overflows int32");
   int ndev = 0;
@@ -419,36 +435,30 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   std::vector<int> ray_groups;  // end index (in ray) of each 64-env block's waves
   if (h->cfg.ray_order == 2 && A * R > 16 * A)
     return fail(RX_EINVAL, "ray_order 2 supports at most 16 sensors (got %d)", R);
+  // launch schedule (rx_config ABI v17 fields; 0 = the measured default for N)
+  const rx_config& c = h->cfg;
   h->dyn_lpe = (A == 1 && N <= RX_DYN1_SMALL_N) ? RX_DYN1_LPE_SMALL : 1;
-  int wide_n = RX_WIDE_N;
-  if (const char* ev = getenv("RX_WIDE_N")) wide_n = atoi(ev);  // A/B knob
+  const int wide_n = c.wide_n == 0 ? RX_WIDE_N : c.wide_n;  // -1: never
   if (A == 1 && N <= wide_n) h->dyn_lpe = 64;
-  if (const char* ev = getenv("RX_ARGMIN_WINDOW")) h->argmin_window = std::max(0, std::min(32, atoi(ev)));  // A/B knob
+  if (A == 1 && c.dyn_lpe != 0) h->dyn_lpe = c.dyn_lpe;
+  h->argmin_window = c.argmin_window == 0 ? 2 : (c.argmin_window < 0 ? 0 : c.argmin_window);
   {  // the window [prev - H, prev + H] is wrapped into [0, W) by one +-W: needs H <= W of every slot
     int min_w = 1 << 30;
     for (int k = 0; k < h->n_tracks; ++k) min_w = std::min(min_w, h->wp_off_h[k + 1] - h->wp_off_h[k]);
     h->argmin_window = std::min(h->argmin_window, min_w);
   }
-  if (const char* ev = getenv("RX_DYN1_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
-    const int v = atoi(ev);
-    if (A == 1 && (v == 1 || v == 2 || v == 4 || v == 64)) h->dyn_lpe = v;
-  }
   // few envs: the culled raycast is a latency chain over too few waves to
   // fill the chip, so 2 or 4 lanes share one ray and split its leaves
   h->ray_lpr = 1;
-  if (h->cfg.ray_order == 2 && h->dyn_lpe != 64)
+  if (h->cfg.ray_order == 2 && h->dyn_lpe != 64) {
     h->ray_lpr = (long long)N * A <= RX_RAY_LPR4_N ? 4 : ((long long)N * A <= RX_RAY_LPR2_N ? 2 : 1);
-  if (const char* ev = getenv("RX_RAY_LPR")) {  // A/B knob: 1, 2 or 4 lanes per ray
-    const int v = atoi(ev);
-    if ((v == 1 || v == 2 || v == 4) && h->cfg.ray_order == 2 && h->dyn_lpe != 64) h->ray_lpr = v;
+    if (c.ray_lpr != 0) h->ray_lpr = c.ray_lpr;
   }
   // few single-agent envs: REWARD (a latency chain of argmins) outlasts the
   // raycast beside it in k_step2 unless 2 lanes share an env's five points
   h->reward_lpe = (A == 1 && N <= RX_REWARD_LPE2_N) ? 2 : 1;
-  if (const char* ev = getenv("RX_REWARD_LPE")) {  // A/B knob: 1, 2 or 4 lanes per env
-    const int v = atoi(ev);
-    if (v == 1 || v == 2 || v == 4) h->reward_lpe = v;
-  }
+  if (c.reward_lpe != 0) h->reward_lpe = c.reward_lpe;
+  h->split = c.split >= 0;
   const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
@@ -544,7 +554,6 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     std::vector<double> z(2 * (size_t)N * A, 0.0);
     if ((rc = upload(h->cs_scratch, z.data(), z.size()))) return rc;
   }
-  if (const char* ev = getenv("RX_SPLIT")) h->split = atoi(ev) != 0;  // A/B knob
   if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
   if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
   h->n_dyn_waves = (int32_t)dyn.size();
@@ -675,13 +684,8 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.cs_scratch = h->cs_scratch.p;
   a.sort_base = h->sort_base.p;
   a.sort_shift = h->sort_shift;
-  static const int quad = [] {  // A/B knob
-    const char* e = getenv("RX_BOX_QUAD");
-    return e ? atoi(e) : 1;
-  }();
-  a.box_quadrants = quad;
-  const char* pf = getenv("RX_SEG_FILTER");  // A/B knob, read per launch so tests can run both paths
-  a.seg_filter = pf ? atoi(pf) : 1;
+  a.box_quadrants = h->cfg.box_quadrants >= 0;
+  a.seg_filter = h->cfg.seg_filter >= 0;
 #ifdef RX_AB_NO_EPSTATS  // A/B build only (tools/build_rev.py): drop the episode-statistics atomics
   a.io.ep_stats = nullptr;
 #endif

@@ -2115,12 +2115,7 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
-    static const int kin_wpb = [] {
-      const char* e = getenv("RX_KIN_WPB");  // A/B knob: waves per k_kin1 workgroup (1 or 4)
-      return e && atoi(e) == 4 ? 4 : 1;
-    }();
-    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3((a->n_dyn_waves + kin_wpb - 1) / kin_wpb), dim3(64 * kin_wpb),
-                       0, s, *a);
+    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
   } else if (part == RX_SPLIT_REWARD) {
     hipLaunchKernelGGL(k_step2<1>, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
   } else {  // RX_SPLIT_REWARD_RAYS: both halves in one launch
@@ -2151,22 +2146,12 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else
       hipLaunchKernelGGL(k_rays_wide<2>, wg, blk, 0, s, *a);
   } else if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
-    // waves per workgroup for the raycast (RX_RAYS_WPB: 1, 2 or 4; A/B knob)
-    static const int wpb = [] {
-      const char* e = getenv("RX_RAYS_WPB");
-      const int v = e ? atoi(e) : 1;
-      return (v == 1 || v == 2 || v == 4) ? v : 1;
-    }();
-    // RX_RAYS_LDS (A/B knob): dynamic LDS bytes per workgroup, to cap the raycast's occupancy
-    static const int lds = [] {
-      const char* e = getenv("RX_RAYS_LDS");
-      return e ? atoi(e) : 0;
-    }();
-    const dim3 rgrd((a->n_ray_waves + wpb - 1) / wpb), rblk(64 * wpb);
+    // one wave per workgroup: finer-grained dispatch fills the tail, and the XCD
+    // placement of rx_assign's ray-wave order holds per wave
     if (n_agents == 1)
-      hipLaunchKernelGGL(k_rays<1>, rgrd, rblk, lds, s, *a);
+      hipLaunchKernelGGL(k_rays<1>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
     else
-      hipLaunchKernelGGL(k_rays<2>, rgrd, rblk, lds, s, *a);
+      hipLaunchKernelGGL(k_rays<2>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
   }
   return (int)hipGetLastError();
 }

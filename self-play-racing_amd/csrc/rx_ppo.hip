@@ -618,8 +618,12 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
                                                      float kl_target, float scale, float* grad, uint8_t* stop,
                                                      float* kl_at_stop, float* kl_out, const norm_args* norm_p,
                                                      norm_args norm) {
-  const bool stopped = *stop;  // tested after the partial loads are issued (one round trip, not two)
+  // tested after the partial loads are issued (one round trip, not two), and made
+  // block-uniform through LDS: block 0's wave 1 may raise *stop during this very
+  // launch, so two waves of a later block could read different values
+  const bool stopped = *stop;
   __shared__ float4 red[kRedSlices][kRedCols];
+  __shared__ int s_stopped;
   const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
   const int p4 = blockIdx.x * (4 * kRedCols) + c * 4;  // first of this thread's 4 parameters
   float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -640,9 +644,10 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
         s.w += v[k].w;
       }
     }
-  if (stopped) return;  // uniform: KL early stop already hit
+  if (threadIdx.x == 0) s_stopped = stopped;
   red[sl][c] = s;
   __syncthreads();
+  if (s_stopped) return;  // block-uniform: KL early stop already hit
   // slices -> 8 groups (group q sums slices q, q+8, ...) -> column total, in order
   __shared__ float4 red2[8][kRedCols];
   if (sl < 8) {

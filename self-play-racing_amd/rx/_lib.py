@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -43,7 +43,14 @@ class RxConfig(ctypes.Structure):
                 ("max_steps", ctypes.c_int32), ("autoreset", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("sensor_half_cone", ctypes.c_double), ("speed_weight", ctypes.c_double),
                 ("cull_chunk", ctypes.c_int32), ("sort_interval", ctypes.c_int32),
-                ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)]
+                ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)] + \
+               [(k, ctypes.c_int32) for k in ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window",
+                                               "seg_filter", "box_quadrants")]
+
+
+# rx_config launch-schedule fields (ABI v17): 0 = auto, -1 = off / none (include/rx.h).
+# Scheduling only: every value gives bit-identical results.
+SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants")
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",

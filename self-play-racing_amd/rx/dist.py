@@ -26,6 +26,17 @@ import torch
 import torch.distributed as td
 
 
+# all-reduces issued through this module (count, payload bytes): bench.py reports
+# the per-update figures of its data-parallel PPO leg from these
+COUNTS = {"all_reduce": 0, "bytes": 0}
+
+
+def _all_reduce(t, **kw):
+    COUNTS["all_reduce"] += 1
+    COUNTS["bytes"] += t.numel() * t.element_size()
+    td.all_reduce(t, **kw)
+
+
 def active():
     return td.is_available() and td.is_initialized() and td.get_world_size() > 1
 
@@ -60,7 +71,7 @@ def sum_stats(s, device):
     if not active():
         return s
     t = torch.tensor([float(s[0]), float(s[1]), float(s[2])], dtype=torch.float64, device=device)
-    td.all_reduce(t)
+    _all_reduce(t)
     return float(t[0]), float(t[1]), int(round(float(t[2])))
 
 
@@ -70,7 +81,7 @@ def minibatch_stats(kl_sum, adv):
     t = torch.stack([kl_sum.detach().to(torch.float64), a.sum(), (a * a).sum(),
                      torch.tensor(float(adv.numel()), dtype=torch.float64, device=adv.device)])
     if active():
-        td.all_reduce(t)
+        _all_reduce(t)
     return t
 
 
@@ -80,7 +91,7 @@ def average_gradients(params):
         return
     grads = [p.grad for p in params if p.grad is not None]
     flat = torch.cat([g.reshape(-1) for g in grads])
-    td.all_reduce(flat)
+    _all_reduce(flat)
     flat.div_(td.get_world_size())
     o = 0
     for g in grads:
@@ -93,7 +104,7 @@ def average_flat(flat):
     """Mean over ranks of the flat gradient buffer (rx.optim.FlatAdam): one all-reduce, no copies."""
     if not active():
         return
-    td.all_reduce(flat)
+    _all_reduce(flat)
     flat.div_(td.get_world_size())
 
 
@@ -101,7 +112,7 @@ def all_reduce_sum(t):
     """In-place SUM over ranks (the fused data-parallel update pre-scales its
     shard gradient and KL by 1/world, so the sum is the global mean)."""
     if active():
-        td.all_reduce(t)
+        _all_reduce(t)
     return t
 
 

@@ -203,6 +203,9 @@ class PPO:
                     g = self._capture_rollout(key, obs, actions, logprobs, dones, rewards, values, next_obs,
                                               next_done)
                 g.replay()
+                # the replayed env kernels moved the engine's working state: the
+                # env-order arrays must be exported before the next read
+                self.envs._launched()
             else:
                 self._rollout_body(obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
         s = self.envs.episode_stats(reset=True)
@@ -489,7 +492,8 @@ class PPO:
         b_inds = np.arange(B)
         nxt = None
         ent.stop.zero_()
-        if device_shuffle and ent.fused is not None and rdist.world() == 1 and not c.get("epoch_sync", False):
+        if (device_shuffle and ent.fused is not None and rdist.world() == 1 and not c.get("epoch_sync", False)
+                and not c.get("shard_update", False)):
             self._update_epochs_async(ent, B // mb)
             return
         for epoch in range(c["update_epochs"]):

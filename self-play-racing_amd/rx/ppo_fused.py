@@ -252,7 +252,7 @@ class Rollout:
             self.eps.normal_()
         io = self.venv._io()
         _lib.check(self.L.rx_rollout(self.venv._h, io, r, _lib.stream_ptr(stream)), "rx_rollout")
-        self.venv._launched()
+        self.venv._launched(stream)
 
 
 # config["fused_rollout"] = "auto": the persistent rollout up to this many envs

@@ -54,11 +54,13 @@ class RacingVectorEnv:
     Parameters mirror the reference constructors: per env a control-point
     array (``track_pool[track_id]``) and a track width; ``n_sensors`` (11 in
     train.py); sensor cone pi/3 for A=1 (racing_env.py:45) and pi/2 for A=2
-    (multi_racing_env.py:50)."""
+    (multi_racing_env.py:50).  ``sched``: launch-schedule overrides, a dict
+    over ``_lib.SCHED_FIELDS`` (rx_config ABI v17: 0 = auto, -1 = off;
+    scheduling only, results are identical -- the tests force each path)."""
 
     def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
                  seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=8,
-                 sort_interval=16, ray_order=None, cull_super=8):
+                 sort_interval=16, ray_order=None, cull_super=8, sched=None):
         self.L = _lib.load()
         self.device = torch.device(device) if device is not None else _default_device()
         if self.device.type != "cuda":
@@ -93,6 +95,7 @@ class RacingVectorEnv:
             # the bound state arrays (env order); the engine steps a working copy in
             # wave order and writes these back on demand (the `state` property)
             self._dev_newer = False
+            self._last_stream = None  # stream of the last launch (state export orders after it)
             self._st = {k: torch.zeros(N * A, **f64) for k in ("x", "y", "angle", "vx", "vy", "progress",
                                                              "last_progress", "last_steering")}
             self._st["finished_step"] = torch.full((N * A,), -1, dtype=torch.int32, device=dev)
@@ -115,9 +118,14 @@ class RacingVectorEnv:
                 ep_done=torch.zeros(N, dtype=torch.uint8, device=dev),
                 ep_stats=torch.zeros(_lib.RX_EP_SHARDS * 4, **f64),
             )
+            sched = dict(sched or {})
+            bad = set(sched) - set(_lib.SCHED_FIELDS)
+            if bad:
+                raise ValueError(f"unknown launch-schedule keys {sorted(bad)} (known: {_lib.SCHED_FIELDS})")
+            self.sched = sched
             cfg = _lib.RxConfig(N, A, R, self.max_steps, _AUTORESET[autoreset], dev.index or 0, int(seed) & (2**64 - 1),
                                 float(half_cone), self.speed_weight, int(cull_chunk), int(sort_interval),
-                                int(ray_order), int(cull_super))
+                                int(ray_order), int(cull_super), *[int(sched.get(k, 0)) for k in _lib.SCHED_FIELDS])
             h = _lib._P()
             _lib.check(self.L.rx_create(cfg, h), "rx_create")
             self._h = h
@@ -211,17 +219,31 @@ class RacingVectorEnv:
         the current stream) if a launch changed it.  After writing the tensors,
         call ``state_changed()`` (set_state does)."""
         if self._dev_newer and not self._closed:
-            _lib.check(self.L.rx_state_export(self._h, _lib.stream_ptr()), "rx_state_export")
+            # export on the stream of the last launch (ordered after it), then
+            # make the current stream wait for the export
+            s = self._last_stream
+            cur = torch.cuda.current_stream(self.device)
+            _lib.check(self.L.rx_state_export(self._h, _lib.stream_ptr(s if s is not None else cur)),
+                       "rx_state_export")
+            if s is not None and s != cur:
+                cur.wait_stream(s)
             self._dev_newer = False
         return self._st
 
     def state_changed(self, stream=None):
-        """The state tensors were written: reload the engine's working copy."""
-        _lib.check(self.L.rx_state_import(self._h, _lib.stream_ptr(stream)), "rx_state_import")
+        """The state tensors were written (on ``stream``, default the current
+        one): reload the engine's working copy there; the stream of the last
+        launch waits for the reload, so later launches on it see the new state."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self.L.rx_state_import(self._h, _lib.stream_ptr(s)), "rx_state_import")
+        if self._last_stream is not None and self._last_stream != s:
+            self._last_stream.wait_stream(s)
         self._dev_newer = False
 
-    def _launched(self):
+    def _launched(self, stream=None):
+        """A launch on ``stream`` (None = the current stream) changed the working state."""
         self._dev_newer = True
+        self._last_stream = stream if stream is not None else torch.cuda.current_stream(self.device)
 
     def set_speed_weights(self, w):
         """Per-env RacingEnv.speed_weight ([N] array), or None to use the uniform value."""
@@ -262,7 +284,7 @@ class RacingVectorEnv:
             m = mask.to(self.device, torch.uint8).contiguous()
         io = self._io(obs=obs_out, full=True)
         _lib.check(self.L.rx_reset(self._h, _lib.ptr(m), io, _lib.stream_ptr(stream)), "rx_reset")
-        self._dev_newer = True
+        self._launched(stream)
         return obs_out if obs_out is not None else self.buf["obs"]
 
     def step_device(self, actions, obs_out=None, reward_out=None, done_out=None, full_info=False, stream=None,
@@ -278,7 +300,7 @@ class RacingVectorEnv:
             _lib.check(self.L.rx_step(self._h, io, _lib.stream_ptr(stream)), "rx_step")
         else:
             _lib.check(self.L.rx_step_phases(self._h, io, int(phases), _lib.stream_ptr(stream)), "rx_step_phases")
-        self._dev_newer = True
+        self._launched(stream)
         return (obs_out if obs_out is not None else self.buf["obs"],
                 reward_out if reward_out is not None else self.buf["reward"],
                 done_out if done_out is not None else self.buf["done_f32"])

@@ -29,30 +29,35 @@ def rx():
     return ve
 
 
+# launch schedule (rx_config ABI v17) the dyn_path fixture imposes on every _venv
+_PATH_SCHED = {}
+
+
 @pytest.fixture(params=["default", "split", "wide"])
-def dyn_path(request, monkeypatch):
+def dyn_path(request):
     """Run a test on the default kernel choice for its env count, on the split
     step (k_kin1 + k_step2: REWARD half beside the raycast), which librx uses
-    at one lane per env -- forced here via RX_DYN1_LPE=1 -- and on the small-N
+    at one lane per env -- forced here via dyn_lpe = 1 -- and on the small-N
     wide kernels (one env per dynamics wave, one ray per raycast wave, brute
-    force over the lanes; librx uses them up to 2,048 envs) forced for any N."""
+    force over the lanes; librx uses them up to 2,048 envs) forced for any N.
+    "default" turns the wide kernels off, so small tests run the k_dyn1<4> +
+    culled k_rays path that the automatic choice skips below 2,049 envs."""
     if request.param == "split":
-        monkeypatch.setenv("RX_DYN1_LPE", "1")
-        monkeypatch.setenv("RX_SPLIT", "1")
-        monkeypatch.setenv("RX_WIDE_N", "0")
+        _PATH_SCHED.update(dyn_lpe=1, split=1, wide_n=-1)
     elif request.param == "wide":
-        monkeypatch.setenv("RX_WIDE_N", "1000000")
+        _PATH_SCHED.update(wide_n=1000000)
     else:
-        monkeypatch.setenv("RX_WIDE_N", "0")
-    return request.param
+        _PATH_SCHED.update(wide_n=-1)
+    yield request.param
+    _PATH_SCHED.clear()
 
 
-def _venv(rx, golden, tracks, n_agents=1, **kw):
+def _venv(rx, golden, tracks, n_agents=1, sched=None, **kw):
     cps = [golden.tracks[k]["cp"] if golden.tracks[k]["label"] != "default" else None for k in tracks]
     ws = [golden.tracks[k]["width"] for k in tracks]
     from rx.track import DEFAULT_CONTROL_POINTS
     cps = [DEFAULT_CONTROL_POINTS if c is None else c for c in cps]
-    return rx.RacingVectorEnv(cps, ws, n_agents=n_agents, **kw)
+    return rx.RacingVectorEnv(cps, ws, n_agents=n_agents, sched={**_PATH_SCHED, **(sched or {})}, **kw)
 
 
 def test_sensor_angles_match_numpy(rx, golden):
@@ -183,13 +188,12 @@ def test_random_rollout_bit_exact_vs_oracle_dev(rx, golden, oracle_dev, dyn_path
         assert np.array_equal(g[k], st[k]), k
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_multi_step_vs_golden_and_oracle(rx, golden, oracle_dev, monkeypatch, split):
+@pytest.mark.parametrize("split", [-1, 1])
+def test_multi_step_vs_golden_and_oracle(rx, golden, oracle_dev, split):
     """Two-car KATs on the one-kernel step (k_dyn2 + k_rays<2>) and on the split
     step (k_kin2 + k_step2<2>)."""
-    monkeypatch.setenv("RX_SPLIT", split)
     step = golden["step_multi"]
-    v = _venv(rx, golden, step["track"], n_agents=2, autoreset="disabled")
+    v = _venv(rx, golden, step["track"], n_agents=2, autoreset="disabled", sched=dict(split=split))
     st = multi_state_from(step)
     flat = {k: st[k].reshape(-1) for k in ("x", "y", "angle", "vx", "vy", "progress", "last_progress",
                                              "last_steering", "flags", "finished_step")}
@@ -316,28 +320,24 @@ def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
 
 
 @pytest.mark.parametrize("n_agents,N", [(1, 1536), (1, 8256), (2, 512)])
-def test_segment_prefilter_is_exact(rx, golden, monkeypatch, n_agents, N):
+def test_segment_prefilter_is_exact(rx, golden, n_agents, N):
     """The float32 segment pre-filter (seg_may_hit) only skips exact segment
-    tests that cannot report a hit: with (RX_SEG_FILTER=1, the default) and
-    without it, obs, rewards and dones are bit-identical over 300 steps of
-    random play (both culled; culled == brute force is checked above).  8,256
-    envs run the split step (k_step2), fewer the one-kernel path (k_rays)."""
+    tests that cannot report a hit: with (seg_filter on, the default) and
+    without it (seg_filter = -1), obs, rewards and dones are bit-identical over
+    300 steps of random play (both culled; culled == brute force is checked
+    above).  8,256 envs run the split step (k_step2), fewer the one-kernel path
+    (k_rays)."""
     tracks = np.arange(N) % golden.n_tracks
-    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step")
-    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step")
-    monkeypatch.setenv("RX_SEG_FILTER", "0")
-    ra0 = va.reset_device().clone()
-    monkeypatch.setenv("RX_SEG_FILTER", "1")
-    assert torch.equal(ra0, vb.reset_device())
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step", sched=dict(seg_filter=-1))
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=3, autoreset="next_step", sched=dict(seg_filter=1))
+    assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(12)
     shape = (N, 2) if n_agents == 1 else (N, 2, 2)
     for t in range(300):
         a = torch.rand(shape, device="cuda", generator=g) * 2 - 1
         if n_agents == 1:
             a[:, 1].abs_()
-        monkeypatch.setenv("RX_SEG_FILTER", "0")
-        oa, ra, da = (x.clone() for x in va.step_device(a))
-        monkeypatch.setenv("RX_SEG_FILTER", "1")
+        oa, ra, da = va.step_device(a)
         ob, rb, db = vb.step_device(a)
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
     va.close()
@@ -346,18 +346,16 @@ def test_segment_prefilter_is_exact(rx, golden, monkeypatch, n_agents, N):
 
 @pytest.mark.parametrize("lpr", [2, 4])
 @pytest.mark.parametrize("n_agents,N", [(1, 1536), (1, 8256), (2, 512), (2, 3000)])
-def test_lanes_per_ray_are_exact(rx, golden, monkeypatch, n_agents, N, lpr):
-    """Two or four lanes per ray (RX_RAY_LPR: the lanes split each scanned
+def test_lanes_per_ray_are_exact(rx, golden, n_agents, N, lpr):
+    """Two or four lanes per ray (ray_lpr: the lanes split each scanned
     leaf and take the minimum of their bests; 4 is the default up to
     RX_RAY_LPR4_N (env, agent) pairs) against one lane per ray: obs, rewards
     and dones are bit-identical over 300 steps of random play.  Ragged sizes
     leave partial ray waves (duplicate-task lanes); 8,256 envs run the split
     step."""
     tracks = np.arange(N) % golden.n_tracks
-    monkeypatch.setenv("RX_RAY_LPR", "1")
-    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step")
-    monkeypatch.setenv("RX_RAY_LPR", str(lpr))
-    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step")
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step", sched=dict(ray_lpr=1))
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step", sched=dict(ray_lpr=lpr))
     assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(13)
     shape = (N, 2) if n_agents == 1 else (N, 2, 2)
@@ -374,18 +372,16 @@ def test_lanes_per_ray_are_exact(rx, golden, monkeypatch, n_agents, N, lpr):
 
 @pytest.mark.parametrize("lpe", [2, 4])
 @pytest.mark.parametrize("N", [4100, 8256])
-def test_reward_lanes_per_env_are_exact(rx, golden, monkeypatch, N, lpe):
-    """The split step's REWARD half at 2 or 4 lanes per env (RX_REWARD_LPE:
+def test_reward_lanes_per_env_are_exact(rx, golden, N, lpe):
+    """The split step's REWARD half at 2 or 4 lanes per env (reward_lpe:
     the five argmin points spread over the env's lanes, the wall test OR-ed
     across them) against one lane per env: obs, rewards and dones
     bit-identical over 300 steps of random play, episode counts exact (ragged last
     dynamics wave at 4,100 envs; the episode-return sums only to f64
     rounding, as their atomic order differs)."""
     tracks = np.arange(N) % golden.n_tracks
-    monkeypatch.setenv("RX_REWARD_LPE", "1")
-    va = _venv(rx, golden, tracks, seed=6, autoreset="next_step")
-    monkeypatch.setenv("RX_REWARD_LPE", str(lpe))
-    vb = _venv(rx, golden, tracks, seed=6, autoreset="next_step")
+    va = _venv(rx, golden, tracks, seed=6, autoreset="next_step", sched=dict(reward_lpe=1))
+    vb = _venv(rx, golden, tracks, seed=6, autoreset="next_step", sched=dict(reward_lpe=lpe))
     assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(14)
     for t in range(300):
@@ -484,21 +480,19 @@ def test_dyn_lanes_per_env_paths_agree(rx, golden):
 
 @pytest.mark.parametrize("n_agents", [1, 2])
 @pytest.mark.parametrize("autoreset", ["next_step", "disabled"])
-def test_split_step_equals_one_kernel_step(rx, golden, monkeypatch, autoreset, n_agents):
+def test_split_step_equals_one_kernel_step(rx, golden, autoreset, n_agents):
     """The split step (k_kin1 / k_kin2 + fused REWARD/raycast k_step2<A>) == the
     one-kernel step bit for bit: obs, rewards (f32 and f64), masks, placement,
     info, episode statistics and the whole f64 state, over 300 steps of random
     play (two cars: start-slot draws, car-car contact and placement included)."""
-    monkeypatch.setenv("RX_DYN1_LPE", "1")
     N = 2048
     tracks = np.arange(N) % golden.n_tracks
     kw = dict(autoreset=autoreset, n_agents=n_agents)
     if n_agents == 2:
         kw["seed"] = 5
-    monkeypatch.setenv("RX_SPLIT", "0")
-    va = _venv(rx, golden, tracks, **kw)
-    monkeypatch.setenv("RX_SPLIT", "1")
-    vb = _venv(rx, golden, tracks, **kw)
+    one = dict(dyn_lpe=1) if n_agents == 1 else {}
+    va = _venv(rx, golden, tracks, sched=dict(one, split=-1), **kw)
+    vb = _venv(rx, golden, tracks, sched=dict(one, split=1), **kw)
     assert torch.equal(va.reset_device(), vb.reset_device())
     g = torch.Generator(device="cuda").manual_seed(17)
     for t in range(300):

@@ -85,3 +85,42 @@ def test_update_abi_validates_without_device():
     b.obs_dim = 15
     args = [None] * 12
     assert L.rx_ppo_minibatch_update(ctypes.byref(b), 0, ctypes.byref(cfg), *args) == _lib.RX_EINVAL
+
+
+def test_schedule_config_is_validated_and_the_library_reads_no_environment():
+    """ABI v17: the launch-schedule choices are rx_config fields
+    with validated ranges -- out-of-range values fail rx_create with RX_EINVAL and
+    a message naming the field, before any HIP call -- and the production library
+    reads no environment variable at all (getenv is not among its imports), so a
+    stray RX_* variable cannot change the product path."""
+    import subprocess
+    from rx import _build, _lib
+    L = _lib.load()
+    h = _lib._P()
+    base = [16, 1, 11, 3000, 0, 0, 0, 1.0471975511965976, 8.0, 8, 16, 2, 8]
+    bad = {"split": 2, "wide_n": -2, "dyn_lpe": 3, "ray_lpr": 8, "reward_lpe": 64, "argmin_window": 33,
+           "seg_filter": 5, "box_quadrants": -3}
+    for k, v in bad.items():
+        sched = [v if f == k else 0 for f in _lib.SCHED_FIELDS]
+        assert L.rx_create(_lib.RxConfig(*base, *sched), h) == _lib.RX_EINVAL, k
+        assert k.encode() in L.rx_last_error(), (k, L.rx_last_error())
+    two = list(base)
+    two[1] = 2
+    assert L.rx_create(_lib.RxConfig(*two, *[2 if f == "dyn_lpe" else 0 for f in _lib.SCHED_FIELDS]), h) \
+        == _lib.RX_EINVAL
+    # every in-range value passes validation (on a CPU-only host rx_create then fails at the device query)
+    import torch
+    if not torch.cuda.is_available():
+        for k, vals in {"split": (-1, 1), "wide_n": (-1, 5), "dyn_lpe": (1, 2, 4, 64), "ray_lpr": (1, 2, 4),
+                        "reward_lpe": (1, 2, 4), "argmin_window": (-1, 1, 32), "seg_filter": (-1, 1),
+                        "box_quadrants": (-1, 1)}.items():
+            for v in vals:
+                sched = [v if f == k else 0 for f in _lib.SCHED_FIELDS]
+                assert L.rx_create(_lib.RxConfig(*base, *sched), h) != _lib.RX_EINVAL, (k, v)
+    und = subprocess.run(["nm", "-D", "--undefined-only", _build.LIB], capture_output=True, text=True, check=True)
+    syms = {ln.split()[-1].split("@")[0] for ln in und.stdout.splitlines() if ln.strip()}
+    assert "getenv" not in syms and "secure_getenv" not in syms, "librx.so must not read the environment"
+    strings = open(_build.LIB, "rb").read()
+    for knob in (b"RX_SEG_FILTER", b"RX_SPLIT", b"RX_RAY_LPR", b"RX_REWARD_LPE", b"RX_DYN1_LPE", b"RX_WIDE_N",
+                 b"RX_ARGMIN_WINDOW", b"RX_BOX_QUAD", b"RX_KIN_WPB", b"RX_RAYS_WPB", b"RX_RAYS_LDS"):
+        assert knob not in strings, knob

@@ -92,12 +92,14 @@ def test_agent_sampling_is_torch_normal():
     assert torch.equal(lp, d.log_prob(ref).sum(-1)) and torch.equal(ent, d.entropy().sum(-1))
 
 
-def test_graph_rollout_equals_eager_across_updates():
+@pytest.mark.parametrize("fused_rollout", ["auto", False])
+def test_graph_rollout_equals_eager_across_updates(fused_rollout):
     """The captured rollout replays with the CURRENT weights, log_std and RNG
-    state: two updates with graph_rollout on == the same two updates eager."""
+    state: two updates with graph_rollout on == the same two updates eager
+    (persistent k_rollout, and the per-step policy + rx_step path)."""
     outs = []
     for graph in (True, False):
-        t, c = _train_single_style(num_envs=64, num_steps=16, graph_rollout=graph)
+        t, c = _train_single_style(num_envs=64, num_steps=16, graph_rollout=graph, fused_rollout=fused_rollout)
         bufs = t._buffers()
         nobs = t.envs.buf["obs"].clone()
         nd = torch.zeros(64, device="cuda")
@@ -111,6 +113,9 @@ def test_graph_rollout_equals_eager_across_updates():
                 nv = t.agent.get_value(nobs).flatten()
             adv, ret = t.compute_advantages(rewards, dones, values, nv, nd)
             t.ppo_update(adv, ret, values, logprobs, actions, obs)
+            # the env state read back after a replay must be the replayed one (not a
+            # stale export): ADVICE r02, graph replays mark the working state newer
+            seq.append([torch.from_numpy(v) for _, v in sorted(t.envs.get_state().items())])
         outs.append(seq)
     for ua, ub in zip(*outs):
         for x, y in zip(ua, ub):
