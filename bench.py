@@ -239,22 +239,33 @@ def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
             "mode_a_one_core_16_envs": mode_a}
 
 
-def time_to_90(configs):
+def time_to_90(configs, seeds=(1, 2, 3)):
     """Second half of BASELINE.json's metric: PPO wall-clock to 90 % success
-    (evaluate.py protocol; tools/time_to_success.py), training time only."""
+    (evaluate.py protocol; tools/time_to_success.py), training time only, as a
+    distribution over ``seeds`` (config["seed"]: the track pool, the initial
+    policy and the sampling streams all change with it, as in train.py).
+    build_s = PPO construction (env table upload, agent, flat buffers), which
+    the training time excludes."""
     from tools.time_to_success import run as tts
     out = []
     for ne, ns, shuffle in configs:
-        r = tts(num_envs=ne, num_steps=ns, eval_every=1, device_shuffle=shuffle == "device", max_minutes=2.0,
-                quiet=True)
-        out.append({"num_envs": ne, "num_steps": ns, "shuffle": shuffle, "value_s": r["value_s"],
-                    "reached_at_step": r["reached_at_step"],
-                    "updates": len(r["curve"]),
-                    "success_rate": r["curve"][-1].get("success_rate") if r["curve"] else None})
+        runs = []
+        for sd in seeds:
+            r = tts(num_envs=ne, num_steps=ns, eval_every=1, device_shuffle=shuffle == "device", max_minutes=1.0,
+                    quiet=True, seed=sd)
+            runs.append({"seed": sd, "value_s": r["value_s"], "build_s": r["build_s"],
+                         "reached_at_step": r["reached_at_step"], "updates": len(r["curve"]),
+                         "success_rate": r["curve"][-1].get("success_rate") if r["curve"] else None})
+        vals = sorted(x["value_s"] for x in runs if x["value_s"] is not None)
+        dist = {"min": vals[0], "median": vals[len(vals) // 2] if len(vals) % 2 else
+                round(0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2]), 4), "max": vals[-1]} if vals else None
+        out.append({"num_envs": ne, "num_steps": ns, "shuffle": shuffle, "value_s": dist,
+                    "reached": f"{len(vals)}/{len(runs)} seeds", "runs": runs})
     return {"metric": "PPO wall-clock to 90% success rate", "unit": "s", "higher_is_better": False,
             "protocol": "evaluate.py: 40 tracks (seed 42) x 5 runs, widths by run, <= 2000 steps, stochastic "
-                        "policy, evaluated after every update; training time only (evaluations excluded)",
-            "runs": out}
+                        "policy, evaluated after every update; training time only (evaluations and PPO "
+                        "construction, build_s, excluded); min / median / max over config seeds",
+            "configs": out}
 
 
 # Algorithmic flops of one minibatch row through k_ppo_grad (both trunks,
@@ -357,6 +368,11 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
             "allreduce_per_update_expected": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
             "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
             "note": "KL early stop off, device shuffles; timed after one warm-up update"}
+
+
+def _lib_path():
+    from rx import _lib
+    return _lib.load()._name
 
 
 def _free_port():
@@ -469,6 +485,10 @@ def main():
     ap.add_argument("--burn-in", type=int, default=100,
                     help="untimed steps before the timed region counted together with --warmup: at least this many "
                          "(a run that starts with every car on its start line is not the steady state)")
+    ap.add_argument("--refill", type=int, default=50,
+                    help="the pre-timing garbage collection runs this many untimed steps before the timed region "
+                         "(part of the untimed count) so the GPU is back at its loaded clock when timing starts; "
+                         "0 = collect right before timing (round-2 order)")
     ap.add_argument("--envs-per-gpu", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -492,6 +512,10 @@ def main():
     ap.add_argument("--no-time-to-90", action="store_true", help="skip the PPO wall-clock-to-90%% runs")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on one GPU)")
+    ap.add_argument("--sched", default="",
+                    help="launch-schedule overrides for A/B runs, 'key=value,...' over rx_config's ABI v17 fields "
+                         "(split, wide_n, dyn_lpe, ray_lpr, reward_lpe, argmin_window, seg_filter, box_quadrants; "
+                         "0 = auto, -1 = off); scheduling only, results are identical")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, reports its device and "
                          "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
@@ -541,6 +565,8 @@ def main():
     shift = torch.tensor([-1.0, 0.0], device=dev)
     untimed = max(args.warmup, args.burn_in)
 
+    sched = {k: int(v) for k, v in (kv.split("=") for kv in args.sched.split(",") if kv)}
+
     def make_groups(G):
         """G independent env groups, each stepping on its own HIP stream (a group's
         step depends only on its own envs, so different groups' kernels overlap)."""
@@ -548,7 +574,7 @@ def main():
         envs = [RacingVectorEnv(pool[lo + g * n:lo + (g + 1) * n], widths[lo + g * n:lo + (g + 1) * n], n_agents=1,
                                 n_sensors=11, device=dev, autoreset="next_step", cull_chunk=args.cull_chunk,
                                 sort_interval=args.sort_interval, ray_order=args.ray_order,
-                                cull_super=args.cull_super)
+                                cull_super=args.cull_super, sched=sched)
                 for g in range(G)]
         # several groups: every group on a stream of its own (torch's current stream is the
         # null stream, which would serialise against the others)
@@ -587,9 +613,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    def timed(one_step, steps, events=None):
+    def timed(one_step, steps, events=None, collect=True):
         sync_all()
-        gc.collect()
+        if collect:
+            gc.collect()
         gc.disable()  # a full collection over the 65,536-track pool stalls the host for tens of ms
         mark("t0")
         t0 = time.perf_counter()
@@ -611,12 +638,23 @@ def main():
     envs, one_step, n = make_groups(G)
     env0 = envs[0]
     n_slots = len(env0.tracks)
-    for _ in range(untimed):
+    schedule = env0.schedule()
+    # untimed steps; the garbage collection that keeps it out of the timed region runs
+    # BEFORE the last --refill of them: it stalls the host for tens of ms, the GPU idles
+    # and drops its clock meanwhile, and the refill steps bring it back under load
+    # (timing starts with a queue-drain sync, as always)
+    refill = max(0, min(args.refill, untimed))
+    for _ in range(untimed - refill):
         one_step()
+    if refill:
+        gc.collect()
+        gc.disable()
+        for _ in range(refill):
+            one_step()
     sync_all()
     ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- timed region: production steps only (one rx_step per step, no instrumentation)
-    elapsed = timed(one_step, args.steps)
+    elapsed = timed(one_step, args.steps, collect=refill == 0)
     ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- instrumented region (after, same state distribution): per-kernel durations of the
     # production launches (k_kin1, k_step2) on every other step; on the others the dynamics
@@ -680,6 +718,8 @@ def main():
                        "stream_groups": G, "envs_per_launch": n,
                        "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
+                       "schedule": schedule, "sched_overrides": sched or None,
+                       "library": os.path.relpath(_lib_path(), ROOT),
                        "parallelism": f"env shards x{world}, no collective in the step"},
             "steady_state": {"untimed_steps_before_timing": untimed,
                              "episodes_ended_before_timing": ep_untimed[2],

@@ -171,6 +171,14 @@ int rx_sensor_angles(const rx_env* h, double* out);
  * reference has no counterpart (its SyncVectorEnv steps envs in order). */
 int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort_shift);
 
+/* Diagnostics (ABI v17): the launch schedule rx_assign resolved from rx_config
+ * for this handle, out int32 [RX_SCHEDULE_W] = split step (0/1), wide kernels
+ * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
+ * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
+ * tables (0/1), dynamics waves, ray waves.  Host only, no device call. */
+#define RX_SCHEDULE_W 10
+int rx_schedule(const rx_env* h, int32_t* out);
+
 /* Track table (host arrays, copied to the device).  Replaces the per-env
  * Track.__init__ geometry (environment/track.py:61-148): slot k has
  * W_k = wp_off[k+1]-wp_off[k] waypoints and 2*W_k boundary segments.
@@ -275,7 +283,8 @@ int rx_gae_scan(int32_t T, int32_t N, const float* rewards, const float* values,
  *           the host-side lr anneal);
  *   stop    device bool or NULL: when *stop != 0 the launch changes nothing
  *           (the KL early stop of agent/ppo.py:178-182 without a host sync);
- *   ws      device f32 scratch of rx_adam_workspace_floats(cfg) elements,
+ *   ws      device f32 scratch of rx_adam_workspace_floats(cfg) elements
+ *           (the clip-norm partials, then Adam's two step scalars),
  *           owned by the caller (one per concurrently stepping optimizer).
  * max_grad_norm <= 0 disables clipping.  Grads are scaled in place, as
  * clip_grad_norm_ does.  Equal to torch's clip + Adam within float rounding

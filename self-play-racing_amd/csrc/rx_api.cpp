@@ -357,6 +357,16 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
   return RX_OK;
 }
 
+int rx_schedule(const rx_env* h, int32_t* out) {
+  if (!h || !out) return fail(RX_EINVAL, "rx_schedule: null argument");
+  if (!h->assigned) return fail(RX_ESTATE, "rx_schedule before rx_assign");
+  const int32_t v[RX_SCHEDULE_W] = {h->split ? 1 : 0, h->dyn_lpe == 64 ? 1 : 0, h->dyn_lpe, h->ray_lpr, h->reward_lpe,
+                                    h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
+                                    h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves};
+  std::copy(v, v + RX_SCHEDULE_W, out);
+  return RX_OK;
+}
+
 int rx_destroy(rx_env* h) {
   if (!h) return RX_OK;
   (void)hipSetDevice(h->cfg.device);
@@ -903,7 +913,7 @@ size_t rx_adam_workspace_floats(const rx_adam_config* cfg) {
   if (adam_cfg_error(cfg) != RX_OK) return 0;
   const int64_t n = cfg->offsets[cfg->n_tensors];
   const int64_t nb = n > 0 ? (n + RX_ADAM_NORM_ELEMS - 1) / RX_ADAM_NORM_ELEMS : 1;
-  return (size_t)(nb * cfg->n_tensors);
+  return (size_t)(nb * cfg->n_tensors) + 2;  // + Adam's two step scalars
 }
 
 int rx_adam_clip_step(const rx_adam_config* cfg, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
@@ -979,7 +989,7 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
 
 size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg) {
   if ((obs_dim != 15 && obs_dim != 19) || adam_cfg_error(cfg) != RX_OK) return 0;
-  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors;
+  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors + 2;  // + Adam's two step scalars
 }
 
 int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
@@ -998,7 +1008,7 @@ int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_conf
   if (!ws_f32 || !ws_f64 || !grad || !exp_avg || !exp_avg_sq || !step || !lr || !stop || !kl_at_stop || !adam_ws)
     return fail(RX_EINVAL, "rx_ppo_minibatch_update: null buffer");
   const hipStream_t s = (hipStream_t)stream;
-  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step)))
+  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step, lr)))
     return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
   if ((rc = rx_launch_adam_apply(cfg, params, grad, exp_avg, exp_avg_sq, step, lr, stop, adam_ws,
                                  rx_ppo_reduce_blocks(b->obs_dim), s)))

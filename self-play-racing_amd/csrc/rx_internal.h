@@ -139,6 +139,15 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
 extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int max_w, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
+// Adam's per-step scalars for step count s (torch.optim.Adam, non-capturable):
+// out[0] = step_size = -lr / (1 - beta1^s), out[1] = sqrt(1 - beta2^s).  Written
+// once per optimizer step next to the clip-norm partials (rx_adam_workspace_floats
+// counts the 2 floats) by the launch that bumps the step count.
+__device__ __forceinline__ void rx_adam_scalars(const rx_adam_config& cfg, float step, double lr, float* out) {
+  const double s = (double)step;
+  out[0] = (float)(-(lr / (1.0 - pow(cfg.beta1, s))));
+  out[1] = (float)sqrt(1.0 - pow(cfg.beta2, s));
+}
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                               const double* lr, const uint8_t* stop, float* ws, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
@@ -150,7 +159,7 @@ extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* sto
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
                                   const rx_adam_config* cfg = nullptr, float* norm_ws = nullptr,
-                                  float* step = nullptr);
+                                  float* step = nullptr, const double* lr = nullptr);
 extern "C" int rx_ppo_reduce_blocks(int obs_dim);
 extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                                     const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s);

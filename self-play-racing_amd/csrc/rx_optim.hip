@@ -4,16 +4,22 @@
 // parameters, so the eager torch path is ~40 launches of a few hundred
 // elements each; here it is two launches, each one memory round trip wide:
 //   k_adam_norm   per-tensor sums of squares of every 64-entry block of the
-//                 gradient -> ws[block][tensor]; bumps the step count;
-//   k_adam_apply  one thread per element: every workgroup folds ws in the same
-//                 order (per-tensor norms -> global norm -> clip coefficient,
-//                 identical in all of them), then clips the gradient and
-//                 applies Adam to its element.
+//                 gradient -> ws[block][tensor]; bumps the step count and
+//                 writes Adam's two bias-correction scalars -> ws[nb * n_t ..];
+//   k_adam_apply  one thread per element: its gradient / moment / parameter
+//                 loads go out first, then every workgroup folds the norm
+//                 partials of each tensor's own blocks in the same order
+//                 (per-tensor norms -> global norm -> clip coefficient,
+//                 identical in all of them), clips the gradient and applies
+//                 Adam to its element.
 // The step count, lr and an early-stop flag live in device memory, so the pair
-// can sit inside a captured graph.
+// can sit inside a captured graph.  The fused PPO minibatch update writes the
+// same ws (partials + scalars) from k_ppo_reduce (rx_ppo.hip) and launches only
+// k_adam_apply.
 #include <hip/hip_runtime.h>
 
 #include "rx.h"
+#include "rx_internal.h"
 
 namespace {
 
@@ -28,7 +34,7 @@ struct adam_args {
   float* step;
   const double* lr;
   const uint8_t* stop;
-  float* ws;  // [nb][n_tensors] partial sums of squares
+  float* ws;  // [nb][n_tensors] partial sums of squares, then the 2 Adam scalars
   int nb;     // partial rows in ws
 };
 
@@ -36,12 +42,16 @@ struct adam_args {
 // consecutive entries, an fmaf chain per lane, then a 16-lane xor tree --
 // exactly the partials k_ppo_reduce writes in the fused minibatch update
 // (rx_ppo.hip), so both optimizer paths clip with bit-identical norms.
-constexpr int kNormBlock = 64;
+constexpr int kNormBlock = RX_ADAM_NORM_ELEMS;
 __global__ __launch_bounds__(kT) void k_adam_norm(adam_args a) {
   if (a.stop && *a.stop) return;  // uniform: KL early stop already hit
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.step += 1.0f;  // k_adam_apply reads the new count
-  if (!(a.cfg.max_grad_norm > 0.0)) return;
   const int n_t = a.cfg.n_tensors;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const float s = *a.step + 1.0f;
+    *a.step = s;  // k_adam_apply reads the new count through the scalars
+    rx_adam_scalars(a.cfg, s, *a.lr, a.ws + (size_t)a.nb * n_t);
+  }
+  if (!(a.cfg.max_grad_norm > 0.0)) return;
   const int64_t n = a.cfg.offsets[n_t];
   const int64_t blk = (int64_t)blockIdx.x * (kT / 16) + (threadIdx.x >> 4);  // 64-entry block of this lane group
   if (blk >= a.nb) return;  // whole 16-lane groups
@@ -66,63 +76,55 @@ __global__ __launch_bounds__(kT) void k_adam_norm(adam_args a) {
 }
 
 __global__ __launch_bounds__(kT) void k_adam_apply(adam_args a) {
-  if (a.stop && *a.stop) return;
   const int n_t = a.cfg.n_tensors;
   const int64_t n = a.cfg.offsets[n_t];
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const bool live = i < n;
+  // the element's operands and the step scalars first: one memory round trip
+  // that overlaps the norm fold below
+  float g = live ? a.g[i] : 0.0f, m = live ? a.m[i] : 0.0f, v = live ? a.v[i] : 0.0f, p = live ? a.p[i] : 0.0f;
+  const float step_size = a.ws[(size_t)a.nb * n_t], bc2_sqrt = a.ws[(size_t)a.nb * n_t + 1];
+  __shared__ int s_stopped;
+  if (threadIdx.x == 0) s_stopped = a.stop ? (int)*a.stop : 0;
   float coef = 1.0f;
   if (a.cfg.max_grad_norm > 0.0) {
     // torch.nn.utils.clip_grad_norm_: total = ||(||g_0||, ..., ||g_k||)||_2,
     // coef = clamp(max_norm / (total + 1e-6), max=1), grads *= coef.
-    // Every workgroup folds the nb partial rows in the same fixed order.
-    // Every workgroup folds the nb partial rows the same way: the [nb][n_t]
-    // partials staged in LDS (coalesced, all loads in flight), then wave w sums
-    // tensors w, w + 4, ...: lane l adds rows l, l + 64, ... in order, a 64-lane
-    // xor tree finishes.
-    constexpr int kMaxPart = 8192;  // LDS floats for the partials
-    __shared__ float part[kMaxPart];
+    // Wave w folds tensors w, w + 4, ...: lane l adds the tensor's blocks
+    // b = l (mod 64) in ascending order, a 64-lane xor tree finishes.  Only the
+    // blocks the tensor overlaps are read: every other partial row holds an
+    // exact 0 for it, so the sums equal a sweep over all nb rows bit for bit,
+    // at nb + n_t loads instead of nb * n_t.
     __shared__ float norms[RX_ADAM_MAX_TENSORS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tot = a.nb * n_t;
-    for (int c0 = 0; c0 < tot; c0 += kMaxPart) {  // one chunk unless nb * n_t > kMaxPart
-      const int c1 = min(tot, c0 + kMaxPart);
-      for (int e = c0 + threadIdx.x; e < c1; e += kT) part[e - c0] = a.ws[e];
-      __syncthreads();
-      for (int u = wave; u < n_t; u += kT / 64) {
-        float s = c0 ? norms[u] : 0.0f;  // running total over the chunks
-        float l = 0.0f;
-        for (int b = lane; b < a.nb; b += 64) {
-          const int e = b * n_t + u;
-          if (e >= c0 && e < c1) l += part[e - c0];
-        }
-        for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
-        if (lane == 0) norms[u] = s + l;
+    for (int u = wave; u < n_t; u += kT / 64) {
+      const int64_t lo = a.cfg.offsets[u], hi = a.cfg.offsets[u + 1];
+      float l = 0.0f;
+      if (hi > lo) {
+        const int b_lo = (int)(lo / kNormBlock), b_hi = (int)((hi - 1) / kNormBlock);
+        for (int b = b_lo + ((lane - b_lo) & 63); b <= b_hi; b += 64) l += a.ws[(size_t)b * n_t + u];
       }
-      __syncthreads();
+      for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+      if (lane == 0) norms[u] = sqrtf(l);
     }
-    if (threadIdx.x < n_t) norms[threadIdx.x] = sqrtf(norms[threadIdx.x]);
     __syncthreads();
     float tot2 = 0.0f;
     for (int u = 0; u < n_t; ++u) tot2 += norms[u] * norms[u];
     const float total = sqrtf(tot2);
     coef = fminf((float)a.cfg.max_grad_norm / (total + 1e-6f), 1.0f);
+  } else {
+    __syncthreads();
   }
-  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-  if (i >= n) return;
-  // torch.optim.Adam (foreach, non-capturable) with step count s (already
-  // incremented by k_adam_norm):
+  if (s_stopped || !live) return;  // block-uniform stop: KL early stop already hit
+  // torch.optim.Adam (foreach, non-capturable) with step count s (the scalars
+  // step_size = -lr / (1 - b1^s), bc2_sqrt = sqrt(1 - b2^s) come from ws):
   //   m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g;
-  //   p += (-lr/(1-b1^s)) * m / (sqrt(v)/sqrt(1-b2^s) + eps)
-  const double s = (double)*a.step;
+  //   p += step_size * m / (sqrt(v)/bc2_sqrt + eps)
   const double b1 = a.cfg.beta1, b2 = a.cfg.beta2;
   const float w1 = (float)(1.0 - b1);
   const float fb2 = (float)b2, w2 = (float)(1.0 - b2);
-  const float step_size = (float)(-(*a.lr / (1.0 - pow(b1, s))));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, s));
   const float eps = (float)a.cfg.eps;
-  const float g = a.g[i] * coef;
-  float m = a.m[i];
-  float v = a.v[i];
-  const float p = a.p[i];
+  g = g * coef;
   a.g[i] = g;
   m = m + w1 * (g - m);  // torch.lerp, weight < 0.5 branch
   v = v * fb2;
@@ -145,8 +147,9 @@ extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, flo
   return (int)hipGetLastError();
 }
 
-// The optimizer half of rx_ppo_minibatch_update: the step count was bumped and
-// the per-tensor sums of squares written (ws[nb][n_tensors]) by k_ppo_reduce.
+// The optimizer half of rx_ppo_minibatch_update: the step count was bumped,
+// the per-tensor sums of squares written (ws[nb][n_tensors]) and the two Adam
+// scalars after them by k_ppo_reduce.
 extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                                     const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s) {
   const int64_t n = cfg->offsets[cfg->n_tensors];

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rx.h"
+#include "rx_internal.h"
 #include "rx_policy.h"
 
 namespace {
@@ -609,8 +610,9 @@ constexpr int kRedBatch = 8;                    // partial rows loaded per threa
 // early-stop flag: the optimizer launch that follows needs no norm pass.
 struct norm_args {
   rx_adam_config cfg;
-  float* ws;    // [gridDim.x][n_tensors]
+  float* ws;    // [gridDim.x][n_tensors], then Adam's 2 step scalars
   float* step;  // Adam step count
+  const double* lr;
 };
 
 __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
@@ -704,7 +706,9 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
       *kl_at_stop = kl;
       *stop = 1;  // read by the optimizer launch that follows on the stream
     } else if (lane == 0 && norm_p) {
-      *norm.step += 1.0f;  // the Adam step this minibatch takes (k_adam_apply reads it)
+      const float st = *norm.step + 1.0f;  // the Adam step this minibatch takes
+      *norm.step = st;
+      rx_adam_scalars(norm.cfg, st, *norm.lr, norm.ws + (size_t)gridDim.x * norm.cfg.n_tensors);
     }
   }
 }
@@ -832,7 +836,7 @@ extern "C" int rx_ppo_reduce_blocks(int obs_dim) {
 
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
-                                  const rx_adam_config* cfg, float* norm_ws, float* step) {
+                                  const rx_adam_config* cfg, float* norm_ws, float* step, const double* lr) {
   const int rp = rows_per_wg(b->mb);
   const int n_wg = (b->mb + rp - 1) / rp;
   ppo_args a{*b, m, rp, stop, klp};
@@ -854,7 +858,7 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
   norm_args na{};
   const norm_args* np = nullptr;
   if (cfg) {
-    na = norm_args{*cfg, norm_ws, step};
+    na = norm_args{*cfg, norm_ws, step, lr};
     np = &na;  // only its non-nullness reaches the device: the struct travels by value
   }
   hipLaunchKernelGGL(k_ppo_reduce, dim3(rx_ppo_reduce_blocks(b->obs_dim)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp,

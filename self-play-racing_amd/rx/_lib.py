@@ -30,7 +30,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act",
            "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
-           "rx_state_import", "rx_state_export")
+           "rx_state_import", "rx_state_export", "rx_schedule")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -50,6 +50,9 @@ class RxConfig(ctypes.Structure):
 
 # rx_config launch-schedule fields (ABI v17): 0 = auto, -1 = off / none (include/rx.h).
 # Scheduling only: every value gives bit-identical results.
+SCHEDULE_W = 10  # rx_schedule: resolved schedule (include/rx.h)
+SCHEDULE_KEYS = ("split", "wide", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
+                 "dyn_waves", "ray_waves")
 SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants")
 
 
@@ -157,6 +160,7 @@ def load(build_if_missing=True):
     L.rx_env_order.argtypes = [_P, _P, _P, _P]
     L.rx_state_import.argtypes = [_P, _P]
     L.rx_state_export.argtypes = [_P, _P]
+    L.rx_schedule.argtypes = [_P, _P]
     L.rx_profile.argtypes = [_P, ctypes.c_int32]
     L.rx_profile_read.argtypes = [_P, _P, _P]
     for name in EXPORTS:

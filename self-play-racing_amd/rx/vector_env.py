@@ -322,6 +322,13 @@ class RacingVectorEnv:
                    "rx_env_order")
         return perm, bins.value, shift.value
 
+    def schedule(self):
+        """The launch schedule librx resolved for this env (rx_schedule): split step,
+        wide kernels, lanes per env / ray, argmin window, pre-filter, wave counts."""
+        out = np.zeros(_lib.SCHEDULE_W, np.int32)
+        _lib.check(self.L.rx_schedule(self._h, out.ctypes.data), "rx_schedule")
+        return {k: int(v) for k, v in zip(_lib.SCHEDULE_KEYS, out)}
+
     def get_state(self):
         return {k: v.cpu().numpy() for k, v in self.state.items() if v is not None}
 

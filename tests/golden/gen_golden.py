@@ -537,12 +537,14 @@ def _ppo_batch(torch, Agent, spaces, obs_dim, T, N, seed, log_std, adv_scale):
     return ag, dict(obs=obs, actions=act, logprobs=logp, values=val, advantages=adv, returns=ret)
 
 
-def gen_ppo_update():
+def gen_ppo_update(big=False):
     """G8: PPO.ppo_update (agent/ppo.py:156-209) run unbound on CPU torch.
 
     Cases: 'full' (2 epochs x 4 minibatches, no KL stop, obs 15), 'd19' (obs
     19, 3 x 2, larger lr), 'stop' (KL early stop inside epoch 2, at a
-    minibatch chosen from the KLs the unstopped run sees).  Recorded: the
+    minibatch chosen from the KLs the unstopped run sees) -> ppo_update.npz;
+    with ``big``: 'mb32k' (configs[1]'s minibatch size: 4,096 envs x 8 steps
+    in ONE 32,768-row minibatch, 2 epochs) -> ppo_update_mb32k.npz.  Recorded: the
     initial state_dict and batch, np.random state before/after, every
     optimizer step's gradient as Adam sees it (flat, parameter order,
     after clip_grad_norm_; the first two steps), the
@@ -609,6 +611,9 @@ def gen_ppo_update():
 
     out = {}
     cases = {
+        "mb32k": dict(obs_dim=15, T=8, N=4096, seed=14, log_std=-0.7, adv_scale=4.0, np_seed=8,
+                      cfg=dict(num_steps=8, num_envs=4096, update_epochs=2, num_minibatches=1, kl_target=1e9)),
+    } if big else {
         "full": dict(obs_dim=15, T=64, N=16, seed=11, log_std=-0.5, adv_scale=3.0, np_seed=5,
                      cfg=dict(num_steps=64, num_envs=16, update_epochs=2, num_minibatches=4, kl_target=1e9)),
         "d19": dict(obs_dim=19, T=32, N=16, seed=12, log_std=-0.9, adv_scale=8.0, np_seed=6,
@@ -658,7 +663,7 @@ def gen_ppo_update():
                 out[f"{tag}_{k}"] = v
         print(f"ppo_update {tag}: {len(grads)} optimizer steps, stop_at={kl_stop_at}, kl_target={c['kl_target']:.6g}")
     out["meta_torch"] = np.array(torch.__version__)
-    _save("ppo_update.npz", **out)
+    _save("ppo_update_mb32k.npz" if big else "ppo_update.npz", **out)
 
 
 def gen_schedules():
@@ -814,11 +819,13 @@ def gen_eval_metrics(track, racing_env):
 
 def main(argv):
     want = set(argv[1:]) or {"geometry", "raycast", "step_single", "traj_single", "step_multi", "gae", "agent",
-                             "ppo_update", "schedules", "eval_metrics"}
-    if want <= {"ppo_update", "schedules"}:
+                             "ppo_update", "ppo_update_mb32k", "schedules", "eval_metrics"}
+    if want <= {"ppo_update", "ppo_update_mb32k", "schedules"}:
         sys.path.insert(0, os.path.join(HERE, "_gym_stub"))
         if "ppo_update" in want:
             gen_ppo_update()
+        if "ppo_update_mb32k" in want:
+            gen_ppo_update(big=True)
         if "schedules" in want:
             gen_schedules()
         return
@@ -840,6 +847,8 @@ def main(argv):
         gen_agent()
     if "ppo_update" in want:
         gen_ppo_update()
+    if "ppo_update_mb32k" in want:
+        gen_ppo_update(big=True)
     if "schedules" in want:
         gen_schedules()
     if "eval_metrics" in want:

@@ -102,6 +102,23 @@ def test_65536_envs_subset_bit_exact_vs_oracle(oracle_dev):
     v.close()
 
 
+def test_4096_envs_configs1_geometry_subset_bit_exact_vs_oracle(oracle_dev):
+    """configs[1]'s env count on its own default launch geometry (the split step
+    with 4 lanes per ray task -- 16 tasks a ray wave -- and the REWARD half at 2
+    lanes per env, as rx_assign picks for 4,096 envs): 1,024 random envs == the
+    oracle bit for bit at every one of 200 steps (environment/racing_env.py:104-167)."""
+    from rx.vector_env import RacingVectorEnv
+    N = 4096
+    pool, widths = _seed1_pool(N)
+    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step")
+    sch = v.schedule()
+    assert (sch["split"], sch["wide"], sch["dyn_lpe"], sch["ray_lpr"], sch["reward_lpe"]) == (1, 0, 1, 4, 2), sch
+    idx = np.sort(np.random.default_rng(17).choice(N, 1024, replace=False))
+    ended = _single_run(v, idx, oracle_dev, 200, seed=19)
+    assert ended > 100
+    v.close()
+
+
 def test_one_env_hip_step_vs_oracle(oracle_dev):
     """configs[0]'s N = 1 on the HIP path (wide kernels): 1,500 steps, every step exact."""
     from rx.vector_env import RacingVectorEnv
@@ -142,18 +159,21 @@ def test_episode_statistics_all_shards_at_65536():
     v.close()
 
 
-def test_8192_two_car_subset_bit_exact_vs_oracle(oracle_dev):
-    """configs[3]'s env at 8,192 two-car envs (split step k_kin2 + k_step2<2>):
-    2,048 random envs == the oracle bit for bit over 200 steps.  On a reset the
-    start-slot order is drawn on the device (the reference draws it from the
-    global np.random, multi_racing_env.py:122-138): the oracle resets with the
-    order the device chose, which must be one of the two slot assignments."""
+@pytest.mark.parametrize("N,n_sub", [(8192, 2048), (4096, 1024)])
+def test_two_car_subset_bit_exact_vs_oracle(oracle_dev, N, n_sub):
+    """configs[3]'s env at 8,192 two-car envs (2 lanes per ray task: 16,384
+    cars) and at 4,096 (4 lanes per ray task), both on the split step k_kin2 +
+    k_step2<2>: a random subset == the oracle bit for bit over 200 steps.  On a reset the start-slot order is drawn on the device (the
+    reference draws it from the global np.random, multi_racing_env.py:122-138):
+    the oracle resets with the order the device chose, which must be one of the
+    two slot assignments."""
     from rx.vector_env import RacingVectorEnv
-    N = 8192
     pool, widths = _seed1_pool(N)
     v = RacingVectorEnv(pool, widths, n_agents=2, device="cuda", autoreset="next_step", seed=9)
+    sch = v.schedule()
+    assert sch["split"] == 1 and sch["wide"] == 0 and sch["ray_lpr"] == (4 if 2 * N <= 8192 else 2), sch
     tab = _oracle_table(v)
-    idx = np.sort(np.random.default_rng(5).choice(N, 2048, replace=False))
+    idx = np.sort(np.random.default_rng(5).choice(N, n_sub, replace=False))
     n = len(idx)
     st = multi_state(n)
     st["track"][:] = v.track_of_env[idx]
@@ -203,7 +223,7 @@ def test_8192_two_car_subset_bit_exact_vs_oracle(oracle_dev):
             g = v.get_state()
             for k in ("x", "y", "angle", "vx", "vy", "progress", "flags", "finished_step"):
                 assert np.array_equal(g[k].reshape(N, 2)[idx], st[k]), (t, k)
-    assert ended > 200
+    assert ended > 200 * n_sub // 2048
     v.close()
 
 

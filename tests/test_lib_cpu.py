@@ -78,7 +78,7 @@ def test_update_abi_validates_without_device():
     assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 0
     cfg.n_tensors, cfg.beta1, cfg.beta2 = 2, 0.9, 0.999
     cfg.offsets[1], cfg.offsets[2] = 1000, 2050
-    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 33 * 2  # ceil(2050 / 64) norm blocks x 2 tensors
+    assert L.rx_adam_workspace_floats(ctypes.byref(cfg)) == 33 * 2 + 2  # ceil(2050 / 64) norm blocks x 2 tensors + 2 scalars
     # fused minibatch update (ABI v13): argument checks before any launch
     assert L.rx_ppo_update_workspace_floats(15, ctypes.byref(cfg)) > 0
     assert L.rx_ppo_update_workspace_floats(7, ctypes.byref(cfg)) == 0

@@ -26,7 +26,7 @@ def _per_step(t, eps, obs, actions, logprobs, dones, rewards, values, next_obs, 
                            done_out=next_done if last else dones[s + 1])
 
 
-@pytest.mark.parametrize("n,T", [(16, 400), (200, 160)])
+@pytest.mark.parametrize("n,T", [(16, 400), (200, 160), (1, 2048)])
 def test_rollout_equals_per_step_path(n, T):
     ta, c = _train_single_style(num_envs=n, num_steps=T)
     tb, _ = _train_single_style(num_envs=n, num_steps=T)
@@ -128,3 +128,46 @@ def test_rollout_used_by_collect_rollout_and_trains():
     out = t.collect_rollout(*bufs, nobs, nd)
     assert torch.isfinite(out[2]).all() and torch.isfinite(out[5]).all()
     assert out[1].abs().max() <= 1.0
+
+
+def test_configs0_one_env_ppo_iteration():
+    """configs[0] ("1 env, from-scratch PPO"): one PPO iteration at num_envs = 1,
+    num_steps = 2048 (configs/base_config.py:5-27 otherwise) on the HIP path --
+    the rollout as ONE k_rollout workgroup (== the per-step path bit for bit:
+    test_rollout_equals_per_step_path[1-2048]), GAE, then 10 epochs x 16
+    minibatches of 128 rows through k_ppo_grad (graph-captured epochs) -- and
+    the same update on the same batch through the torch path (fused_policy =
+    fused_update = False: torch autograd + the flat Adam), agent/ppo.py:97-209.
+    Equal optimizer-step counts and np.random consumption; parameters within the
+    G8 float32 tolerance (tests/test_ppo_golden.py).  KL early stop off so a
+    borderline KL cannot split the two runs."""
+    T = 2048
+    ta, c = _train_single_style(num_envs=1, num_steps=T, kl_target=1e9)
+    tb, _ = _train_single_style(num_envs=1, num_steps=T, kl_target=1e9, fused_policy=False, fused_update=False)
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    assert ta._fused_rollout(T) is not None and tb._fused_rollout(T) is None
+    assert c["minibatch_size"] == 128
+    bufs = ta._buffers()
+    nobs = ta.envs.buf["obs"].clone()
+    nd = torch.zeros(1, device="cuda")
+    obs, actions, logprobs, dones, rewards, values, nobs, nd, ep = ta.collect_rollout(*bufs, nobs, nd)
+    assert float(dones.sum()) > 0, "no episode ended in 2,048 steps"
+    with torch.no_grad():
+        nv = ta.agent.get_value(nobs).flatten()
+    adv, ret = ta.compute_advantages(rewards, dones, values, nv, nd)
+    batch = [x.clone() for x in (adv, ret, values, logprobs, actions, obs)]
+    np.random.seed(123)
+    ta.ppo_update(*batch)
+    rng_a = np.random.get_state()
+    np.random.seed(123)
+    tb.ppo_update(*[x.clone() for x in batch])
+    rng_b = np.random.get_state()
+    torch.cuda.synchronize()
+    assert np.array_equal(rng_a[1], rng_b[1]) and rng_a[2] == rng_b[2]
+    n = int(float(ta._flat.step_t))
+    assert n == int(float(tb._flat.step_t)) == 160
+    lr = c["learning_rate"]
+    sa, sb = ta.agent.state_dict(), tb.agent.state_dict()
+    for k in sa:
+        np.testing.assert_allclose(sa[k].cpu().numpy(), sb[k].cpu().numpy(), rtol=1e-4, atol=0.02 * lr * n,
+                                   err_msg=k)
