@@ -382,6 +382,16 @@ int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_conf
  *                          rx_adam_clip_step that follows is skipped on every
  *                          rank alike. */
 int rx_ppo_adv_moments(const rx_ppo_batch* b, int32_t n_mb, double* moments, void* stream);
+/* ABI v17: rx_ppo_adv_stats / rx_ppo_adv_moments spread over many workgroups
+ * per minibatch (chunks of 2,048 rows, a partial-moment workspace ws of
+ * rx_ppo_adv_workspace_doubles(mb, n_mb) doubles, two launches: chunk moments,
+ * then a fold in chunk order).  Writes the raw (sum, square-sum) moments when
+ * `moments` is given (data parallel: all-reduce, then rx_ppo_adv_finalize),
+ * else (mean, unbiased std) into stats; moments -> rx_ppo_adv_finalize(count =
+ * mb) equals the stats output bit for bit.  Its own summation order: not
+ * bit-identical to rx_ppo_adv_stats. */
+size_t rx_ppo_adv_workspace_doubles(int32_t mb, int32_t n_mb);
+int rx_ppo_adv_stats_ws(const rx_ppo_batch* b, int32_t n_mb, double* ws, float* stats, double* moments, void* stream);
 int rx_ppo_adv_finalize(const double* moments, int32_t n_mb, int64_t count, float* stats, void* stream);
 int rx_ppo_minibatch_grad_shard(const rx_ppo_batch* b, int32_t m, float scale, float* ws_f32, double* ws_f64,
                                 float* grad, float* kl_out, const uint8_t* stop, void* stream);

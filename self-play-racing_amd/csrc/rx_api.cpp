@@ -966,6 +966,22 @@ int rx_ppo_adv_moments(const rx_ppo_batch* b, int32_t n_mb, double* moments, voi
   return RX_OK;
 }
 
+size_t rx_ppo_adv_workspace_doubles(int32_t mb, int32_t n_mb) {
+  return mb > 0 && n_mb > 0 ? 2 * (size_t)n_mb * (size_t)rx_adv_chunks(mb) : 0;
+}
+
+int rx_ppo_adv_stats_ws(const rx_ppo_batch* b, int32_t n_mb, double* ws, float* stats, double* moments, void* stream) {
+  int rc = check_ppo_batch(b);
+  if (rc) return rc;
+  if (n_mb <= 0 || !ws || (!stats && !moments))
+    return fail(RX_EINVAL, "rx_ppo_adv_stats_ws: n_mb=%d ws=%p stats=%p moments=%p", n_mb, (void*)ws, (void*)stats,
+                (void*)moments);
+  if ((int64_t)n_mb * b->mb > b->n_rows) return fail(RX_EINVAL, "rx_ppo_adv_stats_ws: n_mb*mb > n_rows");
+  if ((rc = rx_launch_adv_stats_ws(b, n_mb, ws, moments ? nullptr : stats, moments, (hipStream_t)stream)) != 0)
+    return fail(RX_EHIP, "adv stats launch failed: %s", hipGetErrorString((hipError_t)rc));
+  return RX_OK;
+}
+
 int rx_ppo_adv_finalize(const double* moments, int32_t n_mb, int64_t count, float* stats, void* stream) {
   if (n_mb <= 0 || count <= 0 || !moments || !stats)
     return fail(RX_EINVAL, "rx_ppo_adv_finalize: n_mb=%d count=%lld moments=%p stats=%p", n_mb, (long long)count,

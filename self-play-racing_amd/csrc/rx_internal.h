@@ -154,6 +154,9 @@ extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);
 extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, double* moments, hipStream_t s);
+extern "C" int rx_adv_chunks(int mb);
+extern "C" int rx_launch_adv_stats_ws(const rx_ppo_batch* b, int n_mb, double* ws, float* stats, double* moments,
+                                      hipStream_t s);
 extern "C" int rx_launch_adv_finalize(const double* moments, int n_mb, int64_t count, float* stats, hipStream_t s);
 extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_at_stop, hipStream_t s);
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,

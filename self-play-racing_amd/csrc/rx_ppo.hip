@@ -99,6 +99,25 @@ struct Geo {
   __device__ static constexpr int d_of(int s, int q) { return PREC == kBF16 ? 8 * q + s : 4 * s + q; }
 };
 
+// Profiling build only (-DRX_PPO_STAMPS, tools/ppo_stamps.py): per-wave
+// s_memtime stamps at k_ppo_grad's phase boundaries into a device array read
+// by rx_ppo_stamps_read (exported by that build only).  The product library has
+// no stamps.
+#ifdef RX_PPO_STAMPS
+constexpr int kStampW = 16, kStampMaxWaves = 8192;
+__device__ unsigned long long g_ppo_stamps[kStampMaxWaves * kStampW];
+#define PPO_STAMP(j)                                                                                       \
+  do {                                                                                                     \
+    const int sw_ = ((int)(blockIdx.y * gridDim.x + blockIdx.x) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6)); \
+    if ((threadIdx.x & 63) == 0 && sw_ < kStampMaxWaves && (j) < kStampW)                                \
+      g_ppo_stamps[sw_ * kStampW + (j)] = __builtin_amdgcn_s_memtime();                                   \
+  } while (0)
+#else
+#define PPO_STAMP(j) \
+  do {               \
+  } while (0)
+#endif
+
 struct ppo_args {
   rx_ppo_batch b;
   int32_t m;            // minibatch index within the epoch
@@ -360,6 +379,8 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   for (int e = t0; e < NOUT * 64; e += kT) lds[S::W3 + e] = W[oW3 + e];
   if (t0 < NOUT) lds[S::B3 + t0] = W[ob3 + t0];
   __syncthreads();
+  PPO_STAMP(1);
+  int pass_ = 0;
   const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
   float* sZ = lds + S::SZ;  // [hidden][row]
   float* sH = lds + S::SH;  // [hidden][row]
@@ -429,6 +450,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       for (int j = 0; j < NOUT; ++j) sG[rr * kNA + j] = g[j];
     }
     __syncthreads();
+    PPO_STAMP(2 + 4 * pass_);
     // ================================================================ B
     // dW2[16 wv + i][16 nt + c] += sum_rows dZ2 x H1 (k = row 4s + q; bf16: row 32s + 8q + j)
     if constexpr (PREC == kBF16) {
@@ -481,6 +503,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       }
     }
     __syncthreads();
+    PPO_STAMP(3 + 4 * pass_);
     // ================================================================ C
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -491,6 +514,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
         sH[h * kTS + rr] = H2[t][r];
       }
     __syncthreads();
+    PPO_STAMP(4 + 4 * pass_);
     // ================================================================ D
     // dW1[16 wv + i][d] (+ db1 at d = D) += sum_rows dZ1 x [X | 1]
     if constexpr (PREC == kBF16) {
@@ -531,11 +555,14 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       if (lane < NOUT) db3 += sG[row * kNA + lane];
     }
     __syncthreads();  // the next pass overwrites the transposes
+    PPO_STAMP(5 + 4 * pass_);
+    ++pass_;
     src = src_n;
     src_n = src_nn;
     cur = nxt;
   }
   // ---- tile accumulators -> the partial row (each wave owns rows [16 wv, 16 wv + 16))
+  PPO_STAMP(14);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int o = 16 * wv + 4 * q + r;
@@ -560,6 +587,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   if (lane < NOUT) small[64 + kNA * 64 + lane] = db3;
   if (lane == 0) reinterpret_cast<double*>(small + 64 + kNA * 64 + kNA)[0] = kl;  // 8-aligned: SMALL_PER is even
   __syncthreads();
+  PPO_STAMP(15);
   if (wv != 0) return;
   const float* sm = lds + S::SMALL;
   for (int e = lane; e < 64 + NOUT * 64 + NOUT; e += 64) {
@@ -585,6 +613,7 @@ template <int D, int PREC>
 __global__ __launch_bounds__(kT, RX_PPO_MINW) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
                                                     float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
+  PPO_STAMP(0);
   __shared__ __attribute__((aligned(16))) float lds[GradLds<D>::TOTAL];
   float* out = partial + (size_t)blockIdx.x * Lay<D>::Pp;
   if (blockIdx.y == 0)
@@ -775,6 +804,73 @@ __global__ __launch_bounds__(1024) void k_adv_stats(const float* __restrict__ ad
   }
 }
 
+// The same statistics spread over many workgroups (ABI v17, rx_ppo_adv_stats_ws):
+// minibatch m is cut into chunks of kAdvChunk rows, one 256-thread workgroup
+// each (thread t adds rows t, t + 256, ... of its chunk in order, every perm
+// index and then every gathered advantage of its 8 rows in flight at once; a
+// 64-lane xor tree, the 4 waves in order), which writes the chunk's (sum,
+// square-sum) to ws[m][c]; k_adv_fold then adds a minibatch's chunks in chunk
+// order.  n_mb * n_chunks workgroups gather instead of n_mb.
+constexpr int kAdvChunk = 2048, kAdvT = 256, kAdvPer = kAdvChunk / kAdvT;
+
+__global__ __launch_bounds__(kAdvT) void k_adv_chunk(const float* __restrict__ adv, const int64_t* __restrict__ perm,
+                                                     int mb, int64_t n_rows, int n_chunks, double* __restrict__ ws) {
+  __shared__ double red[2][kAdvT / 64];
+  const int m = blockIdx.x / n_chunks, c = blockIdx.x - m * n_chunks;
+  const int r0 = c * kAdvChunk, r1 = min(mb, r0 + kAdvChunk);
+  const int64_t base = (int64_t)m * mb;
+  int64_t k[kAdvPer];
+#pragma unroll
+  for (int j = 0; j < kAdvPer; ++j) {
+    const int r = r0 + threadIdx.x + kAdvT * j;
+    k[j] = r < r1 ? perm[base + r] : -1;
+  }
+  double x[kAdvPer];
+#pragma unroll
+  for (int j = 0; j < kAdvPer; ++j) x[j] = (k[j] >= 0 && k[j] < n_rows) ? (double)adv[k[j]] : 0.0;
+  double s = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < kAdvPer; ++j) {
+    s += x[j];
+    s2 += x[j] * x[j];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, q = 0.0;
+    for (int w = 0; w < kAdvT / 64; ++w) {
+      a += red[0][w];
+      q += red[1][w];
+    }
+    ws[2 * (size_t)blockIdx.x] = a;
+    ws[2 * (size_t)blockIdx.x + 1] = q;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_adv_fold(const double* __restrict__ ws, int n_mb, int n_chunks, int mb,
+                                                 float* stats, double* moments) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n_mb) return;
+  double a = 0.0, q = 0.0;
+  for (int c = 0; c < n_chunks; ++c) {
+    a += ws[2 * ((size_t)i * n_chunks + c)];
+    q += ws[2 * ((size_t)i * n_chunks + c) + 1];
+  }
+  if (moments) {
+    moments[2 * i] = a;
+    moments[2 * i + 1] = q;
+  } else {
+    adv_write(a, q, (double)mb, stats, i);
+  }
+}
+
 // (mean, unbiased std) of every minibatch from all-reduced moments over ``count`` rows.
 __global__ __launch_bounds__(64) void k_adv_finalize(const double* __restrict__ moments, int n_mb, double count,
                                                      float* stats) {
@@ -819,6 +915,17 @@ extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats
   return (int)hipGetLastError();
 }
 
+extern "C" int rx_adv_chunks(int mb) { return (mb + kAdvChunk - 1) / kAdvChunk; }
+
+extern "C" int rx_launch_adv_stats_ws(const rx_ppo_batch* b, int n_mb, double* ws, float* stats, double* moments,
+                                      hipStream_t s) {
+  const int nc = rx_adv_chunks(b->mb);
+  hipLaunchKernelGGL(k_adv_chunk, dim3(n_mb * nc), dim3(kAdvT), 0, s, b->advantages, b->perm, b->mb, b->n_rows, nc,
+                     ws);
+  hipLaunchKernelGGL(k_adv_fold, dim3((n_mb + 63) / 64), dim3(64), 0, s, ws, n_mb, nc, b->mb, stats, moments);
+  return (int)hipGetLastError();
+}
+
 extern "C" int rx_launch_adv_finalize(const double* moments, int n_mb, int64_t count, float* stats, hipStream_t s) {
   hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(64), 0, s, moments, n_mb, (double)count, stats);
   return (int)hipGetLastError();
@@ -828,6 +935,17 @@ extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* sto
   hipLaunchKernelGGL(k_kl_check, dim3(1), dim3(64), 0, s, kl, kl_target, stop, kl_at_stop);
   return (int)hipGetLastError();
 }
+
+#ifdef RX_PPO_STAMPS
+// profiling build: copy the stamp array out ([kStampMaxWaves][kStampW] u64)
+extern "C" int rx_ppo_stamps_read(unsigned long long* out, int n_waves) {
+  const size_t n = (size_t)(n_waves < kStampMaxWaves ? n_waves : kStampMaxWaves) * kStampW;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ppo_stamps), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  static unsigned long long zero[kStampMaxWaves * kStampW];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ppo_stamps), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int rx_ppo_reduce_blocks(int obs_dim) {
   const int Pp = obs_dim == 15 ? Lay<15>::Pp : Lay<19>::Pp;

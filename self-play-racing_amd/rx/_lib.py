@@ -30,7 +30,8 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_ppo_workspace_doubles", "rx_ppo_adv_stats", "rx_ppo_minibatch_grad", "rx_policy_act",
            "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
-           "rx_state_import", "rx_state_export", "rx_schedule")
+           "rx_state_import", "rx_state_export", "rx_schedule",
+           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -161,11 +162,15 @@ def load(build_if_missing=True):
     L.rx_state_import.argtypes = [_P, _P]
     L.rx_state_export.argtypes = [_P, _P]
     L.rx_schedule.argtypes = [_P, _P]
+    L.rx_ppo_adv_workspace_doubles.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    L.rx_ppo_adv_workspace_doubles.restype = ctypes.c_size_t
+    L.rx_ppo_adv_stats_ws.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P, _P, _P]
     L.rx_profile.argtypes = [_P, ctypes.c_int32]
     L.rx_profile_read.argtypes = [_P, _P, _P]
     for name in EXPORTS:
         if name not in ("rx_last_error", "rx_abi_version", "rx_ppo_workspace_floats", "rx_ppo_workspace_doubles",
-                        "rx_ppo_update_workspace_floats", "rx_adam_workspace_floats"):
+                        "rx_ppo_update_workspace_floats", "rx_adam_workspace_floats",
+                        "rx_ppo_adv_workspace_doubles"):
             getattr(L, name).restype = ctypes.c_int
     if L.rx_abi_version() != ABI_VERSION:
         raise RxError(f"librx ABI {L.rx_abi_version()} != {ABI_VERSION} (rebuild: python -m rx._build)")

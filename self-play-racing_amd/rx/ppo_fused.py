@@ -3,7 +3,7 @@
 ``FusedMinibatchGrad`` binds one flattened rollout (obs, actions, logprobs,
 advantages, returns, values -- persistent buffers), the flat policy
 parameters of rx.optim.FlatAdam and the epoch's index tensor, and issues per
-epoch: one rx_ppo_adv_stats launch (every minibatch's advantage mean/std),
+epoch: one rx_ppo_adv_stats_ws call (every minibatch's advantage mean/std),
 then per minibatch rx_ppo_minibatch_update (forward + loss + backward,
 split-K reduce + KL check + clip norms, Adam).  Everything is enqueued on
 the current stream with no host sync, so PPO captures an epoch as one graph.
@@ -49,6 +49,9 @@ class FusedMinibatchGrad:
         self.stats = torch.zeros(2 * self.n_mb, dtype=torch.float32, device=dev)
         self.ws_f = torch.empty(L.rx_ppo_workspace_floats(D, mb), dtype=torch.float32, device=dev)
         self.ws_d = torch.empty(L.rx_ppo_workspace_doubles(mb), dtype=torch.float64, device=dev)
+        # partial advantage moments (rx_ppo_adv_stats_ws), sized for every epoch's minibatches at once
+        self.adv_ws = torch.empty(L.rx_ppo_adv_workspace_doubles(mb, max(1, int(config["update_epochs"])) * self.n_mb),
+                                  dtype=torch.float64, device=dev)
         self.flat = flat
         self._keep = (b, perm, agent.log_std)  # the struct holds raw pointers into these
         self.batch = _lib.RxPPOBatch(D, mb, B, _lib.ptr(obs), _lib.ptr(actions), _lib.ptr(logprobs),
@@ -58,8 +61,10 @@ class FusedMinibatchGrad:
                                      precision(config))
 
     def adv_stats(self, stream=None):
-        _lib.check(self.L.rx_ppo_adv_stats(self.batch, self.n_mb, _lib.ptr(self.stats), _lib.stream_ptr(stream)),
-                   "rx_ppo_adv_stats")
+        """Every minibatch's advantage (mean, unbiased std) for the current perm:
+        rx_ppo_adv_stats_ws, chunks of 2,048 rows on their own workgroups."""
+        _lib.check(self.L.rx_ppo_adv_stats_ws(self.batch, self.n_mb, _lib.ptr(self.adv_ws), _lib.ptr(self.stats), None,
+                                              _lib.stream_ptr(stream)), "rx_ppo_adv_stats_ws")
 
     def grad(self, m, stop, kl_at_stop, stream=None):
         _lib.check(self.L.rx_ppo_minibatch_grad(self.batch, int(m), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
@@ -76,7 +81,8 @@ class FusedMinibatchGrad:
         mom = self.__dict__.get("moments")
         if mom is None:
             mom = self.moments = torch.empty((self.n_mb, 2), dtype=torch.float64, device=self.stats.device)
-        _lib.check(L.rx_ppo_adv_moments(self.batch, self.n_mb, _lib.ptr(mom), s), "rx_ppo_adv_moments")
+        _lib.check(L.rx_ppo_adv_stats_ws(self.batch, self.n_mb, _lib.ptr(self.adv_ws), None, _lib.ptr(mom), s),
+                   "rx_ppo_adv_stats_ws")
         all_reduce(mom)
         _lib.check(L.rx_ppo_adv_finalize(_lib.ptr(mom), self.n_mb, self.mb * world, _lib.ptr(self.stats), s),
                    "rx_ppo_adv_finalize")
@@ -115,7 +121,7 @@ class FusedMinibatchGrad:
             self.update(m, stop, kl_at_stop)
 
     def epochs_stats(self, perms, stats_out, stream=None):
-        """Advantage statistics of E epochs in ONE rx_ppo_adv_stats launch:
+        """Advantage statistics of E epochs in ONE rx_ppo_adv_stats_ws call:
         ``perms`` int64 [E, B] (one permutation per epoch), ``stats_out``
         float32 [E, n_mb, 2].  Workgroup e * n_mb + m sums minibatch m of epoch
         e exactly as the per-epoch launch does (same rows, same order), so the
@@ -127,8 +133,11 @@ class FusedMinibatchGrad:
         b.perm = _lib.ptr(perms)
         b.n_rows = E * B
         self._keep_epochs = (perms, stats_out)
-        _lib.check(self.L.rx_ppo_adv_stats(b, E * self.n_mb, _lib.ptr(stats_out), _lib.stream_ptr(stream)),
-                   "rx_ppo_adv_stats")
+        need = self.L.rx_ppo_adv_workspace_doubles(self.mb, E * self.n_mb)
+        if self.adv_ws.numel() < need:
+            self.adv_ws = torch.empty(need, dtype=torch.float64, device=self.adv_ws.device)
+        _lib.check(self.L.rx_ppo_adv_stats_ws(b, E * self.n_mb, _lib.ptr(self.adv_ws), _lib.ptr(stats_out), None,
+                                              _lib.stream_ptr(stream)), "rx_ppo_adv_stats_ws")
 
 
 def RxPPOBatch_copy(b):

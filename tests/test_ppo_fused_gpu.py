@@ -272,3 +272,34 @@ def test_adv_moments_finalize_equals_adv_stats():
     a = adv.double()[perm].view(B // mb, mb)
     ref = torch.stack([a.mean(1), a.std(1)], 1).reshape(-1).float()
     torch.testing.assert_close(st3, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,mb", [(4096, 512), (524288, 32768), (2048, 128)])
+def test_adv_stats_ws_spread_over_workgroups(B, mb):
+    """rx_ppo_adv_stats_ws (ABI v17: 2,048-row chunks on their own workgroups,
+    then a fold in chunk order): == float64 statistics of each minibatch of the
+    permuted advantages within float32 rounding (agent/ppo.py:186-187), and its
+    moments -> rx_ppo_adv_finalize(count = mb) == its stats bit for bit."""
+    from rx import _lib
+    L = _lib.load()
+    D = 15
+    obs, act, logp, adv, ret, val = _batch(B, D, seed=5)
+    perm = torch.randperm(B, device="cuda")
+    params = torch.zeros(L.rx_ppo_n_params(D), device="cuda")
+    log_std = torch.zeros(2, device="cuda")
+    n_mb = B // mb
+    stats = torch.zeros(2 * n_mb, device="cuda")
+    b = _lib.RxPPOBatch(D, mb, B, *[_lib.ptr(t) for t in (obs, act, logp, adv, ret, val, perm, params, log_std,
+                                                           stats)], 0.2, 0.5, 0.015)
+    ws = torch.empty(L.rx_ppo_adv_workspace_doubles(mb, n_mb), dtype=torch.float64, device="cuda")
+    assert ws.numel() == 2 * n_mb * max(1, mb // 2048)
+    s = _lib.stream_ptr()
+    _lib.check(L.rx_ppo_adv_stats_ws(b, n_mb, _lib.ptr(ws), _lib.ptr(stats), None, s), "adv_stats_ws")
+    a = adv.double()[perm].view(n_mb, mb)
+    ref = torch.stack([a.mean(1), a.std(1)], 1).reshape(-1).float()
+    torch.testing.assert_close(stats, ref, rtol=1e-6, atol=1e-6)
+    mom = torch.zeros((n_mb, 2), dtype=torch.float64, device="cuda")
+    _lib.check(L.rx_ppo_adv_stats_ws(b, n_mb, _lib.ptr(ws), None, _lib.ptr(mom), s), "adv_moments_ws")
+    st2 = torch.zeros_like(stats)
+    _lib.check(L.rx_ppo_adv_finalize(_lib.ptr(mom), n_mb, mb, _lib.ptr(st2), s), "finalize")
+    assert torch.equal(stats, st2)
