@@ -362,22 +362,40 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     }
     return in;
   };
-  // the first pass's row gathers are issued before the weight staging, so
-  // the two memory latencies overlap
+  // ---- stage the trunk's weights (zero-padded rows) while the first pass's
+  // rows are gathered.  Issue order matters (vector loads complete in order):
+  // the perm indices first, then EVERY staging load into registers, then the
+  // row gathers (which wait only for the perm loads), then the LDS stores --
+  // one memory latency for all of it instead of one round trip per staged
+  // element (stamps: staging 11 k -> see DESIGN.md §3, k_ppo_grad)
   int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
+  constexpr int kW1N = (64 * G::DP + kT - 1) / kT, kW2N = 64 * 64 / kT;
+  float w1v[kW1N], w2v[kW2N], bv[2];
+#pragma unroll
+  for (int j = 0; j < kW1N; ++j) {
+    const int e = t0 + kT * j, o = e / G::DP, d = e - o * G::DP;
+    w1v[j] = (e < 64 * G::DP && d < D) ? W[oW1 + o * D + d] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < kW2N; ++j) w2v[j] = W[oW2 + t0 + kT * j];
+  bv[0] = t0 < 64 ? W[ob1 + t0] : (t0 < 128 ? W[ob2 + t0 - 64] : 0.0f);
+  bv[1] = t0 < NOUT * 64 ? W[oW3 + t0] : 0.0f;
+  const float b3v = t0 < NOUT ? W[ob3 + t0] : 0.0f;
   RowIn cur = load_row(src);
-  // ---- stage the trunk's weights (zero-padded rows)
-  for (int e = t0; e < 64 * G::DP; e += kT) {
-    const int o = e / G::DP, d = e - o * G::DP;
-    lds[S::W1 + e] = d < D ? W[oW1 + o * D + d] : 0.0f;
+#pragma unroll
+  for (int j = 0; j < kW1N; ++j)
+    if (t0 + kT * j < 64 * G::DP) lds[S::W1 + t0 + kT * j] = w1v[j];
+#pragma unroll
+  for (int j = 0; j < kW2N; ++j) {
+    const int e = t0 + kT * j;
+    lds[S::W2 + (e >> 6) * kWS + (e & 63)] = w2v[j];
   }
-  for (int e = t0; e < 64 * 64; e += kT) lds[S::W2 + (e >> 6) * kWS + (e & 63)] = W[oW2 + e];
-  for (int e = t0; e < 64; e += kT) {
-    lds[S::B1 + e] = W[ob1 + e];
-    lds[S::B2 + e] = W[ob2 + e];
-  }
-  for (int e = t0; e < NOUT * 64; e += kT) lds[S::W3 + e] = W[oW3 + e];
-  if (t0 < NOUT) lds[S::B3 + t0] = W[ob3 + t0];
+  if (t0 < 64)
+    lds[S::B1 + t0] = bv[0];
+  else if (t0 < 128)
+    lds[S::B2 + t0 - 64] = bv[0];
+  if (t0 < NOUT * 64) lds[S::W3 + t0] = bv[1];
+  if (t0 < NOUT) lds[S::B3 + t0] = b3v;
   __syncthreads();
   PPO_STAMP(1);
   int pass_ = 0;
