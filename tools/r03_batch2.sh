@@ -2,7 +2,7 @@
 # Round 3, second GPU batch: full -m gpu suite + smoke (tools/r03_check.sh), the
 # first-launch probe, k_ppo_grad stamps with the batched weight staging, a
 # same-session A/B of the fused minibatch step (tree vs librx_r03a = HEAD before the
-# staging change), a rocprofv3 kernel summary of the tree's step, and the 2-rank gloo
+# staging change, librx_r03b = staging without the exp-form tanh), a rocprofv3 kernel summary of the tree's step, and the 2-rank gloo
 # rehearsal of bench.py's own launcher on this one GPU.
 set -u
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r03; mkdir -p $OUT; export TMPDIR=/tmp
@@ -14,7 +14,7 @@ bash tools/r03_stamps.sh || exit 1
 : > $OUT/ppo_micro_ab.jsonl
 for rep in 1 2; do
   for prec in fp32 bf16; do
-    for lib in librx.so librx_r03a.so; do
+    for lib in librx.so librx_r03b.so librx_r03a.so; do
       RX_LIB_PATH=$LIB/$lib timeout -k 10 120 python tools/ppo_micro.py 32768 $prec $lib >> $OUT/ppo_micro_ab.jsonl 2> $OUT/ppo_micro.err || { tail -5 $OUT/ppo_micro.err; exit 1; }
       tail -1 $OUT/ppo_micro_ab.jsonl
     done
