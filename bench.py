@@ -622,6 +622,8 @@ def main():
         t0 = time.perf_counter()
         for k in range(steps):
             one_step(events.get(k) if events else None)
+            if k == 0:
+                mark("first_step_issued")  # diagnostics only (RX_BENCH_MARKS): host time of the first launch
         torch.cuda.synchronize()  # all streams
         gc.enable()
         if dist:

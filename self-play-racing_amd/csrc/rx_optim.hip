@@ -90,26 +90,49 @@ __global__ __launch_bounds__(kT) void k_adam_apply(adam_args a) {
   if (a.cfg.max_grad_norm > 0.0) {
     // torch.nn.utils.clip_grad_norm_: total = ||(||g_0||, ..., ||g_k||)||_2,
     // coef = clamp(max_norm / (total + 1e-6), max=1), grads *= coef.
-    // Wave w folds tensors w, w + 4, ...: lane l adds the tensor's blocks
-    // b = l (mod 64) in ascending order, a 64-lane xor tree finishes.  Only the
-    // blocks the tensor overlaps are read: every other partial row holds an
-    // exact 0 for it, so the sums equal a sweep over all nb rows bit for bit,
-    // at nb + n_t loads instead of nb * n_t.
+    // Thread group u (16 lanes, u < n_t) folds tensor u: lane j adds the
+    // tensor's norm blocks b = b_lo + j, b_lo + j + 16, ... in ascending order
+    // (every load of the fold in flight at once: one memory round trip), then a
+    // 16-lane xor tree.  Only the blocks the tensor overlaps are read -- every
+    // other partial row holds an exact 0 for it -- at nb + n_t loads instead of
+    // nb * n_t.  Every workgroup folds identically.
     __shared__ float norms[RX_ADAM_MAX_TENSORS];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int u = wave; u < n_t; u += kT / 64) {
+    constexpr int kFold = 8;  // blocks per lane in flight (tensors of up to 16 * 8 * 64 entries in one round)
+    const int u = threadIdx.x >> 4, j = threadIdx.x & 15;
+    float l = 0.0f;
+    if (u < n_t) {
       const int64_t lo = a.cfg.offsets[u], hi = a.cfg.offsets[u + 1];
-      float l = 0.0f;
       if (hi > lo) {
         const int b_lo = (int)(lo / kNormBlock), b_hi = (int)((hi - 1) / kNormBlock);
-        for (int b = b_lo + ((lane - b_lo) & 63); b <= b_hi; b += 64) l += a.ws[(size_t)b * n_t + u];
+        for (int b0 = b_lo + j; b0 <= b_hi; b0 += 16 * kFold) {
+          float v[kFold];
+#pragma unroll
+          for (int k = 0; k < kFold; ++k) {
+            const int b = b0 + 16 * k;
+            v[k] = b <= b_hi ? a.ws[(size_t)b * n_t + u] : 0.0f;
+          }
+#pragma unroll
+          for (int k = 0; k < kFold; ++k) l += v[k];
+        }
       }
-      for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
-      if (lane == 0) norms[u] = sqrtf(l);
+    }
+    for (int o = 1; o < 16; o <<= 1) l += __shfl_xor(l, o, 16);
+    if (j == 0 && u < n_t) norms[u] = sqrtf(l);
+    if (n_t > kT / 16) {  // more tensors than 16-lane groups (rx.h allows 32): the rest, one group each, in turn
+      for (int u2 = u + kT / 16; u2 < n_t; u2 += kT / 16) {
+        const int64_t lo = a.cfg.offsets[u2], hi = a.cfg.offsets[u2 + 1];
+        float l2 = 0.0f;
+        if (hi > lo) {
+          const int b_lo = (int)(lo / kNormBlock), b_hi = (int)((hi - 1) / kNormBlock);
+          for (int b = b_lo + j; b <= b_hi; b += 16) l2 += a.ws[(size_t)b * n_t + u2];
+        }
+        for (int o = 1; o < 16; o <<= 1) l2 += __shfl_xor(l2, o, 16);
+        if (j == 0) norms[u2] = sqrtf(l2);
+      }
     }
     __syncthreads();
     float tot2 = 0.0f;
-    for (int u = 0; u < n_t; ++u) tot2 += norms[u] * norms[u];
+    for (int t = 0; t < n_t; ++t) tot2 += norms[t] * norms[t];
     const float total = sqrtf(tot2);
     coef = fminf((float)a.cfg.max_grad_norm / (total + 1e-6f), 1.0f);
   } else {

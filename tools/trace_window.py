@@ -35,6 +35,7 @@ def main():
     for r in csv.DictReader(open(trace)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
+    fsm = [m for m in marks if m[0] == "first_step_issued"]
     t0m = [m for m in marks if m[0] == "t0"][0]
     t1m = [m for m in marks if m[0] == "t1"][0]
     # pick the clock the trace uses: the one whose t0 lies within the trace span
@@ -68,6 +69,8 @@ def main():
         "idle_gaps_us": round(sum(max(g, 0) for g in gaps) / 1e3, 2),
         "largest_gaps_us": sorted((round(g / 1e3, 2) for g in gaps), reverse=True)[:5],
         "last_kernel_to_t1_us": round((t1 - win[-1][1]) / 1e3, 2),
+        "t0_to_first_step_issued_us": (round((fsm[0][1 if res["clock"] == "boottime" else 2] - t0) / 1e3, 2)
+                                       if fsm else None),
         "kernels_in_region": per(win),
         "same_kernels_after_region": per(after),
         "sort_in_region": any(n.startswith("k_sort") for _, _, n in win),
