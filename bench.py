@@ -516,6 +516,9 @@ def main():
                     help="launch-schedule overrides for A/B runs, 'key=value,...' over rx_config's ABI v17 fields "
                          "(split, wide_n, dyn_lpe, ray_lpr, reward_lpe, argmin_window, seg_filter, box_quadrants; "
                          "0 = auto, -1 = off); scheduling only, results are identical")
+    ap.add_argument("--sync", choices=("spin", "block"), default="spin",
+                    help="how the host waits at the timed region's edges: spin on the streams' queues, then "
+                         "torch.cuda.synchronize() (default), or the blocking synchronize alone")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, reports its device and "
                          "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
@@ -605,13 +608,28 @@ def main():
                         envs[g].step_device(acts[g][k], phases=1)
                         envs[g].step_device(acts[g][k], phases=2)
                         envs[g].profile(0)
+        active["streams"] = streams
         return envs, one_step, n
 
-    def sync_all():
+    active = {"streams": [torch.cuda.current_stream(dev)]}
+
+    def drain():
+        """torch.cuda.synchronize(), after spinning on the active streams until
+        their queues are empty (--sync spin, default): a blocking synchronize
+        parks the host thread, and the first launch after the wake-up took
+        120-270 us of host time in the 20-step region against ~30 us for the
+        next ones (tools/first_launch_probe.py, profiles/r03/); spinning first
+        keeps the thread awake, the synchronize itself then returns at once."""
+        if args.sync == "spin":
+            while not all(st.query() for st in active["streams"]):
+                pass
         torch.cuda.synchronize()
+
+    def sync_all():
+        drain()
         if dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        drain()
 
     def timed(one_step, steps, events=None, collect=True):
         sync_all()
@@ -620,17 +638,21 @@ def main():
         gc.disable()  # a full collection over the 65,536-track pool stalls the host for tens of ms
         mark("t0")
         t0 = time.perf_counter()
+        tk = []
         for k in range(steps):
             one_step(events.get(k) if events else None)
-            if k == 0:
-                mark("first_step_issued")  # diagnostics only (RX_BENCH_MARKS): host time of the first launch
-        torch.cuda.synchronize()  # all streams
+            if k < 4 and _MARKS:
+                tk.append(time.perf_counter())  # diagnostics only: host time of the first launches
+        drain()  # all streams
         gc.enable()
         if dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        drain()
         el = time.perf_counter() - t0
         mark("t1")
+        if _MARKS and tk:
+            print("RX_FIRST_STEPS_US " + " ".join(f"{(b - a) * 1e6:.1f}" for a, b in zip([t0] + tk, tk)),
+                  file=sys.stderr, flush=True)
         if dist:
             t = torch.tensor([el], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -645,16 +667,26 @@ def main():
     # BEFORE the last --refill of them: it stalls the host for tens of ms, the GPU idles
     # and drops its clock meanwhile, and the refill steps bring it back under load
     # (timing starts with a queue-drain sync, as always)
+    # The pre-timing sequence (sync, episode-statistics read, sync) runs twice: the
+    # first time that sequence runs in a process, the host's first launch after it
+    # takes 150-220 us instead of ~40 (tools/first_step_breakdown.py: every part of
+    # the call is 5-10x slower, a cold-start effect, gone from the second region on),
+    # and the GPU idles meanwhile.  All of it is untimed.
     refill = max(0, min(args.refill, untimed))
     for _ in range(untimed - refill):
         one_step()
+    ep_untimed = [0.0, 0.0, 0]
     if refill:
         gc.collect()
         gc.disable()
-        for _ in range(refill):
-            one_step()
-    sync_all()
-    ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
+        for half in (refill // 2, refill - refill // 2):
+            for _ in range(half):
+                one_step()
+            sync_all()
+            ep_untimed = [a + b for a, b in zip(ep_untimed, (sum(x) for x in zip(*(e.episode_stats() for e in envs))))]
+    else:
+        sync_all()
+        ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- timed region: production steps only (one rx_step per step, no instrumentation)
     elapsed = timed(one_step, args.steps, collect=refill == 0)
     ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
