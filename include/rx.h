@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 17
+#define RX_ABI_VERSION 18
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -255,6 +255,15 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
 #define RX_KERNEL_KINDS 5
 int rx_profile(rx_env* h, int32_t enable);
 int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count);
+/* Diagnostics (ABI v18): the raw per-wave stamps of recorded launch `launch`
+ * (0-based, record order; synchronises).  *n_waves = the launch's wave slots
+ * (wave index = workgroup index for k_step2: REWARD waves first, then the ray
+ * waves); start[i] / end[i] = device wall-clock ticks (0 = no wave in that
+ * slot) for i < min(*n_waves, cap); *kind = its RX_KERNEL_*; *khz = the clock
+ * rate.  Used to see how a launch's waves fill the chip over time (tail,
+ * per-wave cost by dispatch order).  No counterpart in the reference. */
+int rx_profile_waves(rx_env* h, int32_t launch, uint64_t* start, uint64_t* end, int32_t cap, int32_t* n_waves,
+                     int32_t* kind, int32_t* khz);
 
 /* GAE (agent/ppo.py:134-154), float32, bit-exact lane-per-env recurrence.
  * rewards/values/dones [T][N]; next_value/next_done [N]; adv/returns [T][N]. */

@@ -510,9 +510,36 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     for (size_t g = 0; g < n_groups; ++g) maxw = std::max(maxw, ray_groups[g] - (g ? ray_groups[g - 1] : 0));
     const size_t padded = (n_groups + 7) / 8 * 8;
     std::vector<rx_wave> placed(padded * maxw, rx_wave{0, 0, 0, 0});
+    // RX_RAY_DISPATCH (rx_internal.h): 0 = group-octet-major as just described; 1..3 =
+    // class-major, every group's class-j wave in one run, the classes in the order
+    // 1 centre first (|2j - (maxw - 1)| ascending), 2 ascending j, 3 edge classes first
+    // (|2j - (maxw - 1)| descending, the default).  The XCD of a group's waves is g % 8 in
+    // every mode (padded is a multiple of 8).  Dispatch order is scheduling only.
+    std::vector<int> rank(maxw);
+    std::iota(rank.begin(), rank.end(), 0);
+    if (RX_RAY_DISPATCH == 1 || RX_RAY_DISPATCH == 3) {
+      std::vector<int> cls(maxw);
+      std::iota(cls.begin(), cls.end(), 0);
+      auto off = [&](int j) { return std::abs(2 * j - (maxw - 1)); };
+      std::stable_sort(cls.begin(), cls.end(), [&](int x, int y) {
+        return RX_RAY_DISPATCH == 1 ? off(x) < off(y) : off(x) > off(y);
+      });
+      for (int r = 0; r < maxw; ++r) rank[cls[r]] = r;
+    }
+#ifdef RX_RAY_ORDER_LIST
+    {  // A/B builds: an explicit class order for 11-class groups (RX_RAY_DISPATCH >= 1)
+      const int lst[] = RX_RAY_ORDER_LIST;
+      if (RX_RAY_DISPATCH >= 1 && maxw == (int)(sizeof(lst) / sizeof(lst[0])))
+        for (int r = 0; r < maxw; ++r) rank[lst[r]] = r;
+    }
+#endif
     for (size_t g = 0; g < n_groups; ++g) {
       const int w0 = g ? ray_groups[g - 1] : 0;
-      for (int j = 0; w0 + j < ray_groups[g]; ++j) placed[((g / 8) * maxw + j) * 8 + g % 8] = ray[w0 + j];
+      for (int j = 0; w0 + j < ray_groups[g]; ++j) {
+        const size_t slot = RX_RAY_DISPATCH == 0 ? ((g / 8) * maxw + j) * 8 + g % 8
+                                                 : ((size_t)rank[j] * (padded / 8) + g / 8) * 8 + g % 8;
+        placed[slot] = ray[w0 + j];
+      }
     }
     ray.swap(placed);
   }
@@ -824,6 +851,28 @@ int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count) {
     mean_ms[k] = n[k] ? sum[k] / n[k] : 0.0;
     count[k] = n[k];
   }
+  return RX_OK;
+}
+
+int rx_profile_waves(rx_env* h, int32_t launch, uint64_t* start, uint64_t* end, int32_t cap, int32_t* n_waves,
+                     int32_t* kind, int32_t* khz) {
+  if (!h || !start || !end || !n_waves || !kind || !khz) return fail(RX_EINVAL, "rx_profile_waves: null argument");
+  if (launch < 0 || (size_t)launch >= h->prof_kinds.size())
+    return fail(RX_EINVAL, "rx_profile_waves: launch %d not recorded (%d in the record)", launch,
+                (int)h->prof_kinds.size());
+  if (cap < 0) return fail(RX_EINVAL, "rx_profile_waves: cap %d < 0", cap);
+  RX_HIP(hipSetDevice(h->cfg.device));
+  RX_HIP(hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, h->cfg.device));
+  RX_HIP(hipDeviceSynchronize());
+  const int stride = prof_stride(h);
+  const int n = std::min(stride, cap);
+  const unsigned long long* r = h->prof_buf.p + (size_t)launch * 2 * stride;
+  if (n > 0) {
+    RX_HIP(hipMemcpy(start, r, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    RX_HIP(hipMemcpy(end, r + stride, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  }
+  *n_waves = stride;
+  *kind = h->prof_kinds[launch];
   return RX_OK;
 }
 

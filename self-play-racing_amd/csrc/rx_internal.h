@@ -77,6 +77,16 @@ struct rx_track_view {
 #ifndef RX_REWARD_LPE2_N
 #define RX_REWARD_LPE2_N 4096
 #endif
+// Ray-wave dispatch order (rx_assign's placement of the ray-wave table, ray_order 2).
+// Class j of a 64-env group = its j-th wave of direction-sorted tasks (the cars of a
+// group head alike, so class j ~ sensor ray j: the edge classes look sideways, the
+// centre ones down the track and cost ~1.3x).  0 = group-octet-major (round 2),
+// 1 = class-major centre classes first, 2 = class-major ascending j, 3 = class-major
+// EDGE classes first, the centre ones last (default: 65,536 envs 752 -> 826-833 M
+// env-steps/s, 4,096 envs +3 %, same session, DESIGN.md §3 "Ray-wave dispatch order").
+#ifndef RX_RAY_DISPATCH
+#define RX_RAY_DISPATCH 3
+#endif
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them

@@ -526,7 +526,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   if (lane >= we.count) return;
   // p = the env's position in the wave order: the engine's working state is
   // stored in that order (coalesced); e = the env id, the row of every io buffer
-  const int p = we.perm_start + lane;
+  int p = we.perm_start + lane;
   int e = REW ? -1 : a.perm[p];  // REWARD: loaded after the argmins
 
   const rx_state& S = a.st;
@@ -621,6 +621,10 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
   RX_STAMP(6);
   if (sub != 0) return;  // one lane per env from here on
+  // REWARD: p passes through an empty asm, so the addresses of the late loads and
+  // of the stores below are recomputed from it (2 VALU each) instead of being kept
+  // live as 64-bit pointers across the argmins (they were spilled to scratch)
+  if constexpr (REW) __asm__ volatile("" : "+v"(p));
   if (REW) {  // the REWARD half's late loads (see above)
     e = a.perm[p];
     c.vx = S.vx[p];
@@ -1780,7 +1784,12 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 #ifndef RX_STEP2_MINW_2
 #define RX_STEP2_MINW_2 6  // two-car k_step2<2>: 80 VGPRs (fewer REWARD spills; 8 -> 6 waves: +9 % at 8,192 envs, +1 % at 65,536)
 #endif
-template <int A>
+// One instantiation per (REWARD lanes per env, lanes per ray) schedule: with
+// the three schedules of each half inlined into ONE kernel, its register
+// allocation was the maximum over all of them, and the REWARD half spilled at
+// the raycast's 64-VGPR cap (k_step2<1>: 36 B/lane of scratch) whichever
+// schedule ran.  RLPE is ignored for A = 2 (one lane per env).
+template <int A, int RLPE, int LPR>
 __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
   const unsigned long long prof_t0 = prof_start(a);
@@ -1793,25 +1802,16 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     double ang[A], ep[3] = {0.0, 0.0, 0.0};
     int e = -1;
     if constexpr (A == 1) {
-      // a.reward_lpe lanes per env (fewer argmin points per lane; few envs):
+      // RLPE lanes per env (fewer argmin points per lane; few envs):
       // block b = sub-block * n1 + dynamics wave, so a REWARD wave keeps the
       // XCD (b % 8) of its k_kin1 wave (n1 = n_dyn_waves rounded up to 8)
-      const int n1 = n_rw / a.reward_lpe, w = b % n1, sb = b / n1;
-      if (a.reward_lpe == 4)
-        dyn1_env<4, RX_PART_REWARD>(a, w, ang, e, ep, sb);
-      else if (a.reward_lpe == 2)
-        dyn1_env<2, RX_PART_REWARD>(a, w, ang, e, ep, sb);
-      else
-        dyn1_env<1, RX_PART_REWARD>(a, w, ang, e, ep, 0);
+      const int n1 = n_rw / RLPE, w = b % n1, sb = b / n1;
+      dyn1_env<RLPE, RX_PART_REWARD>(a, w, ang, e, ep, RLPE == 1 ? 0 : sb);
     } else
       dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
-  } else if (a.ray_lpr == 4) {
-    rays_body<A, 4>(a, b - n_rw);
-  } else if (a.ray_lpr == 2) {
-    rays_body<A, 2>(a, b - n_rw);
   } else {
-    rays_body<A, 1>(a, b - n_rw);
+    rays_body<A, LPR>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
 }
@@ -2101,14 +2101,25 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 }  // namespace
 
 // ------------------------------------------------------------ launchers
+// k_step2<A, RLPE, LPR> for the handle's schedule (a->reward_lpe, a->ray_lpr:
+// 1, 2 or 4 each, validated by rx_assign)
+template <int A, int RLPE>
+static void launch_step2_lpr(const rx_kargs* a, dim3 grid, int n_rw, hipStream_t s) {
+  if (a->ray_lpr == 4)
+    hipLaunchKernelGGL((k_step2<A, RLPE, 4>), grid, dim3(64), 0, s, *a, n_rw);
+  else if (a->ray_lpr == 2)
+    hipLaunchKernelGGL((k_step2<A, RLPE, 2>), grid, dim3(64), 0, s, *a, n_rw);
+  else
+    hipLaunchKernelGGL((k_step2<A, RLPE, 1>), grid, dim3(64), 0, s, *a, n_rw);
+}
+
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s) {
   if (n_agents == 2) {  // k_kin2, then k_step2<2> (REWARD waves padded to 8, as below)
     const int n_rw2 = (a->n_dyn_waves + 7) / 8 * 8;
     if (part == RX_SPLIT_KIN)
       hipLaunchKernelGGL((k_dyn2<RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
     else
-      hipLaunchKernelGGL(k_step2<2>, dim3(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves)), dim3(64), 0, s,
-                         *a, n_rw2);
+      launch_step2_lpr<2, 1>(a, dim3(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves)), n_rw2, s);
     return (int)hipGetLastError();
   }
   const int n_rw = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);
@@ -2116,11 +2127,16 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
     hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
-  } else if (part == RX_SPLIT_REWARD) {
-    hipLaunchKernelGGL(k_step2<1>, dim3(n_rw), dim3(64), 0, s, *a, n_rw);
-  } else {  // RX_SPLIT_REWARD_RAYS: both halves in one launch
-    hipLaunchKernelGGL(k_step2<1>, dim3(n_rw + a->n_ray_waves), dim3(64), 0, s, *a, n_rw);
+    return (int)hipGetLastError();
   }
+  // RX_SPLIT_REWARD: the REWARD half alone; RX_SPLIT_REWARD_RAYS: both halves in one launch
+  const dim3 grid(n_rw + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves));
+  if (a->reward_lpe == 4)
+    launch_step2_lpr<1, 4>(a, grid, n_rw, s);
+  else if (a->reward_lpe == 2)
+    launch_step2_lpr<1, 2>(a, grid, n_rw, s);
+  else
+    launch_step2_lpr<1, 1>(a, grid, n_rw, s);
   return (int)hipGetLastError();
 }
 

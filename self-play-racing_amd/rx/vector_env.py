@@ -197,6 +197,24 @@ class RacingVectorEnv:
         _lib.check(self.L.rx_profile_read(self._h, ms, n), "rx_profile_read")
         return {k: (ms[i], n[i]) for i, k in enumerate(_lib.RX_KERNEL_NAMES) if n[i]}
 
+    def profile_waves(self, launch):
+        """Per-wave (start, end) device wall-clock stamps in microseconds from the
+        launch's first wave start, the kernel kind name and the wave-slot count of
+        recorded launch ``launch`` (rx_profile_waves; unused slots are NaN)."""
+        import ctypes
+        cap = 1 << 20
+        st = np.zeros(cap, np.uint64)
+        en = np.zeros(cap, np.uint64)
+        n, kind, khz = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(self.L.rx_profile_waves(self._h, int(launch), st.ctypes.data, en.ctypes.data, cap, ctypes.byref(n),
+                                           ctypes.byref(kind), ctypes.byref(khz)), "rx_profile_waves")
+        m = min(n.value, cap)
+        st, en = st[:m], en[:m]
+        live = st > 0
+        t0 = st[live].min() if live.any() else 0
+        us = lambda t: np.where(live, (t.astype(np.float64) - float(t0)) * 1e3 / khz.value, np.nan)  # noqa: E731
+        return us(st), us(en), _lib.RX_KERNEL_NAMES[kind.value], n.value
+
     def enable_counters(self, on=True):
         """Per-wave culling counters (rx_io.counters): chunk tests / scans."""
         self.counters = torch.zeros(4, dtype=torch.int64, device=self.device) if on else None

@@ -3,7 +3,7 @@
 #   AB_SETS="label|lib|args;label2|lib2|args2" bash tools/ab_args.sh
 # lib: empty = the tree's librx.so, NAME = rx/lib/librx_NAME.so (tools/build_rev.py).
 set -u
-OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/${OUT_SUB:-}; mkdir -p $OUT; export TMPDIR=/tmp
 LIBDIR=$(pwd)/self-play-racing_amd/rx/lib
 IFS=';' read -ra SETS <<< "$AB_SETS"
 for rep in 1 2; do
