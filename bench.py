@@ -595,6 +595,9 @@ def main():
         def one_step(ev=None):
             k = it[0] % bank
             it[0] += 1
+            if G == 1 and ev is None:  # one handle on the current stream: no stream context to enter
+                envs[0].step_device(acts[0][k])
+                return
             for g in range(G):
                 with torch.cuda.stream(streams[g]):
                     if ev is None or g:  # the production call: one rx_step

@@ -1568,9 +1568,31 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
   }
 }
 
+// Profiling build only (-DRX_RAY_STAMPS, tools/ray_stamps.py): per ray wave,
+// s_memtime after a full s_waitcnt at phase boundaries (0 entry, 1 task + state
+// loads, 2 sincos, 3 culling setup, 4 traversal, 5 obs store), the wall clock
+// at entry / exit (6, 7) and the wave's box tests / leaf scans (8, 9), written
+// to io.counters[16 + 12 * wave + j].  The product library has no stamps.
+#ifdef RX_RAY_STAMPS
+#define RAY_STAMP(j)                                 \
+  do {                                               \
+    __builtin_amdgcn_s_waitcnt(0);                   \
+    rstamp[j] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+#else
+#define RAY_STAMP(j) \
+  do {               \
+  } while (0)
+#endif
+
 template <int A, int LPR>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
+#ifdef RX_RAY_STAMPS
+  unsigned long long rstamp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  rstamp[6] = wall_clock64();
+  RAY_STAMP(0);
+#endif
   const rx_wave we = a.ray_waves[wave];
   const int lane = threadIdx.x & 63;
   const int k = uniform(we.track);
@@ -1611,9 +1633,11 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   const int i = A * pos + q;  // working state (position order); the obs row is A * perm[pos] + q
   const double ox = a.st.x[i], oy = a.st.y[i];
   const double theta = a.st.angle[i] + a.rel_angles[ray];  // racing_env.py:50
+  RAY_STAMP(1);
   double sn, cs;
   rx_sincos(theta, &sn, &cs);
   const double v3x = -sn, v3y = cs;
+  RAY_STAMP(2);
   double best = __builtin_inf();
   float bestf = __builtin_inff();
   const int G = a.cull_chunk;
@@ -1650,6 +1674,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
     const seg_pref pf{reinterpret_cast<const float4*>(a.tr.seg_f) + 2 * wp0, rx_f2{oxf, oyf}, rx_f2{-snf, csf},
                       (float)((__builtin_fabs(ox) + __builtin_fabs(oy) + __builtin_fabs(cx) + __builtin_fabs(cy) +
                                2.0 * rad + L + 1.0) * 0x1p-17)};
+    RAY_STAMP(3);
     auto scan = [&](auto filt) {
       constexpr bool F = decltype(filt)::value;
       if (a.box_quadrants && __all(quad == quad0)) {
@@ -1666,12 +1691,24 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
       scan(std::true_type{});
     else
       scan(std::false_type{});
+    RAY_STAMP(4);
+#ifdef RX_RAY_STAMPS
+    rstamp[8] = (unsigned long long)tested;
+    rstamp[9] = (unsigned long long)scanned;
+#else
     if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
       atomicAdd(&a.io.counters[0], (unsigned long long)tested);
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
+#endif
   }
   if (own && (lane & (LPR - 1)) == 0) ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);
+#ifdef RX_RAY_STAMPS
+  RAY_STAMP(5);
+  rstamp[7] = wall_clock64();
+  if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
+    for (int j = 0; j < 10; ++j) a.io.counters[16 + 12 * wave + j] = rstamp[j];
+#endif
 }
 
 // The observation of one ray from the wall minimum `best` (inf = no hit):

@@ -314,11 +314,12 @@ class RacingVectorEnv:
         (rx_step_phases) splits the step into its two kernels for timing."""
         a = self._as_actions(actions)
         io = self._io(actions=a, obs=obs_out, reward=reward_out, done=done_out, full=full_info)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)  # resolved once per step
         if phases == 3:
-            _lib.check(self.L.rx_step(self._h, io, _lib.stream_ptr(stream)), "rx_step")
+            _lib.check(self.L.rx_step(self._h, io, s.cuda_stream), "rx_step")
         else:
-            _lib.check(self.L.rx_step_phases(self._h, io, int(phases), _lib.stream_ptr(stream)), "rx_step_phases")
-        self._launched(stream)
+            _lib.check(self.L.rx_step_phases(self._h, io, int(phases), s.cuda_stream), "rx_step_phases")
+        self._launched(s)
         return (obs_out if obs_out is not None else self.buf["obs"],
                 reward_out if reward_out is not None else self.buf["reward"],
                 done_out if done_out is not None else self.buf["done_f32"])
