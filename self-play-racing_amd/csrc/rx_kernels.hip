@@ -1957,7 +1957,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
   const bool split = a.autoreset != RX_AUTORESET_SAME_STEP;
 #ifdef RX_ROLL_STAMPS  // profiling build (tools/rollout_stamps.py): phase boundaries of workgroup 0
 #define RX_RSTAMP(j) \
-  if (b == 0 && (threadIdx.x & 63) == 0 && a.io.counters && t < 512) a.io.counters[16 + 8 * t + (j)] = wall_clock64()
+  if (b == 0 && (threadIdx.x & 63) == 0 && a.io.counters && t < 512) a.io.counters[16 + 16 * t + (j)] = wall_clock64()
 #else
 #define RX_RSTAMP(j)
 #endif
@@ -2034,7 +2034,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         RX_RSTAMP(4);
       } else {
         for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, pos, ray, sl.seg);
-        if (w == 1) RX_RSTAMP(5);
+        RX_RSTAMP(4 + w);  // ray waves 1 .. 11: slots 5 .. 15
       }
     } else {  // same-step autoreset: the whole step first (k_dyn1's order)
       if (w == 0) {

@@ -104,7 +104,7 @@ struct Geo {
 // by rx_ppo_stamps_read (exported by that build only).  The product library has
 // no stamps.
 #ifdef RX_PPO_STAMPS
-constexpr int kStampW = 16, kStampMaxWaves = 8192;
+constexpr int kStampW = 24, kStampMaxWaves = 8192;
 __device__ unsigned long long g_ppo_stamps[kStampMaxWaves * kStampW];
 #define PPO_STAMP(j)                                                                                       \
   do {                                                                                                     \
@@ -161,7 +161,7 @@ struct WLds {
 // pre-activations: lane (q = 0, l15) holds output j in y[j].
 template <int D, int NOUT, int PREC, class Wt>
 __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>::template XN<PREC>], f4 (&H1)[4],
-                                            f4 (&H2)[4], f4& y, int l15, int q) {
+                                            f4 (&H2)[4], f4& y, int l15, int q, int stamp = -1) {
   constexpr int KS1 = Geo<D>::KS1;
   const int j3 = l15 < NOUT ? l15 : 0;
   const float on = l15 < NOUT ? 1.0f : 0.0f;
@@ -205,6 +205,7 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
 #pragma unroll
       for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
     }
+    if (stamp >= 0) PPO_STAMP(stamp);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -219,6 +220,7 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
 #pragma unroll
       for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
     }
+    if (stamp >= 0) PPO_STAMP(stamp + 1);
     y = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -283,9 +285,10 @@ struct GradLds {
   static constexpr int W1 = 0, B1 = W1 + 64 * Geo<D>::DP, W2 = B1 + 64, B2 = W2 + 64 * kWS, W3 = B2 + 64,
                        B3 = W3 + kNA * 64, WEND = B3 + 4;  // trunk weights
   // the pass's 64 rows: [hidden][row] transposes (dZ2 then dZ1; H1 then H2), [row][d] = [X | 1], [row][j] = g
-  static constexpr int SZ = WEND, SH = SZ + 64 * kTS, SX = SH + 64 * kTS, SG = SX + kRP * Geo<D>::XS,
-                       SMALL = SG + kRP * kNA;  // per-wave db2, dW3, db3, kl
-  static constexpr int SMALL_PER = 64 + kNA * 64 + kNA + 2, TOTAL = SMALL + 4 * SMALL_PER;
+  static constexpr int SZ = WEND, SH = SZ + 64 * kTS, SX = SH + 64 * kTS, SG = SX + kRP * Geo<D>::XS;
+  // per-wave db2, dW3, db3, kl: written after the last pass, over the dZ transpose
+  static constexpr int SMALL = SZ, SMALL_PER = 64 + kNA * 64 + kNA + 2, TOTAL = SG + kRP * kNA;
+  static_assert(4 * SMALL_PER <= 64 * kTS, "per-wave sums must fit in the dZ transpose");
 };
 
 // One trunk (NET: 0 = actor, 1 = critic) of one workgroup: rows_per_wg rows,
@@ -397,9 +400,9 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   if (t0 < NOUT * 64) lds[S::W3 + t0] = bv[1];
   if (t0 < NOUT) lds[S::B3 + t0] = b3v;
   __syncthreads();
+  const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
   PPO_STAMP(1);
   int pass_ = 0;
-  const WLds w{lds + S::W1, lds + S::B1, lds + S::W2, lds + S::B2, lds + S::W3, lds + S::B3, G::DP};
   float* sZ = lds + S::SZ;  // [hidden][row]
   float* sH = lds + S::SH;  // [hidden][row]
   float* sX = lds + S::SX;  // [row][d]
@@ -418,7 +421,8 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       if (d <= D) sX[rr * G::XS + d] = d == D ? 1.0f : x[s];  // the ones column (d = D) carries db1
     }
     f4 H1[4], H2[4], y;
-    mlp_forward<D, NOUT, PREC>(w, x, H1, H2, y, l15, q);
+    mlp_forward<D, NOUT, PREC>(w, x, H1, H2, y, l15, q, pass_ == 0 ? 16 : -1);
+    if (pass_ == 0) PPO_STAMP(18);
     float g[NOUT];  // d loss / d head pre-activation, row rr (every lane of the row)
     if (NET == 0) {
       float mu[kNA], diff[kNA], logp = 0.0f;
@@ -450,6 +454,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
       g[0] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
     }
+    if (pass_ == 0) PPO_STAMP(19);
     f4 dZ[4];  // dZ2 = (W3^T g) * (1 - H2^2)
 #pragma unroll
     for (int t = 0; t < 4; ++t)

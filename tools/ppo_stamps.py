@@ -60,7 +60,7 @@ L = _lib.load()
 L.rx_ppo_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 n_wg = L.rx_ppo_workspace_doubles(mb)
 n_waves = 2 * n_wg * 4
-buf = np.zeros((8192, 16), np.uint64)
+buf = np.zeros((8192, 24), np.uint64)
 for m in range(4):  # warm
     fg.grad(m, stop, kl)
 assert L.rx_ppo_stamps_read(buf.ctypes.data, 8192) == 0
@@ -79,6 +79,10 @@ for m in range(4, 12):
                 "launch_span_cycles": float(s[ok, -1].max() - s[ok, 0].min()),
                 "start_spread_cycles": float(np.percentile(s[ok, 0], 99) - s[ok, 0].min()),
                 "end_spread_cycles": float(s[ok, -1].max() - np.percentile(s[ok, -1], 1))})
+    a = st[:, [1, 16, 17, 18, 19, 2]]  # pass 0, phase A: layer 1, layer 2, head, loss, dZ2 + transposes
+    ok = (a > 0).all(axis=1)
+    res[-1]["p0A_sub_cycles_median"] = dict(zip(["layer1", "layer2", "head", "loss", "dz2_lds"],
+                                                np.median(np.diff(a[ok], axis=1), axis=0).round(0).tolist()))
 labels = ["stage"] + [f"p{p}{ph}" for p in range(res[-1]["passes"]) for ph in "ABCD"] + ["accum", "small"]
 out = {"mb": mb, "precision": prec, "n_wg_per_trunk": n_wg, "labels": labels, "runs": res[-3:]}
 print(json.dumps(out))
