@@ -1991,12 +1991,19 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         float lp = 0.0f;
         if (lane < NA) {
           const int j = lane;
-          float zz = 0.0f;
-#pragma unroll 16
-          for (int k = 0; k < H; ++k) {
-            const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
-            zz = fmaf(sW3[j * H + h], sH2[0][h], zz);
+          // k_policy_act's VALU head (rx_ppo.hip mlp_forward): 4 partial chains
+          // over h = 16t + 4q + r in the order t, r, then (p0 + p1) + (p2 + p3)
+          float pq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pq[q] = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              const int h = 16 * (k >> 2) + 4 * q + (k & 3);
+              pq[q] = fmaf(sW3[j * H + h], sH2[0][h], pq[q]);
+            }
           }
+          const float zz = (pq[0] + pq[1]) + (pq[2] + pq[3]);
           const float mu = rx_policy::tanh_fast(zz + P[L::ab3 + j]);
           const float scale = expf(r.log_std[j]);
           const float var = scale * scale;
@@ -2008,11 +2015,16 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         const float lp1 = __shfl(lp, 1, 64);
         if (lane == 0) r.logprobs[row] = (0.0f + lp) + lp1;  // logp = 0; logp += lp_j in j order
       } else if (lane == 0) {
-        float v = 0.0f;
-        for (int k = 0; k < H; ++k) {
-          const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);
-          v = fmaf(P[L::cW3 + h], sH2[1][h], v);
+        float pq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pq[q] = 0.0f;
+          for (int k = 0; k < 16; ++k) {
+            const int h = 16 * (k >> 2) + 4 * q + (k & 3);
+            pq[q] = fmaf(P[L::cW3 + h], sH2[1][h], pq[q]);
+          }
         }
+        const float v = (pq[0] + pq[1]) + (pq[2] + pq[3]);
         r.values[row] = v + P[L::cb3];
       }
     }

@@ -221,11 +221,25 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
       for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
     }
     if (stamp >= 0) PPO_STAMP(stamp + 1);
+    // head on the VALU (NOUT <= 2 of an MFMA tile's 16 output rows would be
+    // used): lane (q, l15) sums its own hidden units h = 16t + 4q + r in the
+    // order t, r, then the 4 q-lanes of the row combine as (p0 + p1) + (p2 + p3)
+    // (xor 16, then xor 32; k_rollout repeats this order).  Every lane of the
+    // row ends with output j in y[j].
     y = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int j = 0; j < NOUT; ++j) {
+      float acc = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) y = mma(on * w.w3(j3, 16 * t + 4 * q + r), H2[t][r], y);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = fmaf(w.w3(j, 16 * t + 4 * q + r), H2[t][r], acc);
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      y[j] = acc;
+    }
+    (void)j3;
+    (void)on;
   }
 }
 
