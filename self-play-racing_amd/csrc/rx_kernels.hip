@@ -1905,6 +1905,26 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     sW2[1][k * H + j] = P[L::cW2 + i];
   }
   for (int i = threadIdx.x; i < NA * H; i += blockDim.x) sW3[i] = P[L::aW3 + i];
+  // every other policy constant in LDS too: the per-step chain then waits on
+  // no global load (biases, the critic head, the actor's scale terms)
+  __shared__ float sB[2][2][H];  // [trunk][layer][unit]
+  __shared__ float sW3c[H];      // critic head
+  __shared__ float sK[8];        // ab3[0..1], cb3, scale[0..1], log scale[0..1]
+  __shared__ float2 sAct;        // actions[t] of this env: actor -> the dynamics wave
+  __shared__ int sObsTaken;      // steps whose obs the critic wave has copied (split step: KIN waits for it)
+  if (threadIdx.x == 0) sObsTaken = 0;
+  for (int i = threadIdx.x; i < H; i += blockDim.x) {
+    sB[0][0][i] = P[L::ab1 + i], sB[0][1][i] = P[L::ab2 + i];
+    sB[1][0][i] = P[L::cb1 + i], sB[1][1][i] = P[L::cb2 + i];
+    sW3c[i] = P[L::cW3 + i];
+  }
+  if (threadIdx.x < NA) {  // Normal(mu, exp(log_std)): the same expf / logf per step as before, once
+    const float scale = expf(r.log_std[threadIdx.x]);
+    sK[threadIdx.x] = P[L::ab3 + threadIdx.x];
+    sK[3 + threadIdx.x] = scale;
+    sK[5 + threadIdx.x] = logf(scale);
+  }
+  if (threadIdx.x == 0) sK[2] = P[L::cb3];
   // the env's slot, read every step by the argmins, the collision test and the
   // 11 raycasts: LDS latency instead of L2 round trips (rx_rollout sizes it)
   extern __shared__ double4 sSlot[];  // [2W] segments, then [W] waypoints, [W] normals (double2)
@@ -1965,10 +1985,9 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
     if (w == 0) RX_RSTAMP(0);
     const bool last = t + 1 == r.T;
     const int64_t row = (int64_t)t * n + e;
-    if (w < 2) {  // ---- policy (k_policy_act's operations, one row)
-      const int tr = w;  // 0 = actor, 1 = critic
-      if (lane < D) sX[tr][lane] = t == 0 ? r.obs[row * D + lane] : sObs[lane];
-      wave_sync();
+    // ---- policy (k_policy_act's operations, one row): the trunk of tr on
+    // sX[tr] (0 = actor, 1 = critic), then the heads
+    auto trunk = [&](int tr) {
       // k_policy_act's MFMA chains (rx_ppo.hip): inputs d = 0 .. D-1 then the
       // zero padding to a multiple of 4; hidden units in the order t, r, q
       // (h = 16t + 4q + r)
@@ -1977,7 +1996,7 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
       for (int d = 0; d < D; ++d) z = fmaf(sW1[tr][d * H + lane], sX[tr][d], z);
 #pragma unroll
       for (int d = D; d < (D + 3) / 4 * 4; ++d) z = fmaf(0.0f, 0.0f, z);
-      sH1[tr][lane] = rx_policy::tanh_fast(z + P[(tr ? L::cb1 : L::ab1) + lane]);
+      sH1[tr][lane] = rx_policy::tanh_fast(z + sB[tr][0][lane]);
       wave_sync();
       z = 0.0f;
 #pragma unroll 16
@@ -1985,59 +2004,84 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         const int h = (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3);  // k = 16t + 4r + q -> h = 16t + 4q + r
         z = fmaf(sW2[tr][h * H + lane], sH1[tr][h], z);
       }
-      sH2[tr][lane] = rx_policy::tanh_fast(z + P[(tr ? L::cb2 : L::ab2) + lane]);
+      sH2[tr][lane] = rx_policy::tanh_fast(z + sB[tr][1][lane]);
       wave_sync();
-      if (tr == 0) {
-        float lp = 0.0f;
-        if (lane < NA) {
-          const int j = lane;
-          // k_policy_act's VALU head (rx_ppo.hip mlp_forward): 4 partial chains
-          // over h = 16t + 4q + r in the order t, r, then (p0 + p1) + (p2 + p3)
-          float pq[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            pq[q] = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-              const int h = 16 * (k >> 2) + 4 * q + (k & 3);
-              pq[q] = fmaf(sW3[j * H + h], sH2[0][h], pq[q]);
-            }
-          }
-          const float zz = (pq[0] + pq[1]) + (pq[2] + pq[3]);
-          const float mu = rx_policy::tanh_fast(zz + P[L::ab3 + j]);
-          const float scale = expf(r.log_std[j]);
-          const float var = scale * scale;
-          const float smp = r.eps[row * NA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
-          const float act = fminf(fmaxf(smp, -1.0f), 1.0f);
-          r.actions[row * NA + j] = act;
-          lp = rx_policy::normal_logp(act - mu, var, logf(scale));
-        }
-        const float lp1 = __shfl(lp, 1, 64);
-        if (lane == 0) r.logprobs[row] = (0.0f + lp) + lp1;  // logp = 0; logp += lp_j in j order
-      } else if (lane == 0) {
+    };
+    auto actor_head = [&](float eps) {
+      float lp = 0.0f;
+      if (lane < NA) {
+        const int j = lane;
+        // k_policy_act's VALU head (rx_ppo.hip mlp_forward): 4 partial chains
+        // over h = 16t + 4q + r in the order t, r, then (p0 + p1) + (p2 + p3)
         float pq[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           pq[q] = 0.0f;
+#pragma unroll
           for (int k = 0; k < 16; ++k) {
             const int h = 16 * (k >> 2) + 4 * q + (k & 3);
-            pq[q] = fmaf(P[L::cW3 + h], sH2[1][h], pq[q]);
+            pq[q] = fmaf(sW3[j * H + h], sH2[0][h], pq[q]);
           }
         }
-        const float v = (pq[0] + pq[1]) + (pq[2] + pq[3]);
-        r.values[row] = v + P[L::cb3];
+        const float zz = (pq[0] + pq[1]) + (pq[2] + pq[3]);
+        const float mu = rx_policy::tanh_fast(zz + sK[j]);
+        const float scale = sK[3 + j];
+        const float var = scale * scale;
+        const float smp = eps * scale + mu;  // mul_(std).add_(mu): two roundings
+        const float act = fminf(fmaxf(smp, -1.0f), 1.0f);
+        r.actions[row * NA + j] = act;
+        reinterpret_cast<float*>(&sAct)[j] = act;
+        lp = rx_policy::normal_logp(act - mu, var, sK[5 + j]);
       }
-    }
-    __syncthreads();  // actions[t] -> the dynamics wave
-    if (w == 0) RX_RSTAMP(1);
-    at.io.actions = r.actions + (size_t)t * n * NA;
+      const float lp1 = __shfl(lp, 1, 64);
+      if (lane == 0) r.logprobs[row] = (0.0f + lp) + lp1;  // logp = 0; logp += lp_j in j order
+    };
+    auto critic_head = [&]() {
+      if (lane != 0) return;
+      float pq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        pq[q] = 0.0f;
+        for (int k = 0; k < 16; ++k) {
+          const int h = 16 * (k >> 2) + 4 * q + (k & 3);
+          pq[q] = fmaf(sW3c[h], sH2[1][h], pq[q]);
+        }
+      }
+      const float v = (pq[0] + pq[1]) + (pq[2] + pq[3]);
+      r.values[row] = v + sK[2];
+    };
+    auto load_obs = [&](int tr) {  // obs[t] of the env -> sX[tr]
+      if (lane < D) sX[tr][lane] = t == 0 ? r.obs[row * D + lane] : sObs[lane];
+      wave_sync();
+    };
+    at.io.actions = reinterpret_cast<const float*>(&sAct) - (ptrdiff_t)e * NA;  // actions[t] row e, from LDS
     at.io.obs = sObs - (ptrdiff_t)e * D;  // obs[t+1] row in LDS, copied out below
     at.io.reward = r.rewards + (size_t)t * n;
     at.io.done_f32 = last ? r.next_done : r.dones + (size_t)(t + 1) * n;
     double ang[1], ep[3] = {0.0, 0.0, 0.0};
     int ee = -1;
-    if (split) {  // ---- RacingEnv.step as the split step: KIN, then REWARD beside the raycast
-      if (w == 0) dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep, 0, &sl);
+    if (split) {
+      // RacingEnv.step as the split step: the actor, then KIN on wave 0 (KIN only
+      // waits for the critic wave to have copied obs[t], since it overwrites the
+      // non-ray columns of sObs); REWARD beside the raycast, and the critic's
+      // trunk on wave 1 ahead of its ray (wave 1's ray ends first otherwise)
+      if (w == 0) {
+        const float eps = lane < NA ? r.eps[row * NA + lane] : 0.0f;  // in flight during the trunk
+        load_obs(0);
+        trunk(0);
+        actor_head(eps);
+        while (__hip_atomic_load(&sObsTaken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= t)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        RX_RSTAMP(1);
+        dyn1_env<64, RX_PART_KIN>(at, b, ang, ee, ep, 0, &sl);
+      } else if (w == 1) {
+        load_obs(1);
+        if (lane == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&sObsTaken, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
       __syncthreads();  // stepped pose -> the raycast waves
       if (w == 0) RX_RSTAMP(2);
       if (w == 0) {
@@ -2045,10 +2089,24 @@ __global__ __launch_bounds__(64 * kRollWaves) void k_rollout(rx_kargs a, rx_roll
         add_episode_stats(at, ep);
         RX_RSTAMP(4);
       } else {
+        if (w == 1) {
+          trunk(1);
+          critic_head();
+        }
         for (int ray = w - 1; ray < a.n_sensors; ray += kRollWaves - 1) ray_wide<1>(at, pos, ray, sl.seg);
         RX_RSTAMP(4 + w);  // ray waves 1 .. 11: slots 5 .. 15
       }
-    } else {  // same-step autoreset: the whole step first (k_dyn1's order)
+    } else {  // same-step autoreset: the policy, then the whole step (k_dyn1's order), then the rays
+      if (w < 2) {
+        const float eps = (w == 0 && lane < NA) ? r.eps[row * NA + lane] : 0.0f;
+        load_obs(w);
+        trunk(w);
+        if (w == 0)
+          actor_head(eps);
+        else
+          critic_head();
+      }
+      __syncthreads();  // actions[t] -> the dynamics wave
       if (w == 0) {
         dyn1_env<64, RX_PART_FULL>(at, b, ang, ee, ep, 0, &sl);
         add_episode_stats(at, ep);
