@@ -2,7 +2,7 @@
 # Round 3 GPU check: the whole -m gpu suite (one process, per-test time limit),
 # smoke(), then an optional follow-up script ($1).  Stops at the first failing step.
 set -u
-OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r03; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${OUTDIR:-${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r03}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
   > $OUT/pytest_gpu.log 2>&1; rc=$?
 tail -3 $OUT/pytest_gpu.log
