@@ -36,14 +36,26 @@ namespace {
 
 using rx_policy::kH;   // hidden width (agent/ppo.py:20-29)
 using rx_policy::kNA;  // action dims
-constexpr int kT = 256;      // threads per workgroup (4 waves)
-constexpr int kRP = 64;      // rows per workgroup pass (16 per wave)
+constexpr int kT = 256;      // k_policy_act: threads per workgroup (4 waves)
+// k_ppo_grad workgroup: RX_PPO_NW waves (4 or 8), 16 rows each per pass.  With
+// 8 waves one workgroup per CU stages its trunk's weights (half the prologue
+// traffic of two 4-wave workgroups) and the minibatch has half the partial rows;
+// measured no faster (the 8-wave barriers wait longer: minibatch step 39.5-40.3
+// vs 40.5-40.7 us, profiles/r03/ab_ppo_grad_8_waves.json), so 4 is the default
+// and 8 an A/B build (bit-exact tests pass with either).
+#ifndef RX_PPO_NW
+#define RX_PPO_NW 4
+#endif
+constexpr int kGW = RX_PPO_NW;
+static_assert(kGW == 4 || kGW == 8, "k_ppo_grad: 4 or 8 waves per workgroup");
+constexpr int kGT = 64 * kGW;  // k_ppo_grad threads per workgroup
+constexpr int kRP = 16 * kGW;  // rows per workgroup pass (16 per wave)
 #ifndef RX_PPO_MAXWG
-#define RX_PPO_MAXWG 256
+#define RX_PPO_MAXWG (RX_PPO_NW == 8 ? 128 : 256)
 #endif
 constexpr int kMaxWG = RX_PPO_MAXWG;  // row workgroups per minibatch and trunk (rows per workgroup grow beyond that)
 constexpr int kWS = 68;      // LDS row stride of W2 [o][i] (float4-aligned; transposed reads conflict-free)
-constexpr int kTS = 66;      // LDS row stride of the [hidden][row] transposes (operand reads conflict-free)
+constexpr int kTS = kRP + 2;  // LDS row stride of the [hidden][row] transposes (= 2 mod 64: operand reads conflict-free)
 #ifndef RX_PPO_MINW
 #define RX_PPO_MINW 2  // k_ppo_grad: min waves per SIMD (register budget 512 / RX_PPO_MINW)
 #endif
@@ -302,7 +314,7 @@ struct GradLds {
   static constexpr int SZ = WEND, SH = SZ + 64 * kTS, SX = SH + 64 * kTS, SG = SX + kRP * Geo<D>::XS;
   // per-wave db2, dW3, db3, kl: written after the last pass, over the dZ transpose
   static constexpr int SMALL = SZ, SMALL_PER = 64 + kNA * 64 + kNA + 2, TOTAL = SG + kRP * kNA;
-  static_assert(4 * SMALL_PER <= 64 * kTS, "per-wave sums must fit in the dZ transpose");
+  static_assert(kGW * SMALL_PER <= 64 * kTS, "per-wave sums must fit in the dZ transpose");
 };
 
 // One trunk (NET: 0 = actor, 1 = critic) of one workgroup: rows_per_wg rows,
@@ -329,6 +341,14 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   const int t0 = threadIdx.x, lane = t0 & 63, l15 = lane & 15, q = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(t0 >> 6);
   const int rr = 16 * wv + l15;  // this lane's row within the pass
+  // weight-gradient tiles of this wave: output rows [16 rb, 16 rb + 16) of dW2 /
+  // dW1; dW2 column tiles c2 + i (i < NT2); dW1 column tiles c1 + i (i < NA1)
+  // over k-steps [k1_lo, k1_hi) of the pass (8 waves and one dW1 column tile:
+  // the two wave halves split the pass's rows and add at the end)
+  constexpr int NT2 = kGW == 4 ? 4 : 2, NA1 = kGW == 4 ? NT1 : 1;
+  const int rb = kGW == 4 ? wv : (wv & 3), hh = kGW == 4 ? 0 : (wv >> 2);
+  const int c2 = NT2 * hh, c1 = (kGW == 8 && NT1 == 2) ? hh : 0;
+  constexpr bool KSPLIT = kGW == 8 && NT1 == 1;
   const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
   const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
   const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
@@ -341,11 +361,11 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     var[j] = scale * scale;
     lsc[j] = logf(scale);
   }
-  f4 acc2[4], acc1[NT1];  // dW2 rows [16 wv, +16) x 4 column tiles; dW1 (+ db1) rows [16 wv, +16)
+  f4 acc2[NT2], acc1[NA1];  // dW2 / dW1 (+ db1) tiles of rows [16 rb, +16)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) acc2[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k = 0; k < NT2; ++k) acc2[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int k = 0; k < NT1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k = 0; k < NA1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
   float db2 = 0.0f, dw3[NOUT] = {}, db3 = 0.0f;  // lane = hidden unit (db2, dW3), output (db3)
   double kl = 0.0;
   // inputs of a row, loaded one pass ahead (the perm index two passes ahead):
@@ -386,25 +406,25 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   // one memory latency for all of it instead of one round trip per staged
   // element (stamps: staging 11 k -> see DESIGN.md §3, k_ppo_grad)
   int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
-  constexpr int kW1N = (64 * G::DP + kT - 1) / kT, kW2N = 64 * 64 / kT;
+  constexpr int kW1N = (64 * G::DP + kGT - 1) / kGT, kW2N = 64 * 64 / kGT;
   float w1v[kW1N], w2v[kW2N], bv[2];
 #pragma unroll
   for (int j = 0; j < kW1N; ++j) {
-    const int e = t0 + kT * j, o = e / G::DP, d = e - o * G::DP;
+    const int e = t0 + kGT * j, o = e / G::DP, d = e - o * G::DP;
     w1v[j] = (e < 64 * G::DP && d < D) ? W[oW1 + o * D + d] : 0.0f;
   }
 #pragma unroll
-  for (int j = 0; j < kW2N; ++j) w2v[j] = W[oW2 + t0 + kT * j];
+  for (int j = 0; j < kW2N; ++j) w2v[j] = W[oW2 + t0 + kGT * j];
   bv[0] = t0 < 64 ? W[ob1 + t0] : (t0 < 128 ? W[ob2 + t0 - 64] : 0.0f);
   bv[1] = t0 < NOUT * 64 ? W[oW3 + t0] : 0.0f;
   const float b3v = t0 < NOUT ? W[ob3 + t0] : 0.0f;
   RowIn cur = load_row(src);
 #pragma unroll
   for (int j = 0; j < kW1N; ++j)
-    if (t0 + kT * j < 64 * G::DP) lds[S::W1 + t0 + kT * j] = w1v[j];
+    if (t0 + kGT * j < 64 * G::DP) lds[S::W1 + t0 + kGT * j] = w1v[j];
 #pragma unroll
   for (int j = 0; j < kW2N; ++j) {
-    const int e = t0 + kT * j;
+    const int e = t0 + kGT * j;
     lds[S::W2 + (e >> 6) * kWS + (e & 63)] = w2v[j];
   }
   if (t0 < 64)
@@ -493,19 +513,20 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     if constexpr (PREC == kBF16) {
 #pragma unroll
       for (int s = 0; s < kRP / 32; ++s) {
-        const bf8 av = rows8(sZ + (16 * wv + l15) * kTS + 32 * s + 8 * q);
+        const bf8 av = rows8(sZ + (16 * rb + l15) * kTS + 32 * s + 8 * q);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma16(av, rows8(sH + (16 * nt + l15) * kTS + 32 * s + 8 * q), acc2[nt]);
+        for (int i = 0; i < NT2; ++i)
+          acc2[i] = mma16(av, rows8(sH + (16 * (c2 + i) + l15) * kTS + 32 * s + 8 * q), acc2[i]);
       }
     } else {
 #pragma unroll 4
       for (int s = 0; s < kRP / 4; ++s) {
-        const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
-        float bv[4];
+        const float av = sZ[(16 * rb + l15) * kTS + 4 * s + q];
+        float bv[NT2];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) bv[nt] = sH[(16 * nt + l15) * kTS + 4 * s + q];
+        for (int i = 0; i < NT2; ++i) bv[i] = sH[(16 * (c2 + i) + l15) * kTS + 4 * s + q];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc2[nt] = mma(av, bv[nt], acc2[nt]);
+        for (int i = 0; i < NT2; ++i) acc2[i] = mma(av, bv[i], acc2[i]);
       }
     }
 #pragma unroll
@@ -555,31 +576,35 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     // ================================================================ D
     // dW1[16 wv + i][d] (+ db1 at d = D) += sum_rows dZ1 x [X | 1]
     if constexpr (PREC == kBF16) {
+      constexpr int KS = KSPLIT ? kRP / 64 : kRP / 32;  // k-steps of 32 rows
+      const int s0 = KSPLIT ? hh * KS : 0;
 #pragma unroll
-      for (int s = 0; s < kRP / 32; ++s) {
-        const bf8 av = rows8(sZ + (16 * wv + l15) * kTS + 32 * s + 8 * q);
+      for (int s = s0; s < s0 + KS; ++s) {
+        const bf8 av = rows8(sZ + (16 * rb + l15) * kTS + 32 * s + 8 * q);
 #pragma unroll
-        for (int nt = 0; nt < NT1; ++nt) {
-          const int d = 16 * nt + l15;
+        for (int i = 0; i < NA1; ++i) {
+          const int d = 16 * (c1 + i) + l15;
           float v[8];
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) v[jj] = d <= D ? sX[(32 * s + 8 * q + jj) * G::XS + d] : 0.0f;
-          acc1[nt] = mma16(av, to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])),
-                           acc1[nt]);
+          acc1[i] = mma16(av, to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])),
+                          acc1[i]);
         }
       }
     } else {
+      constexpr int KS = KSPLIT ? kRP / 8 : kRP / 4;  // k-steps of 4 rows
+      const int s0 = KSPLIT ? hh * KS : 0;
 #pragma unroll 4
-      for (int s = 0; s < kRP / 4; ++s) {
-        const float av = sZ[(16 * wv + l15) * kTS + 4 * s + q];
-        float bv[NT1];
+      for (int s = s0; s < s0 + KS; ++s) {
+        const float av = sZ[(16 * rb + l15) * kTS + 4 * s + q];
+        float bv[NA1];
 #pragma unroll
-        for (int nt = 0; nt < NT1; ++nt) {
-          const int d = 16 * nt + l15;
-          bv[nt] = d <= D ? sX[(4 * s + q) * G::XS + d] : 0.0f;
+        for (int i = 0; i < NA1; ++i) {
+          const int d = 16 * (c1 + i) + l15;
+          bv[i] = d <= D ? sX[(4 * s + q) * G::XS + d] : 0.0f;
         }
 #pragma unroll
-        for (int nt = 0; nt < NT1; ++nt) acc1[nt] = mma(av, bv[nt], acc1[nt]);
+        for (int i = 0; i < NA1; ++i) acc1[i] = mma(av, bv[i], acc1[i]);
       }
     }
     // dW3 / db3 of own rows (lane = hidden unit / output)
@@ -598,21 +623,18 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     src_n = src_nn;
     cur = nxt;
   }
-  // ---- tile accumulators -> the partial row (each wave owns rows [16 wv, 16 wv + 16))
+  // ---- tile accumulators -> the partial row (each wave owns its tiles)
   PPO_STAMP(14);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int o = 16 * wv + 4 * q + r;
+    const int o = 16 * rb + 4 * q + r;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) out[oW2 + o * kH + 16 * nt + l15] = acc2[nt][r];
-#pragma unroll
-    for (int nt = 0; nt < NT1; ++nt) {
-      const int d = 16 * nt + l15;
-      if (d < D)
-        out[oW1 + o * D + d] = acc1[nt][r];
-      else if (d == D)
-        out[ob1 + o] = acc1[nt][r];
-    }
+    for (int i = 0; i < NT2; ++i) out[oW2 + o * kH + 16 * (c2 + i) + l15] = acc2[i][r];
+  }
+  float* xch = lds + S::SH;  // KSPLIT: the second half's dW1 tile, [row block][lane][4]
+  if constexpr (KSPLIT) {
+    if (hh == 1) *reinterpret_cast<float4*>(xch + (rb * 64 + lane) * 4) =
+        make_float4(acc1[0][0], acc1[0][1], acc1[0][2], acc1[0][3]);
   }
   // ---- per-wave small sums, folded over the waves in a fixed order
 #pragma unroll
@@ -625,11 +647,37 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   if (lane == 0) reinterpret_cast<double*>(small + 64 + kNA * 64 + kNA)[0] = kl;  // 8-aligned: SMALL_PER is even
   __syncthreads();
   PPO_STAMP(15);
+  if (!KSPLIT || hh == 0) {
+    if constexpr (KSPLIT) {  // rows of the pass's first half + its second half, in that order
+      const float4 o2 = *reinterpret_cast<const float4*>(xch + (rb * 64 + lane) * 4);
+      acc1[0][0] += o2.x, acc1[0][1] += o2.y, acc1[0][2] += o2.z, acc1[0][3] += o2.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 16 * rb + 4 * q + r;
+#pragma unroll
+      for (int i = 0; i < NA1; ++i) {
+        const int d = 16 * (c1 + i) + l15;
+        if (d < D)
+          out[oW1 + o * D + d] = acc1[i][r];
+        else if (d == D)
+          out[ob1 + o] = acc1[i][r];
+      }
+    }
+  }
   if (wv != 0) return;
   const float* sm = lds + S::SMALL;
+  constexpr int SP = S::SMALL_PER;
+  auto fold = [&](int k) -> float {  // per-wave partials in a fixed order
+    if constexpr (kGW == 4)
+      return (sm[k] + sm[2 * SP + k]) + (sm[SP + k] + sm[3 * SP + k]);
+    else
+      return ((sm[k] + sm[4 * SP + k]) + (sm[2 * SP + k] + sm[6 * SP + k])) +
+             ((sm[SP + k] + sm[5 * SP + k]) + (sm[3 * SP + k] + sm[7 * SP + k]));
+  };
   for (int e = lane; e < 64 + NOUT * 64 + NOUT; e += 64) {
     const int k = e < 64 + NOUT * 64 ? e : 64 + kNA * 64 + (e - 64 - NOUT * 64);
-    const float v = (sm[k] + sm[2 * S::SMALL_PER + k]) + (sm[S::SMALL_PER + k] + sm[3 * S::SMALL_PER + k]);
+    const float v = fold(k);
     if (e < 64)
       out[ob2 + e] = v;
     else if (e < 64 + NOUT * 64)
@@ -640,14 +688,18 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   if (NET == 0 && lane == 0) {
     const double* kd = reinterpret_cast<const double*>(sm + 64 + kNA * 64 + kNA);
     const int st = S::SMALL_PER / 2;
-    a.kl_partial[blockIdx.x] = (kd[0] + kd[2 * st]) + (kd[st] + kd[3 * st]);
+    if constexpr (kGW == 4)
+      a.kl_partial[blockIdx.x] = (kd[0] + kd[2 * st]) + (kd[st] + kd[3 * st]);
+    else
+      a.kl_partial[blockIdx.x] = ((kd[0] + kd[4 * st]) + (kd[2 * st] + kd[6 * st])) +
+                                 ((kd[st] + kd[5 * st]) + (kd[3 * st] + kd[7 * st]));
   }
 }
 
 // blockIdx.y = trunk (0 actor, 1 critic: their losses share no parameter, so
 // they write disjoint ranges of the same partial row); blockIdx.x = row group.
 template <int D, int PREC>
-__global__ __launch_bounds__(kT, RX_PPO_MINW) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
+__global__ __launch_bounds__(kGT, RX_PPO_MINW) void k_ppo_grad(ppo_args a, const float* __restrict__ W,
                                                     float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
   PPO_STAMP(0);
@@ -999,15 +1051,15 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
   const bool bf = b->precision == kBF16;
   if (b->obs_dim == 15) {
     if (bf)
-      hipLaunchKernelGGL((k_ppo_grad<15, kBF16>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+      hipLaunchKernelGGL((k_ppo_grad<15, kBF16>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     else
-      hipLaunchKernelGGL((k_ppo_grad<15, kF32>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+      hipLaunchKernelGGL((k_ppo_grad<15, kF32>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
     if (bf)
-      hipLaunchKernelGGL((k_ppo_grad<19, kBF16>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+      hipLaunchKernelGGL((k_ppo_grad<19, kBF16>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     else
-      hipLaunchKernelGGL((k_ppo_grad<19, kF32>), dim3(n_wg, 2), dim3(kT), 0, s, a, b->params, partial);
+      hipLaunchKernelGGL((k_ppo_grad<19, kF32>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     P = Lay<19>::P, Pp = Lay<19>::Pp;
   }
   norm_args na{};

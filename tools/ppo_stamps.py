@@ -59,7 +59,8 @@ kl = torch.zeros(1, device="cuda")
 L = _lib.load()
 L.rx_ppo_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 n_wg = L.rx_ppo_workspace_doubles(mb)
-n_waves = 2 * n_wg * 4
+NW = int(os.environ.get("RX_PPO_NW", "4"))  # waves per k_ppo_grad workgroup of the build (rx_ppo.hip RX_PPO_NW)
+n_waves = 2 * n_wg * NW
 buf = np.zeros((8192, 24), np.uint64)
 for m in range(4):  # warm
     fg.grad(m, stop, kl)
@@ -69,7 +70,7 @@ for m in range(4, 12):
     fg.grad(m, stop, kl)
     assert L.rx_ppo_stamps_read(buf.ctypes.data, 8192) == 0
     st = buf[:n_waves].astype(np.float64)
-    passes = (mb // n_wg) // 64
+    passes = (mb // n_wg) // (16 * NW)
     cols = [0, 1] + [c for p in range(passes) for c in (2 + 4 * p, 3 + 4 * p, 4 + 4 * p, 5 + 4 * p)] + [14, 15]
     s = st[:, cols]
     ok = (s > 0).all(axis=1)
