@@ -102,6 +102,7 @@ struct rx_env {
   // spatial sort (scheduling only)
   DevBuf<uint32_t> keys_in;              // [N] bin per perm position (REWARD half)
   bool sort_pending = false;             // keys written, the re-sort runs after this step's raycast
+  bool sort_hist_done = false;           // the REWARD half of the keys' launch also counted the bins
   DevBuf<uint32_t> sort_hist, sort_cursor;  // [sort_bins]
   DevBuf<int32_t> sort_base;             // [n_tracks] first bin of each slot
   int32_t sort_bins = 0, sort_shift = 0;
@@ -768,6 +769,12 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
         return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
       a.tasks_out = nullptr;
       a.sort_keys = keys;
+      // single-agent: the REWARD half also builds the re-sort's histogram (one
+      // launch fewer per re-sort: rx_sort_envs skips k_sort_hist)
+      if (keys && A == 1) {
+        a.sort_hist = h->sort_hist.p;
+        h->sort_hist_done = true;
+      }
       prof_arm(h, a, phases == 3 ? RX_KERNEL_STEP2 : RX_KERNEL_REWARD);
       if ((rc = rx_launch_split(&a, A, phases == 3 ? RX_SPLIT_REWARD_RAYS : RX_SPLIT_REWARD, s)) != 0)
         return fail(RX_EHIP, "k_step2 launch failed: %s", hipGetErrorString((hipError_t)rc));
@@ -794,8 +801,10 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   if (h->sort_pending && (phases & RX_PHASE_RAYS)) {
     h->sort_pending = false;
     rx_state work = h->work, tmp = h->work_tmp;
+    const int hist_done = h->sort_hist_done ? 1 : 0;
+    h->sort_hist_done = false;
     if ((rc = rx_sort_envs(h->keys_in.p, h->cfg.n_envs, A, h->sort_hist.p, h->sort_cursor.p, h->sort_bins,
-                           h->perm[0].p, h->perm[1].p, &work, &tmp, s)) != 0)
+                           h->perm[0].p, h->perm[1].p, &work, &tmp, s, hist_done)) != 0)
       return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
   }
   return RX_OK;

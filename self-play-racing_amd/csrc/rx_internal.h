@@ -103,6 +103,7 @@ struct rx_kargs {
   const double* rel_angles;   // [n_sensors]
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
   uint32_t* sort_keys;        // [N] k_dyn writes the sort bin (sort_base[slot] + (waypoint >> sort_shift)) at its perm position, or nullptr
+  uint32_t* sort_hist;        // with sort_keys: the REWARD half also counts the bins (the re-sort then skips k_sort_hist), or nullptr
   const int32_t* sort_base;   // [n_tracks] first sort bin of each slot (ascending with the slot id)
   int32_t sort_shift;         // waypoints per sort bin = 1 << sort_shift
   // ray_order 2: k_dyn writes the direction-sorted (agent, ray) task ids of
@@ -183,7 +184,7 @@ extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* 
 // tmp -> back); rx_state_sync: working copy <-> the caller's arrays
 extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
                             int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
-                            hipStream_t s);
+                            hipStream_t s, int hist_done = 0);
 extern "C" int rx_launch_permutation(int64_t n, uint64_t seed, int64_t* out, hipStream_t s);
 extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const int32_t* perm, int n, int A,
                              int to_user, hipStream_t s);

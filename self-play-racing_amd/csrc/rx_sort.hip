@@ -183,11 +183,12 @@ __global__ __launch_bounds__(kBlock) void k_feistel_perm(int64_t n, int h, uint6
 
 extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
                             int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
-                            hipStream_t s) {
+                            hipStream_t s, int hist_done) {
   if (n <= 0) return 0;
   if (nbins <= 0 || nbins > RX_SORT_MAX_BINS || (A != 1 && A != 2)) return (int)hipErrorInvalidValue;
   const int grid = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist);
+  // hist_done: the step's REWARD half counted the bins while writing the keys
+  if (!hist_done) hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist);
   hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanThreads), 0, s, hist, cursor, nbins);
   if (A == 1) {
     hipLaunchKernelGGL(k_sort_scatter<1>, dim3(grid), dim3(kBlock), 0, s, keys, n, cursor, perm, perm_tmp, *work,
