@@ -801,8 +801,11 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
 #ifdef RX_DYN_STAMPS
   RX_STAMP(8);
-  if (a.io.counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
-    for (int j = 0; j < 9; ++j) a.io.counters[16 + 12 * wave + j] = stamp[j];
+#ifdef RX_DYN_STAMPS_NO_REWARD  // the split step's KIN phases (tools/dyn_stamps.py kin): REWARD keeps out
+  if constexpr (!REW)
+#endif
+    if (a.io.counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
+      for (int j = 0; j < 9; ++j) a.io.counters[16 + 12 * wave + j] = stamp[j];
 #endif
 }
 

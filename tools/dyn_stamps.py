@@ -2,6 +2,7 @@
 
     python tools/dyn_stamps.py build      # here: compiles rx/lib/librx_stamps.so (-DRX_DYN_STAMPS)
     python tools/dyn_stamps.py [N]        # on the GPU box: per-phase cycles per wave
+    python tools/dyn_stamps.py kin build / kin [N]   # the split step's k_kin1 (8 -> 9: the ray-task sort)
 
 Phases (k_dyn1, stamps after a full s_waitcnt): 0->1 wave record, perm and
 state loads; 1->2 dynamics (sincos); 2->3 argmin window scan; 3->4 waypoint
@@ -17,9 +18,13 @@ sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
 sys.path.insert(0, ROOT)
 LIB = os.path.join(ROOT, "self-play-racing_amd", "rx", "lib", "librx_stamps.so")
 
+KIN = "kin" in sys.argv  # the split step's k_kin1 (a build whose REWARD half writes no stamps)
+if KIN:
+    sys.argv.remove("kin")
+    LIB = LIB.replace("librx_stamps.so", "librx_kstamps.so")
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     from rx import _build
-    print(_build.build(out=LIB, defines=("RX_DYN_STAMPS",)))
+    print(_build.build(out=LIB, defines=("RX_DYN_STAMPS",) + (("RX_DYN_STAMPS_NO_REWARD",) if KIN else ())))
     sys.exit(0)
 
 os.environ["RX_LIB_PATH"] = LIB
@@ -47,12 +52,14 @@ for rep in range(5):
     env.step_device(torch.rand((N, 2), generator=g, device="cuda") * scale + shift, phases=1)
     torch.cuda.synchronize()
     st = env.counters[16:].view(n_waves, 12)[:, :10].cpu().numpy().astype(np.float64)
+    if KIN:  # KIN runs no argmin: stamps 3-5 stay 0; phases loads, kinematics, state / outputs, obs cols, task sort
+        st = st[:, [0, 1, 2, 6, 7, 8, 9]]
     ok = (st > 0).all(axis=1)
     d = np.diff(st[ok], axis=1)
-    span = st[ok, 9].max() - st[ok, 0].min()
+    span = st[ok, -1].max() - st[ok, 0].min()
     res.append({"waves": int(ok.sum()), "phase_cycles_median": np.median(d, axis=0).round(0).tolist(),
                 "phase_cycles_mean": d.mean(axis=0).round(0).tolist(),
-                "wave_total_median": float(np.median(st[ok, 9] - st[ok, 0])),
+                "wave_total_median": float(np.median(st[ok, -1] - st[ok, 0])),
                 "launch_span_cycles": float(span),
                 "start_spread_cycles": float(np.percentile(st[ok, 0], 99) - st[ok, 0].min())})
 print(json.dumps(res[-1], indent=1))
