@@ -60,7 +60,7 @@ RAYS_BYTES_PER_ENV = 24 + 11 * 4   # k_rays algorithmic HBM bytes/env: read x,y,
 # 11 f32 obs = 44 B
 STEP2_BYTES_PER_ENV = 74 + 38 + 44
 STEP_BYTES_PER_ENV = 218           # whole step, SURVEY.md §8(d)
-PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_steady.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_steady.json")
 
 
 def load_pmc(n):
@@ -78,26 +78,109 @@ def load_pmc(n):
     return out
 
 
-def compute_roofline(pmc, launch_ms):
-    """VALU view of the VALU-bound env kernels: busy fraction of the SIMDs' VALU
-    issue over the launch, from PMC SQ_ACTIVE_INST_VALU (quad-cycles per wave,
-    summed) against 1,024 SIMDs x the launch's cycles at the clock PMC saw
-    (GRBM_GUI_ACTIVE / 8 XCDs per launch)."""
-    res = {"bound": "valu", "source": pmc.get("source")}
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X FP64 vector
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md chip table)
+# brute-force (unculled) f64 flops of one single-agent env-step at P = 11
+# sensors -- every ray tested against all S boundary segments, 5 full argmin scans
+ALGO_UNCULLED_FLOP_PER_ENV_STEP = 102830
+F64_KEYS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
+F32_KEYS = ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32")
+
+
+def _flop(c, keys):
+    """FLOP of a launch from its wave-level VALU instruction counts: 64 lanes x
+    (add + mul + transcendental + 2 x fma).  An upper bound (full exec mask)."""
+    if not all(k in c for k in keys):
+        return None
+    add, mul, fma, trans = (c[k] for k in keys)
+    return 64.0 * (add + mul + trans + 2.0 * fma)
+
+
+def compute_roofline(pmc, launch_ms, n, waves=None):
+    """The §8(d) compute roofline of the VALU-bound env step (SURVEY.md:456-457):
+    EXECUTED FP64 flops per launch from the committed steady-state PMC counts
+    (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, same launch size) over the LIVE
+    launch duration, against the 78.6 TF FP64 vector peak; the brute-force
+    count of §8(d) alongside as the algorithmic (unculled) work -- the culled
+    kernel executes far less of it, bit-exactly.  Also the VALU busy fraction
+    (SQ_ACTIVE_INST_VALU quad-cycles x 4 over 1,024 SIMDs x the launch's cycles,
+    GRBM_GUI_ACTIVE / 8 XCDs) and the live wave-slot utilisation of the
+    recorded production launches."""
+    res = {"bound": "valu-fp64", "kernel": "k_step2", "source": pmc.get("source"), "envs_per_launch": n,
+           "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "fp64_flop_per_env_step_algorithmic_unculled": ALGO_UNCULLED_FLOP_PER_ENV_STEP,
+           "flop_note": "executed flops = 64 lanes x (add + mul + trans + 2 fma) wave instructions (PMC, an upper "
+                        "bound: full exec mask); algorithmic_unculled = SURVEY.md §8(d) brute force (every segment "
+                        "of every ray, full argmin scans)"}
+    per_env = 0.0
     for k, t in launch_ms.items():
         c = pmc.get(k, {})
+        d = {"launch_ms_live": round(t, 5) if np.isfinite(t) else None}
         act, gui = c.get("SQ_ACTIVE_INST_VALU"), c.get("GRBM_GUI_ACTIVE")
-        if act is None or gui is None or not np.isfinite(t):
-            continue
-        cycles = gui / 8.0  # GRBM_GUI_ACTIVE: summed over the 8 XCDs
-        busy = 4.0 * act / (1024.0 * cycles)
-        res[k] = {"valu_busy_frac": round(busy, 4), "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
-                  "launch_cycles": round(cycles), "launch_ms_pmc": round(cycles / 2.4e9 * 1e3, 5),
-                  "launch_ms_live": round(t, 5)}
-    if "k_step2" in res:
-        res["frac"] = res["k_step2"]["valu_busy_frac"]
-        res["kernel"] = "k_step2"
+        if act is not None and gui is not None:
+            cycles = gui / 8.0  # GRBM_GUI_ACTIVE: summed over the 8 XCDs
+            d.update(valu_busy_frac=round(4.0 * act / (1024.0 * cycles), 4), launch_cycles=round(cycles),
+                     valu_insts_per_launch=c.get("SQ_INSTS_VALU"))
+        f64, f32 = _flop(c, F64_KEYS), _flop(c, F32_KEYS)
+        if f64 is not None:
+            d["fp64_flop_per_launch"] = round(f64)
+            d["fp64_flop_per_env"] = round(f64 / n, 1)
+            if k != "k_rays":
+                per_env += f64 / n
+            if np.isfinite(t) and t > 0:
+                tf = f64 / (t * 1e-3) / 1e12
+                d["fp64_achieved_tflops"] = round(tf, 3)
+                d["fp64_frac"] = round(tf / FP64_VECTOR_PEAK_TFLOPS, 4)
+        if f32 is not None:
+            d["fp32_flop_per_launch"] = round(f32)
+            if np.isfinite(t) and t > 0:
+                tf = f32 / (t * 1e-3) / 1e12
+                d["fp32_achieved_tflops"] = round(tf, 3)
+                d["fp32_frac"] = round(tf / FP32_VECTOR_PEAK_TFLOPS, 4)
+        res[k] = d
+    s2 = res.get("k_step2", {})
+    if "fp64_frac" in s2:
+        res["achieved"] = s2["fp64_achieved_tflops"]
+        res["frac"] = s2["fp64_frac"]
+        res["fp64_flop_per_env_step_executed"] = round(per_env, 1)
+        res["executed_over_unculled"] = round(per_env / ALGO_UNCULLED_FLOP_PER_ENV_STEP, 4)
+    res["valu_busy_frac"] = s2.get("valu_busy_frac")
+    if waves:
+        res["wave_slots"] = waves
+        res["wave_slot_utilisation"] = waves.get("wave_slot_utilisation")
     return res
+
+
+def wave_slots(env, n_launches, max_step2=16):
+    """Live wave-slot view of the recorded production k_step2 launches (rx_profile
+    per-wave stamps): utilisation = summed wave time / (8,192 slots x span), the
+    drain after the active waves fall below half the slots, the last wave start,
+    and the ray-wave duration / end by class (tools/wave_profile.py summarize)."""
+    from tools.wave_profile import summarize
+    sched = env.schedule()
+    n_rw = sched["reward_lpe"] * ((sched["dyn_waves"] + 7) // 8 * 8)
+    tab = env.ray_wave_table()
+    got = []
+    for k in range(n_launches):
+        try:
+            st, en, kind, _ = env.profile_waves(k)
+        except Exception:  # noqa: BLE001 -- past the record
+            break
+        if kind == "k_step2":
+            got.append(summarize(st, en, n_rw, tab["cls"], tab["sub"]))
+            if len(got) >= max_step2:
+                break
+    if not got:
+        return None
+    m = lambda key: round(float(np.mean([g[key] for g in got])), 3)  # noqa: E731
+    classes = sorted(got[0].get("ray_dur_us_by_class", {}))
+    return {"launches": len(got), "span_us": m("span_us"), "wave_slot_utilisation": m("wave_slot_utilisation"),
+            "tail_after_half_slots_us": m("tail_after_half_slots_us"), "last_wave_start_us": m("last_wave_start_us"),
+            "ray_dur_us_by_class": {j: round(float(np.mean([g["ray_dur_us_by_class"][j] for g in got])), 2)
+                                    for j in classes},
+            "ray_end_us_by_class_max": {j: round(float(np.mean([g["ray_end_us_by_class_max"][j] for g in got])), 2)
+                                        for j in classes},
+            "slots": 8192, "source": "live: rx_profile per-wave stamps of the instrumented production launches"}
 
 
 _MARKS = os.environ.get("RX_BENCH_MARKS") == "1"
@@ -122,9 +205,12 @@ def seed1_pool(n_total):
     return pool, widths
 
 
-def gae_roofline(n_envs, dev, T=128, reps=20):
+def gae_roofline(n_envs, dev, T=512, reps=20):
     """k_gae (agent/ppo.py:134-154) on a [T, N] rollout: HBM-bound, 20 B per
-    (t, env) element (read r, v, d; write A, R; f32) -- SURVEY.md §8(d)."""
+    (t, env) element (read r, v, d; write A, R; f32) -- SURVEY.md §8(d).  At the
+    default T = 512 the five [T, N] arrays (65,536 envs: 671 MB) exceed the
+    256 MiB Infinity Cache, so replaying the same buffers measures HBM; at
+    T = 128 (168 MB) they stay cache-resident (reported as such)."""
     from rx.gae import compute_gae
     g = torch.Generator(device=dev).manual_seed(0)
     r = torch.randn((T, n_envs), generator=g, device=dev)
@@ -143,8 +229,12 @@ def gae_roofline(n_envs, dev, T=128, reps=20):
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1]) / reps
     gbs = 20.0 * T * n_envs / (ms * 1e-3) / 1e9
+    ws = 20 * T * n_envs
     return {"kernel": "k_gae", "T": T, "N": n_envs, "avg_launch_ms": round(ms, 5), "bound": "hbm",
-            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "working_set_bytes": ws,
+            "residency": "exceeds the 256 MiB Infinity Cache: HBM" if ws > (256 << 20) else
+                         "fits the 256 MiB Infinity Cache: L3-assisted, not an HBM figure"}
 
 
 def _cpu_model():
@@ -159,35 +249,6 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
-def _np_envs(pool, widths, n_envs, first=0):
-    from oracle.np_env import NpRacingEnv, NpTrack
-    from rx.track import TrackGeometry
-    envs, geo = [], {}
-    for i in range(first, first + n_envs):
-        key = (id(pool[i]), widths[i])
-        if key not in geo:
-            g = TrackGeometry(pool[i], widths[i])
-            geo[key] = NpTrack(g.waypoints, g.normals, g.segment_cache["starts"], g.segment_cache["v2"],
-                               g.track_width, g.get_start_pos())
-        envs.append(NpRacingEnv(geo[key], 11))
-    return envs
-
-
-def _cpu_worker(args):
-    """Mode B worker: ONE env on one core (SyncVectorEnv of 1), random actions, bounded time."""
-    cp, width, budget_s, seed = args
-    from oracle.np_env import NpSyncVectorEnv
-    venv = NpSyncVectorEnv(_np_envs([cp], [width], 1))
-    venv.reset()
-    rng = np.random.default_rng(seed)
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        venv.step(np.array([[rng.uniform(-1, 1), rng.uniform(0, 1)]], dtype=np.float32))
-        steps += 1
-    return steps, time.perf_counter() - t0
-
-
 def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
     """BASELINE.md §3 CPU baseline on this host: oracle/np_env.py (the reference's
     NumPy step restated, bit-exact vs the reference's golden vectors).
@@ -198,13 +259,13 @@ def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
     host sets it (the GPU box exposes the whole machine's CPUs but gives one
     GPU's job a 16-core share).  Mode A: the reference's plumbing, one process
     stepping 16 envs sequentially (SyncVectorEnv, configs/base_config.py)."""
-    import multiprocessing as mp
+    from oracle.cpu_baseline import np_envs, run_workers
     from oracle.np_env import NpSyncVectorEnv
     aff = len(os.sched_getaffinity(0))
     cap = os.environ.get("OMP_NUM_THREADS")
     cores = min(aff, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else aff
     # Mode A
-    venv = NpSyncVectorEnv(_np_envs(pool, widths, n_envs))
+    venv = NpSyncVectorEnv(np_envs(pool, widths, n_envs))
     venv.reset()
     rng = np.random.default_rng(0)
     steps = 0
@@ -216,19 +277,9 @@ def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
     dt = time.perf_counter() - t0
     mode_a = {"value": round(steps * n_envs / dt, 1), "unit": "env-steps/s", "cores": 1,
               "sample": f"{n_envs} envs x {steps} sequential steps ({steps * n_envs} env-steps, {dt:.1f} s)"}
-    # Mode B
-    ctx = mp.get_context("spawn")
-    old = os.environ.get("OPENBLAS_NUM_THREADS")
-    os.environ["OPENBLAS_NUM_THREADS"] = "1"  # inherited by the spawned workers before they import numpy
-    try:
-        with ctx.Pool(cores) as p:
-            res = p.map(_cpu_worker, [(pool[i % len(pool)], widths[i % len(pool)], budget_s, i)
-                                      for i in range(cores)])
-    finally:
-        if old is None:
-            os.environ.pop("OPENBLAS_NUM_THREADS", None)
-        else:
-            os.environ["OPENBLAS_NUM_THREADS"] = old
+    # Mode B: torch-free child processes (oracle/cpu_baseline.py), each exits 0 on its own
+    res = run_workers([(pool[i % len(pool)], widths[i % len(pool)], budget_s, i) for i in range(cores)],
+                      timeout_s=budget_s + 600)
     tot = sum(r[0] for r in res)
     el = max(r[1] for r in res)
     return {"value": round(tot / el, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
@@ -236,6 +287,8 @@ def cpu_baseline(pool, widths, budget_s=12.0, n_envs=16):
             "sample": f"oracle/np_env.py NumPy restatement of RacingEnv.step (bit-exact vs the reference's golden "
                       f"vectors), Mode B: {cores} processes x 1 env, {tot} env-steps in {el:.1f} s, seed-1 pool, "
                       f"uniform random actions, OPENBLAS_NUM_THREADS=1",
+            "workers": "python -m oracle.cpu_baseline child processes (numpy/scipy only, never torch or HIP), "
+                       "each exits 0 on its own",
             "mode_a_one_core_16_envs": mode_a}
 
 
@@ -368,6 +421,81 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
             "allreduce_per_update_expected": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
             "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
             "note": "KL early stop off, device shuffles; timed after one warm-up update"}
+
+
+def selfplay_leg(dev, envs, T, updates, pool_size=5):
+    """BASELINE.json configs[3]: two-car self-play PPO (agent/self_play_ppo.py:70-187)
+    at ``envs`` envs with an opponent pool of ``pool_size``: rx.selfplay.SelfPlayPPO's
+    own train_iter (pool advance, opponent draw + env rebuild, rollout with the
+    frozen opponent's rx_policy_act in the loop, GAE, the 10 x 16 fused update).
+    The snapshot cadence is shortened to every update (the reference's 15) so the
+    pool is full (pool_size snapshots, FIFO) before timing; KL early stop off and
+    device shuffles so every update does the same work; no checkpoint files.
+    Then one more update with a sync between phases gives the split."""
+    from rx.configs import self_play_config
+    from rx.envs import MultiRacingEnv
+    from rx.selfplay import SelfPlayPPO
+    from rx.track import gen_tracks
+    warm = pool_size + 1
+    cfg = self_play_config(num_envs=envs, num_steps=T, kl_target=1e9, shuffle="device", snapshot_freq=1,
+                           pool_size=pool_size, checkpoint=False)
+    cfg["total_timesteps"] = (warm + updates + 1) * cfg["batch_size"]
+    random.seed(1)
+    np.random.seed(1)
+    torch.manual_seed(1)
+    pool = gen_tracks(envs, seed=1)
+    widths = [np.random.randint(6, 10) for _ in range(envs)]
+    t = SelfPlayPPO(lambda i: MultiRacingEnv(2, 11, pool, i, widths), cfg, device=dev)
+    it = t.train_iter()
+    for _ in range(warm):  # pool filled, graphs captured, workspaces sized
+        next(it)
+    torch.cuda.synchronize()
+    pool_before = len(t.opponent_pool)
+    gc.collect()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(updates):
+        next(it)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    gc.enable()
+    # phase split of one more update, synchronised between phases
+    u = warm + updates
+    obs, actions, logprobs, dones, rewards, values = t._buffers()
+    nobs = t.envs.buf["obs"].clone()
+    nd = torch.zeros(t.num_local_envs, device=dev)
+    ph = {}
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    t.advance_pool(u)
+    t.update_opponent()
+    torch.cuda.synchronize()
+    b = time.perf_counter()
+    out = t.collect_rollout(obs, actions, logprobs, dones, rewards, values, nobs, nd)
+    torch.cuda.synchronize()
+    c = time.perf_counter()
+    obs, actions, logprobs, dones, rewards, values, nobs, nd, _ = out
+    with torch.no_grad():
+        nv = t.agent.get_value(nobs).flatten()
+    adv, ret = t.compute_advantages(rewards, dones, values, nv, nd)
+    torch.cuda.synchronize()
+    d = time.perf_counter()
+    t.ppo_update(adv, ret, values, logprobs, actions, obs)
+    torch.cuda.synchronize()
+    e = time.perf_counter()
+    ph = {"opponent_draw_and_rebuild_ms": round((b - a) * 1e3, 3), "rollout_ms": round((c - b) * 1e3, 3),
+          "gae_ms": round((d - c) * 1e3, 3), "update_ms": round((e - d) * 1e3, 3),
+          "rollout_env_steps_per_s": round(T * envs / (c - b), 1)}
+    B = T * envs
+    res = {"value": round(B * updates / el, 1), "unit": "train env-steps/s (agent-steps = 2x)", "updates": updates,
+           "ms_per_update": round(el / updates * 1e3, 3), "envs": envs, "cars_per_env": 2, "num_steps": T,
+           "batch": B, "pool_size": pool_size, "pool_filled_before_timing": pool_before,
+           "opponent": "frozen pool snapshot, one rx_policy_act launch per step over all envs",
+           "phase_split_one_update": ph,
+           "note": "BASELINE configs[3]; snapshot every update (reference: 15) so the pool is full before timing; "
+                   "KL early stop off, device shuffles, no checkpoint files; timed after the pool-filling updates"}
+    t.envs.close()
+    return res
 
 
 def _lib_path():
@@ -505,9 +633,15 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=128,
                     help="instrumented steps AFTER the timed region: per-kernel durations from per-wave device "
                          "wall-clock stamps (0 = none)")
+    ap.add_argument("--counter-steps", type=int, default=16,
+                    help="after timing, this many steps with the per-wave culling counters on (executed work)")
     ap.add_argument("--ppo-updates", type=int, default=2,
                     help="also time this many PPO updates (configs[1] per GPU; 0 = skip), reported as 'ppo_train'")
     ap.add_argument("--ppo-envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--selfplay-updates", type=int, default=2,
+                    help="also time this many two-car self-play PPO updates (configs[3], pool 5; 0 = skip), "
+                         "reported as 'selfplay_train'")
+    ap.add_argument("--selfplay-envs", type=int, default=8192)
     ap.add_argument("--ppo-steps", type=int, default=128)
     ap.add_argument("--no-time-to-90", action="store_true", help="skip the PPO wall-clock-to-90%% runs")
     ap.add_argument("--dist-backend", default="nccl",
@@ -697,12 +831,35 @@ def main():
     # production launches (k_kin1, k_step2) on every other step; on the others the dynamics
     # phase and the raycast run as separate launches so the raycast has a duration of its own
     prof = {}
+    waves = None
     if args.profile_steps > 0:
         events = {k: ("step" if k % 2 == 0 else "split") for k in range(args.profile_steps)}
         env0.profile(1)
         env0.profile(0)
         prof_el = timed(one_step, args.profile_steps, events)
         prof = env0.profile_read()
+        waves = wave_slots(env0, args.profile_steps * 3) if G == 1 else None
+    # ---- executed-work counters (after timing): per ray wave its box tests and leaf scans,
+    # per REWARD wave its waypoint-box tests and leaf scans (rx_io.counters, one atomic per wave)
+    work = None
+    if args.counter_steps > 0 and G == 1:
+        env0.enable_counters(True)
+        for _ in range(args.counter_steps):
+            one_step()
+        torch.cuda.synchronize()
+        cnt = env0.read_counters()
+        env0.enable_counters(False)
+        sch = env0.schedule()
+        steps_n = args.counter_steps * n
+        work = {k: v for k, v in cnt.items()}
+        work.update(steps=args.counter_steps, envs=n,
+                    ray_box_tests_per_ray_wave=round(cnt["ray_chunk_tests"] / (args.counter_steps * sch["ray_waves"]), 2),
+                    ray_leaf_scans_per_ray_wave=round(cnt["ray_chunks_scanned"] / (args.counter_steps * sch["ray_waves"]),
+                                                      2),
+                    ray_leaf_scans_per_env_step=round(cnt["ray_chunks_scanned"] / steps_n, 3),
+                    wp_leaf_scans_per_env_step=round(cnt["wp_chunks_scanned"] / steps_n, 3),
+                    note="counted per wave (a wave's box test / leaf scan covers its 64 lanes); scheduling-only "
+                         "counters, after the timed region")
     for e in envs:
         e.close()
     async_probe = None
@@ -719,12 +876,17 @@ def main():
         for e in a_envs:
             e.close()
     gae = gae_roofline(E, dev) if rank == 0 else None
+    if gae is not None:
+        gae["cache_resident_T128"] = gae_roofline(E, dev, T=128)
     ppo = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
                   args.ppo_updates) if args.ppo_updates > 0 else None
     # BASELINE configs[1] is named "PPO bf16": the same leg with the bf16 policy kernels
     # (bf16 MFMA operands, f32 accumulation, f32 master weights / Adam), at N = 1 only
     ppo_bf16 = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
                        args.ppo_updates, "bf16") if args.ppo_updates > 0 and world == 1 else None
+    sp = None
+    if args.selfplay_updates > 0 and world == 1:
+        sp = selfplay_leg(dev, args.selfplay_envs, args.ppo_steps, args.selfplay_updates)
     tt90 = None
     if world == 1 and not args.no_time_to_90:
         tt90 = time_to_90([(16, 2048, "numpy"), (4096, 128, "device")])
@@ -772,7 +934,9 @@ def main():
                          "avg_launch_ms": round(step2_ms, 5),
                          "note": "the step is VALU-bound (branchy f64 ray/segment math): the HBM fraction is "
                                  "expected to be tiny; see compute_roofline"},
-            "compute_roofline": compute_roofline(pmc, {"k_step2": step2_ms, "k_rays": ray_ms}),
+            "compute_roofline": compute_roofline(pmc, {"k_step2": step2_ms, "k_kin1": kin_ms, "k_rays": ray_ms}, n,
+                                                 waves),
+            "executed_work": work,
             "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
             "kernel_launches": {k: v[1] for k, v in prof.items()},
             "kernel_timing": f"{args.profile_steps} instrumented steps after the timed region (per-wave device "
@@ -790,6 +954,7 @@ def main():
             "async_stream_groups": async_probe,
             "ppo_train": ppo,
             "ppo_train_bf16": ppo_bf16,
+            "selfplay_train": sp,
             "time_to_90": tt90,
         }
         if cpu is not None:

@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 18
+#define RX_ABI_VERSION 19
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -104,6 +104,15 @@ typedef struct {
   int32_t seg_filter;      /* float32 pre-filter before each exact segment test: 0 auto (on), 1 on, -1 off */
   int32_t box_quadrants;   /* quadrant-ordered float32 box tables for single-quadrant ray waves: 0 auto (on),
                               1 on, -1 off */
+  /* ABI v19: ray-wave dispatch (ray_order 2).  Class j of a 64-env group = its j-th wave of
+     direction-sorted ray tasks (the group's cars head alike, so class j ~ sensor ray j). */
+  int32_t ray_dispatch;    /* order in which the classes are dispatched: 0 auto (3), 1 centre classes first,
+                              2 ascending j, 3 edge classes first / centre last, -1 group-octet-major */
+  int32_t ray_tail;        /* the LAST ray_tail classes of that order (the tail of the launch, whose waves
+                              run as the chip drains) cast at ray_tail_lpr lanes per ray: each of their
+                              64-task waves becomes ray_tail_lpr waves of 64 / ray_tail_lpr tasks.  Only
+                              with 1 lane per ray elsewhere.  0 auto, -1 none, 1 .. 16 */
+  int32_t ray_tail_lpr;    /* 0 auto (2), 2 or 4 */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -171,12 +180,14 @@ int rx_sensor_angles(const rx_env* h, double* out);
  * reference has no counterpart (its SyncVectorEnv steps envs in order). */
 int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort_shift);
 
-/* Diagnostics (ABI v17): the launch schedule rx_assign resolved from rx_config
+/* Diagnostics (ABI v17, v19): the launch schedule rx_assign resolved from rx_config
  * for this handle, out int32 [RX_SCHEDULE_W] = split step (0/1), wide kernels
  * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
  * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
- * tables (0/1), dynamics waves, ray waves.  Host only, no device call. */
-#define RX_SCHEDULE_W 10
+ * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
+ * classes, tail lanes per ray, first tail wave (-1 = none).  Host only, no
+ * device call. */
+#define RX_SCHEDULE_W 14
 int rx_schedule(const rx_env* h, int32_t* out);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env
@@ -264,6 +275,14 @@ int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count);
  * per-wave cost by dispatch order).  No counterpart in the reference. */
 int rx_profile_waves(rx_env* h, int32_t launch, uint64_t* start, uint64_t* end, int32_t cap, int32_t* n_waves,
                      int32_t* kind, int32_t* khz);
+/* Diagnostics (ABI v19): the ray-wave table rx_assign built, host int32 [cap][4]
+ * = (track slot, perm start, first task, task count) per ray wave in dispatch
+ * order (wave i is k_step2 workgroup n_reward + i, k_rays workgroup i);
+ * *n_waves = the table length.  A wave's class j within its 64-env group is
+ * (first task - perm start * A * n_sensors) / 64 (ray_order 2, 1 lane per ray
+ * outside the tail).  Host only, no device call.  No counterpart in the
+ * reference. */
+int rx_ray_waves(const rx_env* h, int32_t* out, int32_t cap, int32_t* n_waves);
 
 /* GAE (agent/ppo.py:134-154), float32, bit-exact lane-per-env recurrence.
  * rewards/values/dones [T][N]; next_value/next_done [N]; adv/returns [T][N]. */

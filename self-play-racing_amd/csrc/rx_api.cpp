@@ -90,6 +90,7 @@ struct rx_env {
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // the env order (perm[0]: env id at each position) and the re-sort's shadow
   DevBuf<rx_wave> dyn_waves, ray_waves;
+  std::vector<rx_wave> ray_waves_h;  // host copy of the ray-wave table (rx_ray_waves)
   DevBuf<int32_t> slot_n;   // envs per slot (ray-major decode)
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
@@ -97,6 +98,9 @@ struct rx_env {
   int32_t ray_lpr = 1;  // lanes per ray task (ray_order 2, not wide): 64 / ray_lpr tasks a ray wave
   int32_t reward_lpe = 1;  // split step, single-agent: lanes per env in k_step2's REWARD half
   int32_t argmin_window = 2;
+  int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
+  int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
+  int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
@@ -302,6 +306,12 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "reward_lpe must be 0 (auto), 1, 2 or 4 (got %d)", cfg->reward_lpe);
   if (cfg->argmin_window < -1 || cfg->argmin_window > 32)
     return fail(RX_EINVAL, "argmin_window must be 0 (auto), -1 (none) or 1 .. 32 (got %d)", cfg->argmin_window);
+  if (cfg->ray_dispatch < -1 || cfg->ray_dispatch > 3)
+    return fail(RX_EINVAL, "ray_dispatch must be 0 (auto), -1, 1, 2 or 3 (got %d)", cfg->ray_dispatch);
+  if (cfg->ray_tail < -1 || cfg->ray_tail > 16)
+    return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
+  if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
+    return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 1))
     return fail(RX_EINVAL, "dyn_lpe / reward_lpe > 1 are single-agent schedules (n_agents = 2)");
   if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
@@ -363,7 +373,8 @@ int rx_schedule(const rx_env* h, int32_t* out) {
   if (!h->assigned) return fail(RX_ESTATE, "rx_schedule before rx_assign");
   const int32_t v[RX_SCHEDULE_W] = {h->split ? 1 : 0, h->dyn_lpe == 64 ? 1 : 0, h->dyn_lpe, h->ray_lpr, h->reward_lpe,
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
-                                    h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves};
+                                    h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
+                                    h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -470,6 +481,12 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->reward_lpe = (A == 1 && N <= RX_REWARD_LPE2_N) ? 2 : 1;
   if (c.reward_lpe != 0) h->reward_lpe = c.reward_lpe;
   h->split = c.split >= 0;
+  // ray-wave class order and the tail split (ABI v19; scheduling only)
+  h->ray_dispatch = c.ray_dispatch == 0 ? RX_RAY_DISPATCH : (c.ray_dispatch < 0 ? 0 : c.ray_dispatch);
+  h->ray_tail_lpr = c.ray_tail_lpr == 0 ? RX_RAY_TAIL_LPR : c.ray_tail_lpr;
+  h->ray_tail = c.ray_tail == 0 ? RX_RAY_TAIL : (c.ray_tail < 0 ? 0 : c.ray_tail);
+  if (h->cfg.ray_order != 2 || h->ray_lpr != 1 || h->ray_dispatch == 0 || h->dyn_lpe == 64) h->ray_tail = 0;
+  h->ray_tail_from = -1;
   const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
@@ -510,38 +527,69 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     int maxw = 0;
     for (size_t g = 0; g < n_groups; ++g) maxw = std::max(maxw, ray_groups[g] - (g ? ray_groups[g - 1] : 0));
     const size_t padded = (n_groups + 7) / 8 * 8;
-    std::vector<rx_wave> placed(padded * maxw, rx_wave{0, 0, 0, 0});
-    // RX_RAY_DISPATCH (rx_internal.h): 0 = group-octet-major as just described; 1..3 =
+    // ray_dispatch (rx_config, ABI v19): 0 = group-octet-major as just described; 1..3 =
     // class-major, every group's class-j wave in one run, the classes in the order
     // 1 centre first (|2j - (maxw - 1)| ascending), 2 ascending j, 3 edge classes first
     // (|2j - (maxw - 1)| descending, the default).  The XCD of a group's waves is g % 8 in
     // every mode (padded is a multiple of 8).  Dispatch order is scheduling only.
+    const int mode = h->ray_dispatch;
     std::vector<int> rank(maxw);
     std::iota(rank.begin(), rank.end(), 0);
-    if (RX_RAY_DISPATCH == 1 || RX_RAY_DISPATCH == 3) {
+    if (mode == 1 || mode == 3) {
       std::vector<int> cls(maxw);
       std::iota(cls.begin(), cls.end(), 0);
       auto off = [&](int j) { return std::abs(2 * j - (maxw - 1)); };
-      std::stable_sort(cls.begin(), cls.end(), [&](int x, int y) {
-        return RX_RAY_DISPATCH == 1 ? off(x) < off(y) : off(x) > off(y);
-      });
+      std::stable_sort(cls.begin(), cls.end(), [&](int x, int y) { return mode == 1 ? off(x) < off(y) : off(x) > off(y); });
       for (int r = 0; r < maxw; ++r) rank[cls[r]] = r;
     }
 #ifdef RX_RAY_ORDER_LIST
-    {  // A/B builds: an explicit class order for 11-class groups (RX_RAY_DISPATCH >= 1)
+    {  // A/B builds: an explicit class order for 11-class groups (ray_dispatch >= 1)
       const int lst[] = RX_RAY_ORDER_LIST;
-      if (RX_RAY_DISPATCH >= 1 && maxw == (int)(sizeof(lst) / sizeof(lst[0])))
-        for (int r = 0; r < maxw; ++r) rank[lst[r]] = r;
+      if (mode >= 1 && maxw == (int)(sizeof(lst) / sizeof(lst[0]))) {
+        // the list must be a permutation of 0..maxw-1: a repeated class would give two
+        // ray waves one placed slot (one silently overwritten, its rays never cast)
+        std::vector<bool> seen(maxw, false);
+        for (int r = 0; r < maxw; ++r) {
+          if (lst[r] < 0 || lst[r] >= maxw || seen[lst[r]])
+            return fail(RX_EINVAL, "RX_RAY_ORDER_LIST is not a permutation of 0..%d", maxw - 1);
+          seen[lst[r]] = true;
+          rank[lst[r]] = r;
+        }
+      }
     }
 #endif
+    // The tail split (ray_tail, class-major modes only): the waves of the last ray_tail
+    // ranks run as the chip drains, where a wave's latency chain -- not the shared VALU --
+    // sets its duration.  Each of their 64-task records becomes m = ray_tail_lpr records of
+    // 64 / m tasks, cast at m lanes per ray (the lanes split each scanned leaf: a shorter
+    // chain, the same result, DESIGN.md §3 "Lanes per ray").  Rank r occupies mult[r]
+    // consecutive runs of `padded` slots; sub-record s of group g's rank-r wave goes to
+    // base[r] + (s * (padded / 8) + g / 8) * 8 + g % 8, so it keeps the group's XCD.  All
+    // tail waves sit at the end of the table: ray_tail_from is the first of them.
+    const int tail = mode == 0 ? 0 : std::min(h->ray_tail, maxw);
+    std::vector<size_t> mult(maxw, 1), base(maxw + 1, 0);
+    for (int r = maxw - tail; r < maxw; ++r) mult[r] = (size_t)h->ray_tail_lpr;
+    for (int r = 0; r < maxw; ++r) base[r + 1] = base[r] + mult[r] * padded;
+    std::vector<rx_wave> placed(base[maxw], rx_wave{0, 0, 0, 0});
     for (size_t g = 0; g < n_groups; ++g) {
       const int w0 = g ? ray_groups[g - 1] : 0;
       for (int j = 0; w0 + j < ray_groups[g]; ++j) {
-        const size_t slot = RX_RAY_DISPATCH == 0 ? ((g / 8) * maxw + j) * 8 + g % 8
-                                                 : ((size_t)rank[j] * (padded / 8) + g / 8) * 8 + g % 8;
-        placed[slot] = ray[w0 + j];
+        const rx_wave w = ray[w0 + j];
+        if (mode == 0) {
+          placed[((g / 8) * maxw + j) * 8 + g % 8] = w;
+          continue;
+        }
+        const int r = rank[j];
+        const int m = (int)mult[r], per = tpw / m;
+        for (int sub = 0; sub < m; ++sub) {
+          const size_t slot = base[r] + ((size_t)sub * (padded / 8) + g / 8) * 8 + g % 8;
+          placed[slot] = rx_wave{w.track, w.perm_start, w.task_start + sub * per,
+                                 std::max(0, std::min(per, w.count - sub * per))};
+        }
       }
     }
+    h->ray_tail = tail;
+    h->ray_tail_from = tail > 0 ? (int32_t)base[maxw - tail] : -1;
     ray.swap(placed);
   }
   RX_HIP(hipSetDevice(h->cfg.device));
@@ -594,10 +642,12 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   }
   if ((rc = upload(h->dyn_waves, dyn.data(), dyn.size()))) return rc;
   if ((rc = upload(h->ray_waves, ray.data(), ray.size()))) return rc;
+  h->ray_waves_h = ray;
   h->n_dyn_waves = (int32_t)dyn.size();
   h->n_ray_waves = (int32_t)ray.size();
   h->assigned = true;
   h->sort_pending = false;
+  h->sort_hist_done = false;  // the histogram was re-uploaded as zeros above (or sorting is off)
   if (h->bound && h->st.track) RX_HIP(hipMemcpy(h->st.track, track_of_env, N * sizeof(int32_t), hipMemcpyHostToDevice));
   if (h->bound) return sync_state(h, 0);  // the new wave order: re-read the caller's arrays
   return RX_OK;
@@ -712,6 +762,8 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.ray_order = h->cfg.ray_order;
   a.dyn_lpe = h->dyn_lpe;
   a.ray_lpr = h->ray_lpr;
+  a.ray_tail_from = h->ray_tail_from;
+  a.ray_tail_lpr = h->ray_tail_lpr;
   a.reward_lpe = h->reward_lpe;
   a.argmin_window = h->argmin_window;
   a.slot_nenv = h->slot_n.p;
@@ -758,6 +810,14 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
   if (dyn && h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0) {
     a.sort_keys = h->keys_in.p;
+    // The histogram is zero unless sort_hist_done, when it holds the counts of
+    // the keys this launch is about to overwrite (keys requested again before
+    // their sort ran: rx_step_phases(1) twice, or a reset in between): clear it,
+    // so the fused count below, or k_sort_hist, starts from zero.
+    if (h->sort_hist_done) {
+      RX_HIP(hipMemsetAsync(h->sort_hist.p, 0, (size_t)h->sort_bins * sizeof(uint32_t), s));
+      h->sort_hist_done = false;
+    }
     h->sort_pending = true;
   }
   if (split) {
@@ -882,6 +942,21 @@ int rx_profile_waves(rx_env* h, int32_t launch, uint64_t* start, uint64_t* end, 
   }
   *n_waves = stride;
   *kind = h->prof_kinds[launch];
+  return RX_OK;
+}
+
+int rx_ray_waves(const rx_env* h, int32_t* out, int32_t cap, int32_t* n_waves) {
+  if (!h || !n_waves || (cap > 0 && !out)) return fail(RX_EINVAL, "rx_ray_waves: null argument");
+  if (!h->assigned) return fail(RX_ESTATE, "rx_ray_waves before rx_assign");
+  const size_t n = h->ray_waves_h.size();
+  for (size_t i = 0; i < n && (int64_t)i < (int64_t)cap; ++i) {
+    const rx_wave& w = h->ray_waves_h[i];
+    out[4 * i + 0] = w.track;
+    out[4 * i + 1] = w.perm_start;
+    out[4 * i + 2] = w.task_start;
+    out[4 * i + 3] = w.count;
+  }
+  *n_waves = (int32_t)n;
   return RX_OK;
 }
 

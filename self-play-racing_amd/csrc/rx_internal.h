@@ -87,6 +87,14 @@ struct rx_track_view {
 #ifndef RX_RAY_DISPATCH
 #define RX_RAY_DISPATCH 3
 #endif
+// rx_config.ray_tail / ray_tail_lpr automatic values: the last RX_RAY_TAIL classes of the
+// dispatch order cast at RX_RAY_TAIL_LPR lanes per ray (0 = no tail split)
+#ifndef RX_RAY_TAIL
+#define RX_RAY_TAIL 0
+#endif
+#ifndef RX_RAY_TAIL_LPR
+#define RX_RAY_TAIL_LPR 2
+#endif
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them
@@ -136,6 +144,8 @@ struct rx_kargs {
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
   int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
   int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
+  int32_t ray_tail_from;  // ray waves >= this one (the dispatch tail) hold 64 / ray_tail_lpr tasks each, cast at
+  int32_t ray_tail_lpr;   // ray_tail_lpr lanes per ray (2 or 4); -1 = no tail split (rx_config.ray_tail)
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);

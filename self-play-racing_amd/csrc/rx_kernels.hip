@@ -1761,6 +1761,24 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
   a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 
+// A ray wave of the table: at the schedule's LPR lanes per ray, or -- for the
+// dispatch tail (rx_config.ray_tail: the waves at and after a.ray_tail_from,
+// 64 / ray_tail_lpr tasks each, rx_assign) -- at ray_tail_lpr lanes per ray.
+// Only one-lane-per-ray schedules have a tail.
+template <int A, int LPR>
+__device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
+  if constexpr (LPR == 1) {
+    if (a.ray_tail_from >= 0 && wave >= a.ray_tail_from) {
+      if (a.ray_tail_lpr == 4)
+        rays_body<A, 4>(a, wave);
+      else
+        rays_body<A, 2>(a, wave);
+      return;
+    }
+  }
+  rays_body<A, LPR>(a, wave);
+}
+
 template <int A>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
@@ -1770,7 +1788,7 @@ __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   else if (a.ray_lpr == 2)
     rays_body<A, 2>(a, wave);
   else
-    rays_body<A, 1>(a, wave);
+    rays_dispatch<A, 1>(a, wave);
   prof_end(a, wave, prof_t0);
 }
 
@@ -1862,7 +1880,7 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
       dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
     add_episode_stats(a, ep);
   } else {
-    rays_body<A, LPR>(a, b - n_rw);
+    rays_dispatch<A, LPR>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
 }

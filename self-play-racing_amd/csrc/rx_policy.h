@@ -22,16 +22,23 @@ struct Lay {  // flat parameter offsets, module.parameters() order; Pp = partial
 // where ocml's tanhf takes ~30 and a small-|x| polynomial branch ~15.  Absolute
 // error <= 1.4e-7 over the whole range (float32 emulation with correctly rounded
 // exp2 / reciprocal: tools/tanh_error.py), i.e. float rounding of the
-// activations; relative error grows only where |x| is tiny and tanh(x) is
-// itself ~x.  The policy's outputs stay within float rounding of torch's
-// forward (tests/test_ppo_fused_gpu.py, tests/test_bf16_gpu.py).  Every kernel
-// that evaluates the policy uses this one function, so k_rollout and
+// activations.  Relative error: the form cancels as |x| -> 0 (1 - 2/(e + 1)
+// with e ~ 1), so below |x| = 2^-12 the result is x itself (tanh x = x (1 -
+// x^2/3 + ...): relative error < 2^-25, i.e. exact in float32 up to rounding);
+// between 2^-12 and ~0.1 the bound is the absolute 1.4e-7, a relative error of
+// up to 1.4e-7 / |x| (6e-4 at 2^-12, 1.4e-6 at 0.1).  tests/test_ppo_fused_gpu.py
+// ::test_policy_act_near_zero_preactivations checks torch parity there with
+// that combined bound.  The policy's outputs stay within float rounding of
+// torch's forward (tests/test_ppo_fused_gpu.py, tests/test_bf16_gpu.py).  Every
+// kernel that evaluates the policy uses this one function, so k_rollout and
 // rx_policy_act stay bit-identical.  (The VALU count matters: k_ppo_grad's
 // forward phase issued ~770 VALU per pass with the polynomial form, 500 with
-// this one, beside 96 MFMAs.)
+// this one, beside 96 MFMAs; the small-|x| select adds 2.)
 __device__ __forceinline__ float tanh_fast(float x) {
-  const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * 2.8853900817779268f);  // exp(2|x|); inf past ~44
-  return __builtin_copysignf(fmaf(__builtin_amdgcn_rcpf(e + 1.0f), -2.0f, 1.0f), x);
+  const float ax = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // exp(2|x|); inf past ~44
+  const float t = __builtin_copysignf(fmaf(__builtin_amdgcn_rcpf(e + 1.0f), -2.0f, 1.0f), x);
+  return ax < 0x1p-12f ? x : t;
 }
 
 // Normal(mu, exp(log_std)).log_prob(a) for one action dim, in torch's operation

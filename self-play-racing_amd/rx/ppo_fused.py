@@ -135,6 +135,9 @@ class FusedMinibatchGrad:
         self._keep_epochs = (perms, stats_out)
         need = self.L.rx_ppo_adv_workspace_doubles(self.mb, E * self.n_mb)
         if self.adv_ws.numel() < need:
+            # a graph captured over adv_stats() / shard_epoch() holds the old buffer's
+            # address: keep it alive for the lifetime of this object, never free it
+            self.__dict__.setdefault("_retired_ws", []).append(self.adv_ws)
             self.adv_ws = torch.empty(need, dtype=torch.float64, device=self.adv_ws.device)
         _lib.check(self.L.rx_ppo_adv_stats_ws(b, E * self.n_mb, _lib.ptr(self.adv_ws), _lib.ptr(stats_out), None,
                                               _lib.stream_ptr(stream)), "rx_ppo_adv_stats_ws")

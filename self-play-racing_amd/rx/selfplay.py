@@ -185,7 +185,11 @@ class SelfPlayPPO(PPO):
         info = ck.get("training_info", {"steps": [], "rewards": [], "opponent_pool_size": []})
         return ck["update"], ck["global_step"], info
 
-    def train(self, resume_from=None):
+    def train_iter(self, resume_from=None):
+        """agent/self_play_ppo.py:70-187 as a generator: yields (update,
+        num_updates, global_step, EpisodeSummary, info) after every update.
+        config["checkpoint"] = False skips the every-10-updates checkpoint files
+        (benchmarks); the default keeps the reference's cadence."""
         c = self.config
         obs, actions, logprobs, dones, rewards, values = self._buffers()
         next_obs = self.envs.buf["obs"].clone()
@@ -197,6 +201,7 @@ class SelfPlayPPO(PPO):
         else:
             start, global_step = 0, 0
             info = {"steps": [], "rewards": [], "opponent_pool_size": []}
+        self._iter_info = info
         for update in range(start, num_updates):
             self.advance_pool(update)
             self.update_opponent()
@@ -211,11 +216,18 @@ class SelfPlayPPO(PPO):
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
             global_step += c["batch_size"]
-            if self.checkpoint_due(update) and rdist.rank() == 0:
+            if c.get("checkpoint", True) and self.checkpoint_due(update) and rdist.rank() == 0:
                 self.save_checkpoint(update, global_step, info)
+            yield update, num_updates, global_step, ep, info
+
+    def train(self, resume_from=None):
+        info = None
+        for update, num_updates, global_step, ep, info in self.train_iter(resume_from):
             if ep:
                 info["opponent_pool_size"].append(len(self.opponent_pool))
             self._log(update, num_updates, global_step, ep, info, extra=f" | Pool Size: {len(self.opponent_pool)}")
+        if info is None:  # resumed past the last update: the checkpoint's info
+            info = self._iter_info
         self._save_info(info)
         return info
 

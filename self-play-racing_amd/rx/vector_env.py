@@ -202,7 +202,7 @@ class RacingVectorEnv:
         launch's first wave start, the kernel kind name and the wave-slot count of
         recorded launch ``launch`` (rx_profile_waves; unused slots are NaN)."""
         import ctypes
-        cap = 1 << 20
+        cap = self.__dict__.get("_prof_cap") or self._prof_waves_cap()
         st = np.zeros(cap, np.uint64)
         en = np.zeros(cap, np.uint64)
         n, kind, khz = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
@@ -214,6 +214,34 @@ class RacingVectorEnv:
         t0 = st[live].min() if live.any() else 0
         us = lambda t: np.where(live, (t.astype(np.float64) - float(t0)) * 1e3 / khz.value, np.nan)  # noqa: E731
         return us(st), us(en), _lib.RX_KERNEL_NAMES[kind.value], n.value
+
+    def _prof_waves_cap(self):
+        """Wave slots of a recorded launch (rx_profile_waves with cap 0 reports it)."""
+        import ctypes
+        n, kind, khz = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        z = np.zeros(1, np.uint64)
+        _lib.check(self.L.rx_profile_waves(self._h, 0, z.ctypes.data, z.ctypes.data, 0, ctypes.byref(n),
+                                           ctypes.byref(kind), ctypes.byref(khz)), "rx_profile_waves")
+        self._prof_cap = max(1, n.value)
+        return self._prof_cap
+
+    def ray_wave_table(self):
+        """The ray-wave table in dispatch order (rx_ray_waves, host only): a dict of
+        int arrays track, perm_start, task_start, count, plus per wave its class
+        (the j-th 64 direction-sorted tasks of its 64-env group) and sub-wave
+        (tail waves split a class's 64 tasks over ray_tail_lpr waves)."""
+        n = ctypes.c_int32(0)
+        _lib.check(self.L.rx_ray_waves(self._h, None, 0, ctypes.byref(n)), "rx_ray_waves")
+        t = np.zeros((max(n.value, 1), 4), np.int32)
+        _lib.check(self.L.rx_ray_waves(self._h, t.ctypes.data, n.value, ctypes.byref(n)), "rx_ray_waves")
+        t = t[:n.value]
+        off = t[:, 2].astype(np.int64) - t[:, 1].astype(np.int64) * self.n_agents * self.n_sensors
+        sch = self.schedule()
+        per = np.where(np.arange(len(t)) >= (sch["ray_tail_from"] if sch["ray_tail_from"] >= 0 else len(t)),
+                       64 // max(1, sch["ray_tail_lpr"]), 64 // max(1, sch["ray_lpr"]))
+        return {"track": t[:, 0], "perm_start": t[:, 1], "task_start": t[:, 2], "count": t[:, 3],
+                "cls": np.where(t[:, 3] > 0, off // (64 // max(1, sch["ray_lpr"])), -1),
+                "sub": np.where(t[:, 3] > 0, (off % 64) // per, -1)}
 
     def enable_counters(self, on=True):
         """Per-wave culling counters (rx_io.counters): chunk tests / scans."""

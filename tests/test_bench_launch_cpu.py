@@ -48,3 +48,25 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_cpu_baseline_workers_are_torch_free_and_exit_cleanly():
+    """bench.py's Mode B CPU-baseline workers (oracle/cpu_baseline.py, VERDICT r03
+    #6): fresh child processes that never import torch (so no HIP runtime and no
+    torch signal handlers), exit 0 on their own, and step the oracle env."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
+    from rx.track import gen_tracks
+    from oracle.cpu_baseline import run_workers
+    import numpy as np
+    np.random.seed(1)
+    pool = gen_tracks(2, seed=1)
+    res = run_workers([(pool[0], 7, 0.3, 0), (pool[1], 8, 0.3, 1)], timeout_s=120)
+    assert len(res) == 2 and all(s > 0 and sec >= 0.3 for s, sec in res)
+    arg = json.dumps({"cp": np.asarray(pool[0]).tolist(), "width": 6, "budget_s": 0.1, "seed": 0})
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "self-play-racing_amd")]))
+    r = subprocess.run([sys.executable, "-m", "oracle.cpu_baseline"], input=arg, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["torch_loaded"] is False and out["steps"] > 0

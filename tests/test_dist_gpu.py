@@ -142,3 +142,71 @@ def test_two_rank_action_noise_differs():
     torch.manual_seed(_cfg()["seed"])
     want = torch.empty(64, 2, device="cuda").normal_()
     assert np.array_equal(res[0][0], want.cpu().numpy())
+
+
+def _rccl_worker(port, q):
+    """One rank, process group over RCCL ("nccl") on cuda:0: the fused shard update
+    with every bucket / moment all-reduce a real RCCL all_reduce on device memory
+    (rx.dist.all_reduce_sum is replaced, since rx.dist.active() is False at world 1)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as td
+    import rx.dist as rd
+    from tests.test_optim_gpu import _rollout
+    from tests.test_ppo_fused_gpu import _trainer
+    torch.cuda.set_device(0)
+    td.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert td.get_backend() == "nccl"
+        calls = {"n": 0, "bytes": 0, "dev": True}
+
+        def rccl_sum(t):
+            calls["n"] += 1
+            calls["bytes"] += t.numel() * t.element_size()
+            calls["dev"] &= t.is_cuda
+            td.all_reduce(t)  # RCCL, on its own stream, ordered after librx's launches on the current one
+            return t
+
+        res = []
+        for shard in (False, True):
+            t = _trainer(graph_update=False, shard_update=shard, kl_target=1e9)
+            data = _rollout(t)
+            np.random.seed(4)
+            saved = rd.all_reduce_sum
+            if shard:
+                rd.all_reduce_sum = rccl_sum
+            try:
+                for u in range(2):
+                    t._anneal(u, 4)
+                    t.ppo_update(*data)
+            finally:
+                rd.all_reduce_sum = saved
+            torch.cuda.synchronize()
+            res.append((t._flat.flat_param.cpu().numpy().copy(), t._flat.exp_avg.cpu().numpy().copy(),
+                        float(t._flat.step_t)))
+            c = t.config
+        ver = ".".join(str(v) for v in torch.cuda.nccl.version())
+        q.put((res, calls, c["update_epochs"], c["num_minibatches"], ver))
+    finally:
+        td.destroy_process_group()
+
+
+def test_rccl_world1_shard_update_equals_fused():
+    """RCCL executed: init_process_group("nccl") at world size 1,
+    the data-parallel launch sequence (adv moments -> RCCL all-reduce -> finalize;
+    per optimizer step rx_ppo_minibatch_grad_shard -> RCCL all-reduce of
+    FlatAdam.bucket -> rx_ppo_kl_check -> rx_adam_clip_step) over two updates ==
+    the single-rank fused update bit for bit.  The stream ordering between the
+    librx launches on torch's current stream and RCCL's collective is what the
+    8-GPU run relies on."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    pr.start()
+    res, calls, E, n_mb, ver = q.get(timeout=600)
+    pr.join(timeout=120)
+    assert pr.exitcode == 0
+    (pa, ma, sa), (pb, mb_, sb) = res
+    assert calls["dev"] and calls["n"] == 2 * E * (n_mb + 1)  # per update: E moment + E * n_mb bucket all-reduces
+    assert sa == sb == 2 * E * n_mb
+    assert np.array_equal(pa, pb) and np.array_equal(ma, mb_)
+    print(f"\nRCCL {ver}: {calls['n']} all-reduces, {calls['bytes']} B, shard update == fused bit for bit")

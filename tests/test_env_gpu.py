@@ -319,6 +319,50 @@ def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
         assert torch.equal(ob, oc) and torch.equal(rb, rc) and torch.equal(db, dc), t
 
 
+def test_resort_histogram_survives_split_phase_sequences(rx, golden):
+    """The split step's REWARD half counts the re-sort bins as it writes the keys
+    (rx_api.cpp sort_hist_done).  Keys requested again before their sort ran --
+    rx_step_phases(1) twice with sort_interval = 1, or rx_step_phases(1) then a
+    reset -- must not leave a stale or doubled histogram (k_sort_scatter would
+    write past N).  Against an unsorted env on the same phase sequence: obs,
+    rewards, dones and the state bit-identical, and the wave order a permutation."""
+    N = 8256
+    tracks = np.arange(N) % golden.n_tracks
+    va = _venv(rx, golden, tracks, seed=2, autoreset="next_step", sort_interval=0)
+    vb = _venv(rx, golden, tracks, seed=2, autoreset="next_step", sort_interval=1)
+    assert vb.schedule()["split"] == 1
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(23)
+
+    def act():
+        a = torch.rand((N, 2), device="cuda", generator=g) * 2 - 1
+        a[:, 1].abs_()
+        return a
+
+    for t in range(40):
+        a1, a2 = act(), act()
+        if t % 2 == 0:  # dynamics twice (keys re-requested before the sort), then the raycast (sort)
+            for v in (va, vb):
+                v.step_device(a1, phases=1)
+                v.step_device(a2, phases=1)
+            oa, ra, da = va.step_device(a2, phases=2)
+            ob, rb, db = vb.step_device(a2, phases=2)
+        else:  # dynamics (keys + fused count), then a reset of every env (keys rewritten, not counted)
+            for v in (va, vb):
+                v.step_device(a1, phases=1)
+                v.reset_device()
+            oa, ra, da = va.step_device(a2)
+            ob, rb, db = vb.step_device(a2)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        perm = vb.env_order()[0]
+        assert np.array_equal(np.sort(perm), np.arange(N)), t
+    sa, sb = va.get_state(), vb.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    va.close()
+    vb.close()
+
+
 @pytest.mark.parametrize("n_agents,N", [(1, 1536), (1, 8256), (2, 512)])
 def test_segment_prefilter_is_exact(rx, golden, n_agents, N):
     """The float32 segment pre-filter (seg_may_hit) only skips exact segment
@@ -366,6 +410,45 @@ def test_lanes_per_ray_are_exact(rx, golden, n_agents, N, lpr):
         oa, ra, da = va.step_device(a)
         ob, rb, db = vb.step_device(a)
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    va.close()
+    vb.close()
+
+
+@pytest.mark.parametrize("tail,tail_lpr,dispatch", [(3, 2, 0), (11, 4, 0), (5, 2, 1), (2, 4, 2)])
+@pytest.mark.parametrize("n_agents,N", [(1, 8256), (2, 3000)])
+def test_ray_tail_split_is_exact(rx, golden, n_agents, N, tail, tail_lpr, dispatch):
+    """rx_config.ray_tail (ABI v19): the last `tail` ray-wave classes of the
+    dispatch order cast at 2 or 4 lanes per ray (each 64-task wave split into
+    2 or 4 waves, placed at the end of the table on the group's XCD) against the
+    plain one-lane-per-ray table: obs, rewards and dones bit-identical over 300
+    steps of random play, on the split step (k_step2) and for two cars; the
+    dispatch orders (edges-first auto, centre-first, ascending) likewise."""
+    tracks = np.arange(N) % golden.n_tracks
+    base = dict(ray_lpr=1, ray_tail=-1)
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step", sched=base)
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=4, autoreset="next_step",
+               sched=dict(ray_lpr=1, ray_tail=tail, ray_tail_lpr=tail_lpr, ray_dispatch=dispatch))
+    sb = vb.schedule()
+    assert sb["ray_tail"] == tail and sb["ray_tail_lpr"] == tail_lpr and sb["ray_tail_from"] > 0
+    tab = vb.ray_wave_table()
+    assert (tab["count"][sb["ray_tail_from"]:] <= 64 // tail_lpr).all()
+    assert tab["count"].sum() == N * n_agents * 11  # every task in exactly one wave
+    tasks = np.concatenate([np.arange(s, s + c) for s, c in zip(tab["task_start"], tab["count"]) if c > 0])
+    assert np.array_equal(np.sort(tasks), np.arange(N * n_agents * 11))
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(15)
+    shape = (N, 2) if n_agents == 1 else (N, 2, 2)
+    for t in range(300):
+        a = torch.rand(shape, device="cuda", generator=g) * 2 - 1
+        if n_agents == 1:
+            a[:, 1].abs_()
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    # the raycast on its own (k_rays, rx_step_phases) reads the same table
+    oa = va.step_device(torch.zeros(shape, device="cuda"), phases=2)[0]
+    ob = vb.step_device(torch.zeros(shape, device="cuda"), phases=2)[0]
+    assert torch.equal(oa, ob)
     va.close()
     vb.close()
 

@@ -155,6 +155,44 @@ def test_policy_act_matches_torch(D, n):
     torch.testing.assert_close(val, v_ref.flatten(), rtol=1e-5, atol=1e-5)
 
 
+def test_policy_act_near_zero_preactivations():
+    """tanh_fast near 0 (rx_policy.h): with every weight scaled down the hidden
+    pre-activations are ~1e-5, where 1 - 2/(exp(2|x|) + 1) alone would cancel to a
+    relative error of ~6e-3; the small-|x| select keeps the policy within float
+    rounding RELATIVE to its tiny outputs.  log_std = -20 makes the action ~ mu.
+    Tolerance: 2e-5 relative to each output's scale (float rounding of a 64-term sum;
+    without the select the error is ~6e-3 of it)."""
+    from rx.agent import Agent
+    from rx.optim import FlatAdam
+    from rx.ppo_fused import PolicyAct
+    from rx.spaces import Box
+    torch.manual_seed(4)
+    D, n = 15, 512
+    ag = Agent(Box(-1, 1, (D,)), Box(-1, 1, (2,))).cuda()
+    ag.log_std.fill_(-20.0)
+    with torch.no_grad():
+        for seq in (ag.actor_mu, ag.critic):
+            seq[0].weight.mul_(1e-5)
+        ag.actor_mu[4].weight.mul_(100.0)  # mu ~ 1e-5 rather than 1e-7
+    ref = copy.deepcopy(ag)
+    fl = FlatAdam(ag, torch.optim.Adam(ag.parameters(), lr=1e-3, eps=1e-5), 0.5)
+    pa = PolicyAct(ag, fl, n, D)
+    obs = torch.rand(n, D, device="cuda") * 2 - 1
+    act = torch.empty(n, 2, device="cuda")
+    lp = torch.empty(n, device="cuda")
+    val = torch.empty(n, device="cuda")
+    torch.manual_seed(78)
+    pa(obs, act, lp, val)
+    torch.manual_seed(78)
+    with torch.no_grad():
+        a_ref, _, _, v_ref = ref.get_action_and_value(obs)
+    v_ref = v_ref.flatten()
+    assert 1e-7 < float(v_ref.abs().median()) < 1e-3 and 1e-7 < float(a_ref.abs().median()) < 1e-3
+    # relative to the outputs' own scale (a row whose sum cancels has no relative bound)
+    torch.testing.assert_close(val, v_ref, rtol=2e-5, atol=2e-5 * float(v_ref.abs().max()))
+    torch.testing.assert_close(act, a_ref, rtol=2e-5, atol=2e-5 * float(a_ref.abs().max()))
+
+
 def test_fused_policy_rollout_runs_and_differs_only_by_rounding():
     """A fused-policy rollout step == the torch-policy step on the same state and noise
     (first step only: later steps may diverge chaotically through crash thresholds)."""

@@ -33,6 +33,9 @@ PASSES = [
      "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
     ["TCC_HIT_sum", "TCC_MISS_sum", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_WAVES",
      "SQ_BUSY_CYCLES", "SQ_INST_LEVEL_VMEM", "GRBM_GUI_ACTIVE"],
+    # executed floating-point work (bench.py compute_roofline): wave-level VALU instructions by kind, 8 SQ
+    ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
+     "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32"],
 ]
 KERNELS = ("k_step2", "k_kin1", "k_kin2", "k_rays", "k_dyn1", "k_dyn2", "k_gae", "k_sort_hist", "k_sort_scan",
            "k_sort_scatter", "k_state_copy", "k_state_sync", "k_ppo_grad", "k_policy_act")
@@ -98,7 +101,7 @@ def main():
     ap.add_argument("--passes", default=None, help="counter passes 'C1,C2;C3,...' instead of the default four")
     ap.add_argument("--bench-args", default="--steps 24 --burn-in 100 --warmup 0 --profile-steps 16 "
                                             "--no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 "
-                                            "--no-time-to-90")
+                                            "--no-time-to-90 --selfplay-updates 0 --counter-steps 0")
     args = ap.parse_args()
     cmd = [sys.executable, "bench.py", "--envs-per-gpu", str(args.envs)] + args.bench_args.split()
     if args.cmd:
@@ -106,7 +109,7 @@ def main():
     passes = [p.split(",") for p in args.passes.split(";")] if args.passes else PASSES
     acc = defaultdict(dict)
     for i, counters in enumerate(passes):
-        d = run_pass(args.scratch, i, counters, cmd, args.timeout, required=args.passes is not None or i < 3)
+        d = run_pass(args.scratch, i, counters, cmd, args.timeout, required=args.passes is not None or i in (0, 1, 2, 4))
         if d is None:
             continue
         for (k, g), cs in collect(d).items():

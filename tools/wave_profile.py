@@ -1,6 +1,6 @@
 """How k_step2's waves fill the chip over one production launch (diagnostic).
 
-    python tools/wave_profile.py [n_envs] [steps]      (GPU box)
+    python tools/wave_profile.py [n_envs] [steps] [sched k=v,...]      (GPU box)
 
 The bench workload (seed-1 pool, uniform random actions, next-step autoreset)
 after a 150-step burn-in; `steps` production steps are recorded with
@@ -23,7 +23,13 @@ sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
 sys.path.insert(0, ROOT)
 
 
-def summarize(st, en, n_rw, maxw, slots=8192):
+def summarize(st, en, n_rw, cls=None, sub=None, slots=8192):
+    """One recorded k_step2 launch.  st / en: per-wave start / end (us from the
+    first start, NaN = no wave) in workgroup order, REWARD waves [0, n_rw) first;
+    cls / sub: per RAY wave (dispatch order) its class and tail sub-wave from the
+    library's own table (RacingVectorEnv.ray_wave_table: exact for every
+    dispatch mode and tail split).  wave_slot_utilisation = the launch's summed
+    wave time over slots x span (8 waves on each of 1,024 SIMDs)."""
     live = ~np.isnan(st)
     span = float(np.nanmax(en[live]))
     dur = en - st
@@ -45,18 +51,45 @@ def summarize(st, en, n_rw, maxw, slots=8192):
         "first_wave_end_us": round(float(np.nanmin(en[live])), 2),
         "active_waves_by_us": act.tolist(),
         "tail_after_half_slots_us": round(span - half_t, 2),
-        "wave_us_sum_over_slots_span": round(float(np.nansum(dur[live])) / (slots * span), 3),
+        "wave_slot_utilisation": round(float(np.nansum(dur[live])) / (slots * span), 3),
         "ray_dur_us_by_dispatch_decile": [round(float(np.mean(dur[d])), 2) for d in dec if len(d)],
         "ray_start_us_by_dispatch_decile": [round(float(np.mean(st[d])), 2) for d in dec if len(d)],
     }
-    # ray wave p (dispatch order) -> class j (the j-th 64 direction-sorted tasks of its
-    # 64-env group) under rx_assign's placement: group-octet-major, class, group % 8
-    # (ray_order 2, RX_RAY_DISPATCH 0); reported for the default placement only
-    pr = ray_idx - n_rw
-    cls = (pr // 8) % maxw
-    res["ray_dur_us_by_class"] = [round(float(np.nanmean(dur[ray_idx[cls == j]])), 2) for j in range(maxw)]
-    res["ray_start_us_by_class"] = [round(float(np.nanmean(st[ray_idx[cls == j]])), 2) for j in range(maxw)]
+    if cls is not None:
+        c = np.full(len(st), -1, np.int64)
+        m = min(len(cls), len(st) - n_rw)
+        c[n_rw:n_rw + m] = cls[:m]
+        classes = sorted(int(j) for j in np.unique(c[ray]) if j >= 0)
+        res["ray_dur_us_by_class"] = {j: round(float(np.nanmean(dur[ray & (c == j)])), 2) for j in classes}
+        res["ray_start_us_by_class"] = {j: round(float(np.nanmean(st[ray & (c == j)])), 2) for j in classes}
+        res["ray_end_us_by_class_max"] = {j: round(float(np.nanmax(en[ray & (c == j)])), 2) for j in classes}
     return res
+
+
+def record(env, act, steps):
+    """Record `steps` production steps of `env` and summarise every k_step2 launch."""
+    sched = env.schedule()
+    n_rw = sched["reward_lpe"] * ((sched["dyn_waves"] + 7) // 8 * 8)  # k_step2: REWARD workgroups first
+    tab = env.ray_wave_table()
+    torch.cuda.synchronize()
+    env.profile(1)
+    for _ in range(steps):
+        env.step_device(act())
+    env.profile(0)
+    torch.cuda.synchronize()
+    out = []
+    k = 0
+    while True:
+        try:
+            st, en, kind, n = env.profile_waves(k)
+        except Exception:  # noqa: BLE001 -- past the record
+            break
+        if kind == "k_step2":
+            s = summarize(st, en, n_rw, tab["cls"], tab["sub"])
+            s["launch"] = k
+            out.append((s, st, en))
+        k += 1
+    return sched, out
 
 
 def main():
@@ -64,8 +97,9 @@ def main():
     from rx.vector_env import RacingVectorEnv
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    sched = {k: int(v) for k, v in (kv.split("=") for kv in (sys.argv[3] if len(sys.argv) > 3 else "").split(",") if kv)}
     pool, widths = seed1_pool(N)
-    env = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step")
+    env = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=sched)
     env.reset_device()
     g = torch.Generator(device="cuda").manual_seed(0)
     scale = torch.tensor([2.0, 1.0], device="cuda")
@@ -75,30 +109,13 @@ def main():
         return torch.addcmul(shift, torch.rand((N, 2), generator=g, device="cuda"), scale)
     for _ in range(150):
         env.step_device(act())
-    sched = env.schedule()
-    n_rw = sched["reward_lpe"] * ((sched["dyn_waves"] + 7) // 8 * 8)  # k_step2: REWARD workgroups first
-    torch.cuda.synchronize()
-    env.profile(1)
-    for _ in range(steps):
-        env.step_device(act())
-    env.profile(0)
-    torch.cuda.synchronize()
+    sched, launches = record(env, act, steps)
     out = {"n_envs": N, "schedule": sched, "launches": []}
-    k = 0
-    while True:
-        try:
-            st, en, kind, n = env.profile_waves(k)
-        except Exception:  # noqa: BLE001 -- past the record
-            break
-        if kind == "k_step2":
-            maxw = -(-64 * sched["ray_lpr"] * 11 // 64)  # ray waves per 64-env group (11 sensors)
-            s = summarize(st, en, n_rw, maxw)
-            if not out["launches"]:
-                s["raw_start_us"] = np.round(st, 2).tolist()
-                s["raw_end_us"] = np.round(en, 2).tolist()
-            s["launch"] = k
-            out["launches"].append(s)
-        k += 1
+    for i, (s, st, en) in enumerate(launches):
+        if i == 0:
+            s["raw_start_us"] = np.round(st, 2).tolist()
+            s["raw_end_us"] = np.round(en, 2).tolist()
+        out["launches"].append(s)
     print(json.dumps(out), flush=True)
 
 
