@@ -2,9 +2,15 @@
 keys (actor_mu.{0,2,4}, critic.{0,2,4}, log_std buffer), so checkpoints move
 between the reference and this engine unchanged (SURVEY.md §5 checkpoint row).
 
-The MLP is ~10.5k parameters: its GEMMs are far too small for hand-written
-MFMA tiles to matter, so it stays on PyTorch-ROCm (rocBLAS/hipBLASLt), as the
-north star prescribes; the env step and GAE are the hand-written kernels.
+This module is the parameter container and the torch reference forward.  On
+the default device path the MLP does NOT run on rocBLAS: the rollout's
+forward + sampling is the hand-written MFMA kernel k_policy_act
+(rx.ppo_fused.PolicyAct, rx_ppo.hip) and the PPO minibatch forward / loss /
+backward is k_ppo_grad (v_mfma_f32_16x16x4_f32, or the bf16 MFMA with
+config["policy_dtype"] = "bf16"), both over the flat parameter buffer that
+backs these modules' tensors (rx.optim.FlatAdam).  The torch forward here
+(get_action_and_value) is what config["fused_policy"] / ["fused_update"] =
+False fall back to, and what the parity tests compare the kernels against.
 """
 import numpy as np
 import torch
