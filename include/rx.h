@@ -485,6 +485,18 @@ typedef struct rx_rollout_io {
 int rx_rollout_supported(const rx_env* h);
 int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream);
 
+/* ABI v19: the same T-step rollout for ANY single-agent handle as a sequence of
+ * launches enqueued by ONE call: per step t, rx_policy_act on obs[t] with
+ * eps[t] (actions[t], logprobs[t], values[t]) at matrix-core `precision`, then
+ * rx_step of actions[t] writing obs[t+1] (next_obs at t = T-1), rewards[t] and
+ * dones[t+1] (next_done).  Every kernel and every output equals the per-step
+ * Python loop (rx_policy_act + rx_step per step) with the same eps bit for bit;
+ * what it removes is T x (tensor slicing + two ctypes calls + a noise launch)
+ * of host time per rollout -- the eager rollout of a few thousand envs was
+ * host-bound.  `io` as for rx_rollout.  Replaces the step loop of
+ * PPO.collect_rollout, agent/ppo.py:97-132. */
+int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t precision, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1006,6 +1006,32 @@ int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream)
   return RX_OK;
 }
 
+int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t precision, void* stream) {
+  if (!h || !io || !r) return fail(RX_EINVAL, "rx_rollout_steps: null argument");
+  if (!h->assigned || !h->bound) return fail(RX_ESTATE, "rx_rollout_steps: needs an assigned, bound handle");
+  if (h->cfg.n_agents != 1) return fail(RX_EINVAL, "rx_rollout_steps: single-agent handles only");
+  if (r->T <= 0) return fail(RX_EINVAL, "rx_rollout_steps: T=%d must be > 0", r->T);
+  if (r->obs_dim != h->D) return fail(RX_EINVAL, "rx_rollout_steps: obs_dim %d != the handle's %d", r->obs_dim, h->D);
+  if (!r->params || !r->log_std || !r->eps || !r->obs || !r->actions || !r->logprobs || !r->values || !r->rewards ||
+      !r->dones || !r->next_obs || !r->next_done)
+    return fail(RX_EINVAL, "rx_rollout_steps: null rollout buffer");
+  const int64_t N = h->cfg.n_envs, D = h->D;
+  for (int32_t t = 0; t < r->T; ++t) {
+    const bool last = t + 1 == r->T;
+    const rx_policy_io pio{r->obs_dim, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
+                           r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision};
+    int rc = rx_policy_act(&pio, stream);
+    if (rc) return rc;
+    rx_io s = *io;
+    s.actions = r->actions + t * N * 2;
+    s.obs = last ? r->next_obs : r->obs + (t + 1) * N * D;
+    s.reward = r->rewards + t * N;
+    s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;
+    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
+  }
+  return RX_OK;
+}
+
 static int gae(int32_t T, int32_t N, const float* r, const float* v, const float* d, const float* nv, const float* nd,
                double gamma, double lam, float* adv, float* ret, int scan, void* stream) {
   if (T <= 0 || N <= 0) return fail(RX_EINVAL, "rx_gae: T=%d N=%d must be > 0", T, N);

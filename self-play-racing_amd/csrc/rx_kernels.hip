@@ -416,7 +416,7 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
 constexpr int kTaskSectors = 64;
 template <int A>
 __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
-                                                 int32_t* cnt) {
+                                                 int32_t* cnt, int32_t* stage) {
   constexpr int kMaxT = 16 * A;  // rx_assign enforces n_sensors <= 16 for ray_order 2
   const int R = a.n_sensors, AR = A * R;
   const int lane = threadIdx.x & 63;
@@ -444,14 +444,20 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
     if (lane >= o) c += v;
   }
   cnt[lane] = c - c0;  // exclusive offset of sector `lane`
+  const int total = __shfl(c, 63, 64);  // the block's tasks (AR per env lane)
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  // scatter the task ids into the wave's LDS staging row, then store the row
+  // coalesced (each of them was a scattered 4-byte global store: 704 per wave)
   if (p >= 0) {
-    int32_t* out = a.tasks_out + (size_t)perm_start * AR;
 #pragma unroll
     for (int t = 0; t < kMaxT; ++t)
-      if (t < AR) out[cnt[pk[t] & 63] + (pk[t] >> 6)] = A * p * R + t;  // task id (A*p + q)*R + r
+      if (t < AR) stage[cnt[pk[t] & 63] + (pk[t] >> 6)] = A * p * R + t;  // task id (A*p + q)*R + r
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int32_t* out = a.tasks_out + (size_t)perm_start * AR;
+  for (int i = lane; i < total; i += 64) out[i] = stage[i];
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -854,8 +860,13 @@ template <int LPE, int PART>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
-  __shared__ int32_t tcnt[4][kTaskSectors];
-  int32_t* cnt = tcnt[threadIdx.x >> 6];
+  // ray-task sort: per wave 64 sector counters and a staging row of its <= 64 x 16 task ids
+  // (k_kin1 runs one wave per workgroup, k_dyn1 four)
+  constexpr int NW = PART == RX_PART_KIN ? 1 : 4;
+  __shared__ int32_t tcnt[NW][kTaskSectors];
+  __shared__ int32_t tstage[NW][64 * 16];
+  const int wl = NW == 1 ? 0 : (int)(threadIdx.x >> 6);
+  int32_t* cnt = tcnt[wl];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
   const unsigned long long prof_t0 = prof_start(a);
@@ -863,7 +874,7 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   int e = -1;  // set on the lane that finishes an env (sub 0)
   dyn1_env<LPE, PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
-  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
+  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, tstage[wl]);
   prof_end(a, wave, prof_t0);
 #ifdef RX_DYN_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
@@ -1311,8 +1322,11 @@ template <int PART>
 __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
-  __shared__ int32_t tcnt[4][kTaskSectors];
-  int32_t* cnt = tcnt[threadIdx.x >> 6];
+  constexpr int NW = PART == RX_PART_KIN ? 1 : 4;  // k_kin2: one wave per workgroup
+  __shared__ int32_t tcnt[NW][kTaskSectors];
+  __shared__ int32_t tstage[NW][64 * 32];
+  const int wl = NW == 1 ? 0 : (int)(threadIdx.x >> 6);
+  int32_t* cnt = tcnt[wl];
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
   const unsigned long long prof_t0 = prof_start(a);
@@ -1320,7 +1334,7 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   int e = -1;
   dyn2_env<PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
-  if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt);
+  if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, tstage[wl]);
   prof_end(a, wave, prof_t0);
 }
 

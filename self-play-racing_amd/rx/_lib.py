@@ -31,7 +31,8 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
-           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves")
+           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves",
+           "rx_rollout_steps")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -150,6 +151,7 @@ def load(build_if_missing=True):
     L.rx_policy_act.argtypes = [ctypes.POINTER(RxPolicyIO), _P]
     L.rx_rollout_supported.argtypes = [_P]
     L.rx_rollout.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO), _P]
+    L.rx_rollout_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO), ctypes.c_int32, _P]
     L.rx_ppo_adv_moments.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P]
     L.rx_ppo_adv_finalize.argtypes = [_P, ctypes.c_int32, ctypes.c_int64, _P, _P]
     L.rx_ppo_minibatch_grad_shard.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, ctypes.c_float, _P, _P, _P,

@@ -160,6 +160,19 @@ class PPO:
             pa = self._policy_act = ppo_fused.PolicyAct(self.agent, self._flat, obs.shape[1], obs.shape[2], prec)
         return pa
 
+    def _step_rollout(self, obs):
+        """rx_rollout_steps driver (config["rollout_steps"], default "auto" = on)
+        for a single-agent handle on the fused policy path, else None."""
+        from . import ppo_fused
+        c = self.config
+        if (self._fused_policy(obs) is None or not ppo_fused.StepRollout.supported(self.envs, self.agent, c)):
+            return None
+        T, prec = obs.shape[0], ppo_fused.precision(c)
+        sr = self.__dict__.get("_steps_rollout")
+        if sr is None or sr.T != T or sr.n != self.envs.num_envs or sr.prec != prec:
+            sr = self._steps_rollout = ppo_fused.StepRollout(self.agent, self._flat, self.envs, T, prec)
+        return sr
+
     def _rollout_body(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done):
         T = obs.shape[0]
         obs[0].copy_(next_obs)
@@ -167,6 +180,10 @@ class PPO:
         ro = self._fused_rollout(T)
         if ro is not None:  # few envs: the whole rollout is one persistent launch
             ro(obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
+            return
+        sr = self._step_rollout(obs)
+        if sr is not None:  # T x (rx_policy_act + rx_step) enqueued by one library call
+            sr(obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
             return
         fused = self._fused_policy(obs)
         for step in range(T):

@@ -267,6 +267,59 @@ class Rollout:
         self.venv._launched(stream)
 
 
+class StepRollout:
+    """rx_rollout_steps driver: the T-step rollout of any single-agent handle as
+    ONE library call that enqueues T x (rx_policy_act + rx_step) -- the kernels
+    of the per-step loop, in its order, with pointer arithmetic in C instead of
+    T x (tensor slicing + two ctypes calls) of host time.  The N(0, 1) noise of
+    all T steps is drawn up front with ONE torch normal_() on [T, N, 2] (the
+    same distribution; with T = 1 the same sample as a per-step draw); given
+    the same noise every output equals the per-step loop bit for bit
+    (tests/test_rollout_gpu.py)."""
+
+    def __init__(self, agent, flat, venv, T, prec=_lib.RX_PREC_FP32):
+        self.L = _lib.load()
+        self.agent, self.flat, self.venv, self.T, self.prec = agent, flat, venv, int(T), int(prec)
+        self.n, self.obs_dim = venv.num_envs, venv.D
+        self.eps = torch.empty((self.T, self.n, 2), dtype=torch.float32, device=flat.flat_param.device)
+        self._cache = {}
+
+    @staticmethod
+    def supported(venv, agent, config):
+        if not hasattr(venv, "_h") or venv.n_agents != 1 or not policy_supported(agent, venv.D):
+            return False
+        mode = config.get("rollout_steps", "auto")
+        return not (mode is False or mode == "off")
+
+    def __call__(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done, eps=None, stream=None):
+        T, n, D = self.T, self.n, self.obs_dim
+        shapes = {"obs": (obs, (T, n, D)), "actions": (actions, (T, n, 2)), "logprobs": (logprobs, (T, n)),
+                  "values": (values, (T, n)), "rewards": (rewards, (T, n)), "dones": (dones, (T, n)),
+                  "next_obs": (next_obs, (n, D)), "next_done": (next_done, (n,))}
+        e = self.eps if eps is None else eps
+        key = tuple(t.data_ptr() for t in (obs, actions, logprobs, dones, rewards, values, next_obs, next_done, e))
+        r = self._cache.get(key)
+        if r is None:
+            for k, (t, shp) in shapes.items():
+                if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous():
+                    raise ValueError(f"rx_rollout_steps: {k} must be a contiguous float32 {shp}, got "
+                                     f"{tuple(t.shape)} {t.dtype}")
+            if tuple(e.shape) != (T, n, 2) or e.dtype != torch.float32 or not e.is_contiguous():
+                raise ValueError("rx_rollout_steps: eps must be a contiguous float32 [T, N, 2]")
+            if len(self._cache) > 64:
+                self._cache.clear()
+            r = self._cache[key] = _lib.RxRolloutIO(
+                T, D, _lib.ptr(self.flat.flat_param), _lib.ptr(self.agent.log_std), _lib.ptr(e), _lib.ptr(obs),
+                _lib.ptr(actions), _lib.ptr(logprobs), _lib.ptr(values), _lib.ptr(rewards), _lib.ptr(dones),
+                _lib.ptr(next_obs), _lib.ptr(next_done))
+        if eps is None:
+            self.eps.normal_()
+        io = self.venv._io()
+        _lib.check(self.L.rx_rollout_steps(self.venv._h, io, r, self.prec, _lib.stream_ptr(stream)),
+                   "rx_rollout_steps")
+        self.venv._launched(stream)
+
+
 # config["fused_rollout"] = "auto": the persistent rollout up to this many envs
 # (one workgroup per env runs all T steps; beyond what the chip holds at once
 # the workgroups would run in waves, each paying T steps of latency)

@@ -171,3 +171,69 @@ def test_configs0_one_env_ppo_iteration():
     for k in sa:
         np.testing.assert_allclose(sa[k].cpu().numpy(), sb[k].cpu().numpy(), rtol=1e-4, atol=0.02 * lr * n,
                                    err_msg=k)
+
+
+@pytest.mark.parametrize("n,T,prec", [(4096, 64, "fp32"), (3000, 40, "bf16"), (64, 30, "fp32")])
+def test_rollout_steps_equals_per_step_path(n, T, prec):
+    """rx_rollout_steps (ABI v19: T x (rx_policy_act + rx_step) enqueued by ONE
+    call, the default eager rollout of every single-agent handle the persistent
+    kernel does not take) == the Python per-step loop bit for bit with the same
+    noise -- configs[1]'s 4,096 envs (split step, 4 lanes per ray), a ragged
+    3,000 in bf16, and 64 envs on the small-N kernels -- over two chained
+    rollouts: every buffer, the env state and the episode statistics."""
+    ta, c = _train_single_style(num_envs=n, num_steps=T, policy_dtype=prec, fused_rollout=False)
+    tb, _ = _train_single_style(num_envs=n, num_steps=T, policy_dtype=prec, fused_rollout=False)
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    bufs_a = ta._buffers()
+    sr = ta._step_rollout(bufs_a[0])
+    assert sr is not None and sr.prec == (1 if prec == "bf16" else 0)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    eps = torch.randn((T, n, 2), device="cuda", generator=g) * 1.5
+    outs = []
+    for tr, fused in ((ta, True), (tb, False)):
+        bufs = tr._buffers()
+        nobs = tr.envs.buf["obs"].clone()
+        nd = torch.zeros(n, device="cuda")
+        for _ in range(2):
+            obs, actions, logprobs, dones, rewards, values = bufs
+            obs[0].copy_(nobs)
+            dones[0].copy_(nd)
+            if fused:
+                sr(obs, actions, logprobs, dones, rewards, values, nobs, nd, eps=eps)
+            else:
+                pa = tr._fused_policy(obs)
+                for s in range(T):
+                    pa(obs[s], actions[s], logprobs[s], values[s], eps=eps[s])
+                    last = s + 1 == T
+                    tr.envs.step_device(actions[s], obs_out=nobs if last else obs[s + 1], reward_out=rewards[s],
+                                        done_out=nd if last else dones[s + 1])
+        torch.cuda.synchronize()
+        outs.append(([x.clone() for x in bufs] + [nobs.clone(), nd.clone()], tr.envs.get_state(),
+                     tr.envs.episode_stats()))
+    (ba, sa, ea), (bb, sb, eb) = outs
+    names = ("obs", "actions", "logprobs", "dones", "rewards", "values", "next_obs", "next_done")
+    for k, x, y in zip(names, ba, bb):
+        assert torch.equal(x, y), k
+    assert (ba[3] > 0).any() and (ba[1].abs() == 1.0).any()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    assert ea[1:] == eb[1:] and ea[0] == pytest.approx(eb[0], rel=1e-12)
+
+
+def test_collect_rollout_uses_rollout_steps_and_keeps_t1_stream():
+    """collect_rollout takes rx_rollout_steps for configs[1]-size handles; with
+    T = 1 its [1, N, 2] noise draw is the very sample a per-step [N, 2] draw
+    makes, so the step equals the per-step fused path run from the same seed."""
+    ta, _ = _train_single_style(num_envs=4096, num_steps=1)
+    tb, _ = _train_single_style(num_envs=4096, num_steps=1, rollout_steps=False)
+    tb.agent.load_state_dict(ta.agent.state_dict())
+    outs = []
+    for t in (ta, tb):
+        bufs = t._buffers()
+        nobs = t.envs.buf["obs"].clone()
+        nd = torch.zeros(4096, device="cuda")
+        torch.manual_seed(3)
+        outs.append(t.collect_rollout(*bufs, nobs, nd))
+    assert ta.__dict__.get("_steps_rollout") is not None and tb.__dict__.get("_steps_rollout") is None
+    for x, y in zip(outs[0][:8], outs[1][:8]):
+        assert torch.equal(x, y)
