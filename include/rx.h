@@ -453,6 +453,9 @@ typedef struct rx_policy_io {
   int64_t obs_stride;     /* e.g. 2*19 for one car's rows of a two-car [n][2][19] buffer */
   int64_t act_stride;     /* e.g. 4 for one car's actions in [n][2][2] */
   int32_t precision;      /* RX_PREC_FP32 (default) or RX_PREC_BF16 (ABI v14) */
+  float* actions2;        /* ABI v19: NULL, or a second copy of the actions (e.g. the agent's slot of a two-car
+                             env's [n][2][2] action buffer), rows act2_stride floats apart (0 = 2) */
+  int64_t act2_stride;
 } rx_policy_io;
 int rx_policy_act(const rx_policy_io* io, void* stream);
 
@@ -496,6 +499,30 @@ int rx_rollout(rx_env* h, const rx_io* io, const rx_rollout_io* r, void* stream)
  * host-bound.  `io` as for rx_rollout.  Replaces the step loop of
  * PPO.collect_rollout, agent/ppo.py:97-132. */
 int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t precision, void* stream);
+
+/* ABI v19: the self-play rollout (environment/wrappers.py:29-55 inside
+ * agent/self_play_ppo.py's collect_rollout) of a TWO-CAR handle the same way:
+ * per step t the frozen opponent's rx_policy_act on its rows of the env's obs
+ * buffer (opp_eps[t], actions into its slot of the env's action buffer), the
+ * agent's rx_policy_act on obs[t] (eps[t]; actions into actions[t] AND its slot
+ * of the env's action buffer), rx_step, then one copy of the agent's obs row and
+ * reward out of the env's [N][2] buffers into obs[t+1] / rewards[t].  Five
+ * launches per step from one call (the Python step ran nine: two noise draws,
+ * three copies).  Every output equals SelfPlayVectorEnv's per-step path with
+ * the same noise bit for bit.  `r` is the agent's rollout (obs_dim 19). */
+typedef struct rx_selfplay_io {
+  const float* opp_params;   /* the frozen opponent's flat parameters */
+  const float* opp_log_std;  /* [2] */
+  const float* opp_eps;      /* [T][N][2] N(0,1) noise of the opponent */
+  float* env_actions;        /* [N][2][2] the handle's action buffer */
+  float* env_obs;            /* [N][2][D] the handle's observation buffer (rx_io.obs) */
+  float* env_reward;         /* [N][2] the handle's reward buffer (rx_io.reward) */
+  float* sink;               /* [2N] float32 scratch: the opponent's log-probs / values */
+  int32_t agent;             /* the learning agent's car (0 or 1); the opponent is the other */
+  int32_t opp_precision;     /* RX_PREC_* of the opponent's forward */
+} rx_selfplay_io;
+int rx_selfplay_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, const rx_selfplay_io* sp,
+                              int32_t precision, void* stream);
 
 #ifdef __cplusplus
 }

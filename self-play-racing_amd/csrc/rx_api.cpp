@@ -1019,7 +1019,8 @@ int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t
   for (int32_t t = 0; t < r->T; ++t) {
     const bool last = t + 1 == r->T;
     const rx_policy_io pio{r->obs_dim, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
-                           r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision};
+                           r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
+                           nullptr, 0};
     int rc = rx_policy_act(&pio, stream);
     if (rc) return rc;
     rx_io s = *io;
@@ -1028,6 +1029,47 @@ int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t
     s.reward = r->rewards + t * N;
     s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;
     if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
+  }
+  return RX_OK;
+}
+
+int rx_selfplay_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, const rx_selfplay_io* sp,
+                              int32_t precision, void* stream) {
+  if (!h || !io || !r || !sp) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: null argument");
+  if (!h->assigned || !h->bound) return fail(RX_ESTATE, "rx_selfplay_rollout_steps: needs an assigned, bound handle");
+  if (h->cfg.n_agents != 2) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: two-car handles only");
+  if (r->T <= 0) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: T=%d must be > 0", r->T);
+  if (r->obs_dim != h->D) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: obs_dim %d != the handle's %d", r->obs_dim, h->D);
+  if (sp->agent != 0 && sp->agent != 1) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: agent must be 0 or 1");
+  if (!r->params || !r->log_std || !r->eps || !r->obs || !r->actions || !r->logprobs || !r->values || !r->rewards ||
+      !r->dones || !r->next_obs || !r->next_done || !sp->opp_params || !sp->opp_log_std || !sp->opp_eps ||
+      !sp->env_actions || !sp->env_obs || !sp->env_reward || !sp->sink)
+    return fail(RX_EINVAL, "rx_selfplay_rollout_steps: null buffer");
+  const int64_t N = h->cfg.n_envs, D = h->D;
+  const int q = sp->agent, o = 1 - q;
+  for (int32_t t = 0; t < r->T; ++t) {
+    const bool last = t + 1 == r->T;
+    // the frozen opponent on its rows of the env's observation buffer (wrappers.py:36-39)
+    const rx_policy_io opp{(int32_t)D, N, sp->env_obs + o * D, sp->opp_eps + t * N * 2, sp->opp_params,
+                           sp->opp_log_std, sp->env_actions + 2 * o, sp->sink, sp->sink + N, 2 * D, 4,
+                           sp->opp_precision, nullptr, 0};
+    int rc = rx_policy_act(&opp, stream);
+    if (rc) return rc;
+    // the learning agent on obs[t]: actions into the rollout row and the env's action slot
+    const rx_policy_io pio{(int32_t)D, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
+                           r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
+                           sp->env_actions + 2 * q, 4};
+    if ((rc = rx_policy_act(&pio, stream))) return rc;
+    rx_io s = *io;
+    s.actions = sp->env_actions;
+    s.obs = sp->env_obs;
+    s.reward = sp->env_reward;
+    s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;  // dones['__all__'] (wrappers.py:51)
+    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
+    if ((rc = rx_launch_agent_rows((int)N, (int)D, q, sp->env_obs, sp->env_reward,
+                                   last ? r->next_obs : r->obs + (t + 1) * N * D, r->rewards + t * N,
+                                   (hipStream_t)stream)) != 0)
+      return fail(RX_EHIP, "agent-row copy launch failed: %s", hipGetErrorString((hipError_t)rc));
   }
   return RX_OK;
 }
@@ -1229,7 +1271,8 @@ int rx_policy_act(const rx_policy_io* io, void* stream) {
   if (io->n <= 0) return fail(RX_EINVAL, "rx_policy_act: n=%lld", (long long)io->n);
   if (io->precision != RX_PREC_FP32 && io->precision != RX_PREC_BF16)
     return fail(RX_EINVAL, "rx_policy_act: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", io->precision);
-  if ((io->obs_stride != 0 && io->obs_stride < io->obs_dim) || (io->act_stride != 0 && io->act_stride < 2))
+  if ((io->obs_stride != 0 && io->obs_stride < io->obs_dim) || (io->act_stride != 0 && io->act_stride < 2) ||
+      (io->act2_stride != 0 && io->act2_stride < 2))
     return fail(RX_EINVAL, "rx_policy_act: row strides overlap (obs %lld, act %lld)", (long long)io->obs_stride,
                 (long long)io->act_stride);
   if (!io->obs || !io->eps || !io->params || !io->log_std || !io->actions || !io->logprobs || !io->values)

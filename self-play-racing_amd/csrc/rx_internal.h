@@ -158,6 +158,8 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024
 extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int max_w, hipStream_t s);
+extern "C" int rx_launch_agent_rows(int N, int D, int q, const float* obs, const float* rew, float* obs_out,
+                                    float* rew_out, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s);
 // Adam's per-step scalars for step count s (torch.optim.Adam, non-capturable):

@@ -2334,6 +2334,27 @@ extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int 
   return (int)hipGetLastError();
 }
 
+// Self-play rollout (rx_selfplay_rollout_steps): agent q's observation row and
+// reward out of a two-car handle's [N][2][D] / [N][2] step outputs into the
+// rollout's [N][D] / [N] rows.  Lane = one float.
+__global__ __launch_bounds__(256) void k_agent_rows(int N, int D, int q, const float* __restrict__ obs,
+                                                    const float* __restrict__ rew, float* __restrict__ obs_out,
+                                                    float* __restrict__ rew_out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < N * D) {
+    const int e = i / D, d = i - e * D;
+    obs_out[i] = obs[(size_t)(2 * e + q) * D + d];
+  }
+  if (i < N) rew_out[i] = rew[2 * i + q];
+}
+
+extern "C" int rx_launch_agent_rows(int N, int D, int q, const float* obs, const float* rew, float* obs_out,
+                                    float* rew_out, hipStream_t s) {
+  const int n = N * D > N ? N * D : N;
+  hipLaunchKernelGGL(k_agent_rows, dim3((n + 255) / 256), dim3(256), 0, s, N, D, q, obs, rew, obs_out, rew_out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,
                              const float* nd, float g, float gl, float* adv, float* ret, int scan, hipStream_t s) {
   if (scan) {

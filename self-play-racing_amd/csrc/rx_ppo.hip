@@ -294,6 +294,7 @@ __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float*
       const float smp = io.eps[row * kNA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
       const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
       io.actions[row * as + j] = a;
+      if (io.actions2) io.actions2[row * (io.act2_stride > 0 ? io.act2_stride : kNA) + j] = a;
       logp += normal_logp(a - mu, var, logf(scale));
     }
     io.logprobs[row] = logp;

@@ -32,7 +32,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
            "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves",
-           "rx_rollout_steps")
+           "rx_rollout_steps", "rx_selfplay_rollout_steps")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -98,7 +98,13 @@ class RxRolloutIO(ctypes.Structure):
 class RxPolicyIO(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("n", ctypes.c_int64)] + \
                [(k, _P) for k in ("obs", "eps", "params", "log_std", "actions", "logprobs", "values")] + \
-               [("obs_stride", ctypes.c_int64), ("act_stride", ctypes.c_int64), ("precision", ctypes.c_int32)]
+               [("obs_stride", ctypes.c_int64), ("act_stride", ctypes.c_int64), ("precision", ctypes.c_int32),
+                ("actions2", _P), ("act2_stride", ctypes.c_int64)]
+
+
+class RxSelfplayIO(ctypes.Structure):
+    _fields_ = [(k, _P) for k in ("opp_params", "opp_log_std", "opp_eps", "env_actions", "env_obs", "env_reward",
+                                  "sink")] + [("agent", ctypes.c_int32), ("opp_precision", ctypes.c_int32)]
 
 
 class RxError(RuntimeError):
@@ -152,6 +158,8 @@ def load(build_if_missing=True):
     L.rx_rollout_supported.argtypes = [_P]
     L.rx_rollout.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO), _P]
     L.rx_rollout_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO), ctypes.c_int32, _P]
+    L.rx_selfplay_rollout_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.POINTER(RxRolloutIO),
+                                            ctypes.POINTER(RxSelfplayIO), ctypes.c_int32, _P]
     L.rx_ppo_adv_moments.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, _P, _P]
     L.rx_ppo_adv_finalize.argtypes = [_P, ctypes.c_int32, ctypes.c_int64, _P, _P]
     L.rx_ppo_minibatch_grad_shard.argtypes = [ctypes.POINTER(RxPPOBatch), ctypes.c_int32, ctypes.c_float, _P, _P, _P,

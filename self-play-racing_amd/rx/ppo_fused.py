@@ -320,6 +320,72 @@ class StepRollout:
         self.venv._launched(stream)
 
 
+class SelfPlayStepRollout:
+    """rx_selfplay_rollout_steps driver: the self-play rollout of a two-car handle
+    (rx.selfplay.SelfPlayVectorEnv with a frozen-policy opponent on
+    rx_policy_act) as ONE library call enqueueing per step the opponent's and the
+    agent's rx_policy_act, rx_step and one agent-row copy -- five launches where
+    the per-step Python path ran nine (two noise draws, three copies).  Noise of
+    both policies is drawn up front ([T, N, 2] each); given the same noise every
+    output equals the per-step path bit for bit (tests/test_selfplay_train_gpu.py)."""
+
+    def __init__(self, agent, flat, spenv, T, prec=_lib.RX_PREC_FP32):
+        self.L = _lib.load()
+        self.agent, self.flat, self.spenv, self.T, self.prec = agent, flat, spenv, int(T), int(prec)
+        self.venv = spenv.venv
+        self.n, self.obs_dim = self.venv.num_envs, self.venv.D
+        dev = flat.flat_param.device
+        self.eps = torch.empty((self.T, self.n, 2), dtype=torch.float32, device=dev)
+        self.opp_eps = torch.empty((self.T, self.n, 2), dtype=torch.float32, device=dev)
+        self.sink = torch.empty(2 * self.n, dtype=torch.float32, device=dev)
+        self._cache = {}
+
+    @staticmethod
+    def supported(spenv, agent, config):
+        mode = config.get("rollout_steps", "auto")
+        if mode is False or mode == "off":
+            return False
+        v = getattr(spenv, "venv", None)
+        return (v is not None and hasattr(v, "_h") and v.n_agents == 2 and spenv._opp_fused is not None
+                and policy_supported(agent, v.D))
+
+    def __call__(self, obs, actions, logprobs, dones, rewards, values, next_obs, next_done, eps=None, opp_eps=None,
+                 stream=None):
+        T, n, D = self.T, self.n, self.obs_dim
+        e = self.eps if eps is None else eps
+        oe = self.opp_eps if opp_eps is None else opp_eps
+        opp = self.spenv._opp_fused
+        key = tuple(t.data_ptr() for t in (obs, actions, logprobs, dones, rewards, values, next_obs, next_done, e, oe,
+                                           opp.flat.flat_param, opp.agent.log_std)) + (opp.prec,)
+        r = self._cache.get(key)
+        if r is None:
+            shapes = {"obs": (obs, (T, n, D)), "actions": (actions, (T, n, 2)), "logprobs": (logprobs, (T, n)),
+                      "values": (values, (T, n)), "rewards": (rewards, (T, n)), "dones": (dones, (T, n)),
+                      "next_obs": (next_obs, (n, D)), "next_done": (next_done, (n,)), "eps": (e, (T, n, 2)),
+                      "opp_eps": (oe, (T, n, 2))}
+            for k, (t, shp) in shapes.items():
+                if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous():
+                    raise ValueError(f"rx_selfplay_rollout_steps: {k} must be a contiguous float32 {shp}")
+            if len(self._cache) > 64:
+                self._cache.clear()
+            b = self.venv.buf
+            r = self._cache[key] = (
+                _lib.RxRolloutIO(T, D, _lib.ptr(self.flat.flat_param), _lib.ptr(self.agent.log_std), _lib.ptr(e),
+                                 _lib.ptr(obs), _lib.ptr(actions), _lib.ptr(logprobs), _lib.ptr(values),
+                                 _lib.ptr(rewards), _lib.ptr(dones), _lib.ptr(next_obs), _lib.ptr(next_done)),
+                _lib.RxSelfplayIO(_lib.ptr(opp.flat.flat_param), _lib.ptr(opp.agent.log_std), _lib.ptr(oe),
+                                  _lib.ptr(self.spenv._act), _lib.ptr(b["obs"]), _lib.ptr(b["reward"]),
+                                  _lib.ptr(self.sink), self.spenv.agent_idx, opp.prec))
+        if eps is None:
+            self.eps.normal_()
+        if opp_eps is None:
+            self.opp_eps.normal_()
+        io = self.venv._io()
+        _lib.check(self.L.rx_selfplay_rollout_steps(self.venv._h, io, r[0], r[1], self.prec, _lib.stream_ptr(stream)),
+                   "rx_selfplay_rollout_steps")
+        self.venv._launched(stream)
+
+
 # config["fused_rollout"] = "auto": the persistent rollout up to this many envs
 # (one workgroup per env runs all T steps; beyond what the chip holds at once
 # the workgroups would run in waves, each paying T steps of latency)

@@ -160,6 +160,20 @@ class SelfPlayPPO(PPO):
             self.envs.set_opponent(self._opp_static, self._opp_flat if fused else None, ppo_fused.precision(self.config))
         self.envs.reset_device()
 
+    def _step_rollout(self, obs):
+        """rx_selfplay_rollout_steps driver (config["rollout_steps"], default on)
+        while the opponent is a frozen policy on rx_policy_act; the random
+        opponent of an empty pool keeps the per-step path."""
+        from . import ppo_fused
+        c = self.config
+        if self._fused_policy(obs) is None or not ppo_fused.SelfPlayStepRollout.supported(self.envs, self.agent, c):
+            return None
+        T, prec = obs.shape[0], ppo_fused.precision(c)
+        sr = self.__dict__.get("_sp_steps_rollout")
+        if sr is None or sr.T != T or sr.n != self.envs.num_envs or sr.prec != prec:
+            sr = self._sp_steps_rollout = ppo_fused.SelfPlayStepRollout(self.agent, self._flat, self.envs, T, prec)
+        return sr
+
     def collect_rollout(self, *bufs):
         # one captured graph per opponent kind (random vs frozen policy): the kind
         # changes control flow inside the step, the weights do not (static module)

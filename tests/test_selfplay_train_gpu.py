@@ -101,3 +101,70 @@ def test_selfplay_training_pool5_at_configs3_size():
     assert len(t.opponent_pool) == 5
     assert torch.isfinite(t._flat.flat_param).all()
     t.envs.close()
+
+
+@pytest.mark.parametrize("n,T,prec", [(8192, 24, "fp32"), (3000, 20, "bf16")])
+def test_selfplay_rollout_steps_equals_per_step_path(n, T, prec):
+    """rx_selfplay_rollout_steps (ABI v19) == SelfPlayVectorEnv's per-step path
+    (opponent rx_policy_act on the env's agent-1 rows, agent rx_policy_act on
+    obs[t], action copy, rx_step, obs / reward copies) with the same agent and
+    opponent noise, bit for bit over two chained rollouts: every buffer, the
+    two-car state and the episode statistics."""
+    import random
+    from rx.configs import self_play_config
+    from rx.envs import MultiRacingEnv
+    from rx.selfplay import SelfPlayPPO
+    from rx.track import gen_tracks
+    res = []
+    g = torch.Generator(device="cuda").manual_seed(8)
+    eps = torch.randn((T, n, 2), device="cuda", generator=g) * 1.5
+    oeps = torch.randn((T, n, 2), device="cuda", generator=g) * 1.5
+    for fused in (True, False):
+        cfg = self_play_config(num_envs=n, num_steps=T, shuffle="device", checkpoint=False, policy_dtype=prec,
+                               rollout_steps="auto" if fused else False)
+        random.seed(1)
+        np.random.seed(1)
+        torch.manual_seed(1)
+        pool = gen_tracks(n, seed=1)
+        widths = [np.random.randint(6, 10) for _ in range(n)]
+        t = SelfPlayPPO(lambda i: MultiRacingEnv(2, 11, pool, i, widths), cfg, device="cuda")
+        torch.manual_seed(5)
+        t.opponent_pool.append(t.snapshot_agent())
+        with torch.no_grad():  # an opponent that differs from the agent, with a visible mean
+            t.opponent_pool[0].actor_mu[4].weight.mul_(40.0)
+        np.random.seed(0)
+        t.update_opponent()
+        sp = t.envs
+        bufs = t._buffers()
+        nobs = sp.buf["obs"].clone()
+        nd = torch.zeros(n, device="cuda")
+        sr = t._step_rollout(bufs[0])
+        assert (sr is not None) == fused
+        for _ in range(2):
+            obs, actions, logprobs, dones, rewards, values = bufs
+            obs[0].copy_(nobs)
+            dones[0].copy_(nd)
+            if fused:
+                sr(obs, actions, logprobs, dones, rewards, values, nobs, nd, eps=eps, opp_eps=oeps)
+            else:
+                pa = t._fused_policy(obs)
+                for s in range(T):
+                    pa(obs[s], actions[s], logprobs[s], values[s], eps=eps[s])
+                    sp._opp_fused(sp.venv.buf["obs"][:, sp.opp_idx], sp._act[:, sp.opp_idx], eps=oeps[s])
+                    sp._act[:, sp.agent_idx].copy_(actions[s])
+                    last = s + 1 == T
+                    o, r, _ = sp.venv.step_device(sp._act, done_out=nd if last else dones[s + 1])
+                    (nobs if last else obs[s + 1]).copy_(o[:, sp.agent_idx])
+                    rewards[s].copy_(r[:, sp.agent_idx])
+        torch.cuda.synchronize()
+        res.append(([x.clone() for x in bufs] + [nobs.clone(), nd.clone()], sp.venv.get_state(),
+                    sp.venv.episode_stats()))
+        sp.close()
+    (ba, sa, ea), (bb, sb, eb) = res
+    names = ("obs", "actions", "logprobs", "dones", "rewards", "values", "next_obs", "next_done")
+    for k, x, y in zip(names, ba, bb):
+        assert torch.equal(x, y), k
+    assert (ba[3] > 0).any()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    assert ea[1:] == eb[1:] and ea[0] == pytest.approx(eb[0], rel=1e-12)
