@@ -439,7 +439,7 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     warm = pool_size + 1
     cfg = self_play_config(num_envs=envs, num_steps=T, kl_target=1e9, shuffle="device", snapshot_freq=1,
                            pool_size=pool_size, checkpoint=False)
-    cfg["total_timesteps"] = (warm + updates + 1) * cfg["batch_size"]
+    cfg["total_timesteps"] = (warm + updates + 2) * cfg["batch_size"]
     random.seed(1)
     np.random.seed(1)
     torch.manual_seed(1)
@@ -459,33 +459,13 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
-    # phase split of one more update, synchronised between phases
-    u = warm + updates
-    obs, actions, logprobs, dones, rewards, values = t._buffers()
-    nobs = t.envs.buf["obs"].clone()
-    nd = torch.zeros(t.num_local_envs, device=dev)
-    ph = {}
-    torch.cuda.synchronize()
-    a = time.perf_counter()
-    t.advance_pool(u)
-    t.update_opponent()
-    torch.cuda.synchronize()
-    b = time.perf_counter()
-    out = t.collect_rollout(obs, actions, logprobs, dones, rewards, values, nobs, nd)
-    torch.cuda.synchronize()
-    c = time.perf_counter()
-    obs, actions, logprobs, dones, rewards, values, nobs, nd, _ = out
-    with torch.no_grad():
-        nv = t.agent.get_value(nobs).flatten()
-    adv, ret = t.compute_advantages(rewards, dones, values, nv, nd)
-    torch.cuda.synchronize()
-    d = time.perf_counter()
-    t.ppo_update(adv, ret, values, logprobs, actions, obs)
-    torch.cuda.synchronize()
-    e = time.perf_counter()
-    ph = {"opponent_draw_and_rebuild_ms": round((b - a) * 1e3, 3), "rollout_ms": round((c - b) * 1e3, 3),
-          "gae_ms": round((d - c) * 1e3, 3), "update_ms": round((e - d) * 1e3, 3),
-          "rollout_env_steps_per_s": round(T * envs / (c - b), 1)}
+    # phase split of one more update of the same loop (same buffers and graphs), a device
+    # sync at every phase boundary (SelfPlayPPO.phase_ms)
+    t.phase_ms = {}
+    next(it)
+    ph = dict(t.phase_ms)
+    t.phase_ms = None
+    ph["rollout_env_steps_per_s"] = round(T * envs / (ph["rollout_ms"] * 1e-3), 1)
     B = T * envs
     res = {"value": round(B * updates / el, 1), "unit": "train env-steps/s (agent-steps = 2x)", "updates": updates,
            "ms_per_update": round(el / updates * 1e3, 3), "envs": envs, "cars_per_env": 2, "num_steps": T,

@@ -114,10 +114,16 @@ class SelfPlayPPO(PPO):
         return SelfPlayVectorEnv(venv, 0, seed=c["seed"] + rdist.rank())
 
     def snapshot_agent(self):
-        snap = Agent(self.envs.single_observation_space, self.envs.single_action_space).to(self.device)
-        snap.load_state_dict(copy.deepcopy(self.agent.state_dict()))
+        """A frozen copy of the current policy (agent/self_play_ppo.py:31-44 builds a
+        fresh Agent and loads a deep copy of the state dict).  Here: ONE deepcopy of
+        the module -- its parameters are views of the flat parameter buffer, so the
+        copy is one device-to-device copy of that buffer (and of the gradient buffer)
+        with the same views -- instead of a CPU orthogonal init, 13 pageable host to
+        device copies (each one a stream sync) and 13 state-dict copies."""
+        snap = copy.deepcopy(self.agent)
         snap.eval()
         for p in snap.parameters():
+            p.grad = None
             p.requires_grad = False
         return snap
 
@@ -216,23 +222,43 @@ class SelfPlayPPO(PPO):
             start, global_step = 0, 0
             info = {"steps": [], "rewards": [], "opponent_pool_size": []}
         self._iter_info = info
+        # phase_ms (benchmarks): a dict to receive the last update's phase times, each
+        # phase bracketed by device syncs (None = no syncs, the normal path)
+        mark = self._phase_mark
         for update in range(start, num_updates):
+            mark(None)
             self.advance_pool(update)
             self.update_opponent()
             if c.get("refresh_obs_on_rebuild", False):
                 next_obs.copy_(self.envs.buf["obs"])
                 next_done.zero_()
             self._anneal(update, num_updates)
+            mark("opponent_draw_and_rebuild_ms")
             obs, actions, logprobs, dones, rewards, values, next_obs, next_done, ep = self.collect_rollout(
                 obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
+            mark("rollout_ms")
             with torch.no_grad():
                 next_value = self.agent.get_value(next_obs).flatten()
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
+            mark("gae_ms")
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
+            mark("update_ms")
             global_step += c["batch_size"]
             if c.get("checkpoint", True) and self.checkpoint_due(update) and rdist.rank() == 0:
                 self.save_checkpoint(update, global_step, info)
             yield update, num_updates, global_step, ep, info
+
+    phase_ms = None
+
+    def _phase_mark(self, name):
+        if self.phase_ms is None:
+            return
+        import time
+        torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        if name is not None:
+            self.phase_ms[name] = round((now - self._phase_t) * 1e3, 3)
+        self._phase_t = now
 
     def train(self, resume_from=None):
         info = None
