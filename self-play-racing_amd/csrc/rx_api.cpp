@@ -312,8 +312,9 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
-  if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 1))
-    return fail(RX_EINVAL, "dyn_lpe / reward_lpe > 1 are single-agent schedules (n_agents = 2)");
+  if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
+    return fail(RX_EINVAL, "n_agents = 2: dyn_lpe > 1 is a single-agent schedule, and reward_lpe is 1 or 2 "
+                           "(a lane per car)");
   if ((long long)cfg->n_envs * cfg->n_agents * cfg->n_sensors > 0x7fffffffLL)
     return fail(RX_EINVAL, "n_envs * n_agents * n_sensors overflows int32");
   int ndev = 0;
@@ -478,7 +479,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   }
   // few single-agent envs: REWARD (a latency chain of argmins) outlasts the
   // raycast beside it in k_step2 unless 2 lanes share an env's five points
-  h->reward_lpe = (A == 1 && N <= RX_REWARD_LPE2_N) ? 2 : 1;
+  h->reward_lpe = (A == 1 && N <= RX_REWARD_LPE2_N) || (A == 2 && N <= RX_REWARD2_LPE2_N) ? 2 : 1;
   if (c.reward_lpe != 0) h->reward_lpe = c.reward_lpe;
   h->split = c.split >= 0;
   // ray-wave class order and the tail split (ABI v19; scheduling only)

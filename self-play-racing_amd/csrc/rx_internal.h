@@ -77,6 +77,11 @@ struct rx_track_view {
 #ifndef RX_REWARD_LPE2_N
 #define RX_REWARD_LPE2_N 4096
 #endif
+// two-car envs: k_step2<2>'s REWARD half with a lane per car (one closest-waypoint
+// pass per wave instead of two) up to this many envs (0 = never; set by A/B)
+#ifndef RX_REWARD2_LPE2_N
+#define RX_REWARD2_LPE2_N 0
+#endif
 // Ray-wave dispatch order (rx_assign's placement of the ray-wave table, ray_order 2).
 // Class j of a 64-env group = its j-th wave of direction-sorted tasks (the cars of a
 // group head alike, so class j ~ sensor ray j: the edge classes look sideways, the

@@ -954,12 +954,19 @@ __device__ __forceinline__ bool rect_intersect(const double ax[4], const double 
 // KIN passes "the cars touched" to REWARD in env_flags (RX_EF_TOUCH) and the
 // stepped cos / sin of each moving car in cs_scratch[2e + q].
 #define RX_EF_TOUCH 4u
-template <int PART>
-__device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3]) {
+// RLPE (REWARD only): lanes per env.  2 = a lane pair per env, lane `sub` runs
+// car `sub`'s closest-waypoint pass (the REWARD chain's two sequential passes
+// become one), the pair exchanges progress / crash flag, and lane 0 of the pair
+// does the rest; sub_block picks which 32 of the dynamics wave's 64 envs.
+template <int PART, int RLPE = 1>
+__device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
+                                         int sub_block = 0) {
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
+  static_assert(RLPE == 1 || (RLPE == 2 && REW), "two lanes per env: the REWARD part only");
   if (wave >= a.n_dyn_waves) return;
   const rx_wave we = a.dyn_waves[wave];
-  const int lane = threadIdx.x & 63;
+  const int lane = (int)(threadIdx.x & 63) / RLPE + sub_block * (64 / RLPE);
+  const int sub = (int)threadIdx.x & (RLPE - 1);
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
   const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
@@ -1030,7 +1037,42 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
         }
       }
     }
-    if (REW && (mv[0] || mv[1])) {
+    if (REW && RLPE == 2) {
+      // lane `sub` = car `sub`: ONE pass per wave over both cars' points (the
+      // argmin is per lane, culling over the wave's union), then the pair swaps
+      const bool mvq = sub ? mv[1] : mv[0];
+      Car cq = sub ? c[1] : c[0];
+      if (__any(mvq)) {
+        const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[2 * p + sub];
+        double px[5], py[5];
+        px[0] = cq.x;
+        py[0] = cq.y;
+        corners(cq.x, cq.y, sc.x, sc.y, px + 1, py + 1);
+        int idx[5];
+        if (a.cull_chunk > 0) {
+          const int prev[1] = {prev_waypoint(cq.progress, W)};
+          const double ccx[1] = {cq.x}, ccy[1] = {cq.y};
+          argmin_culled<5, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
+                              a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, px, py, prev, ccx, ccy,
+                              a.argmin_window, idx, a.io.counters, nullptr, mvq);
+        } else {
+          argmin_pts<5>(wp, W, px, py, idx);
+        }
+        if (mvq) {
+          cq.progress = (double)idx[0] / (double)W;
+          bool out = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) out = out || corner_out(wp, nrm, idx[1 + j], px[1 + j], py[1 + j], width);
+          cq.crashed = out;
+        }
+      }
+      const double po = __shfl_xor(cq.progress, 1, 64);
+      const int co = __shfl_xor(cq.crashed ? 1 : 0, 1, 64);
+      c[0].progress = sub ? po : cq.progress;
+      c[0].crashed = sub ? (co != 0) : cq.crashed;
+      c[1].progress = sub ? cq.progress : po;
+      c[1].crashed = sub ? cq.crashed : (co != 0);
+    } else if (REW && (mv[0] || mv[1])) {
       // one pass per car (as FULL's culled passes below): corners of the stepped
       // pose (car.py:26-43, KIN's cos / sin), the 5 closest waypoints, wall
       // collision; only this car's corners are live during its pass
@@ -1061,6 +1103,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
         }
       }
     }
+    if (REW && RLPE == 2 && sub != 0) return;  // one lane per env from here on
     if (REW) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -1136,6 +1179,7 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
     }
     if (!REW) steps += 1;
   }
+  if (REW && RLPE == 2 && sub != 0) return;  // (not stepping: the pass above did not run)
   if (!KIN && stepping) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1871,7 +1915,8 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 // the three schedules of each half inlined into ONE kernel, its register
 // allocation was the maximum over all of them, and the REWARD half spilled at
 // the raycast's 64-VGPR cap (k_step2<1>: 36 B/lane of scratch) whichever
-// schedule ran.  RLPE is ignored for A = 2 (one lane per env).
+// schedule ran.  For A = 2, RLPE 2 gives each car of an env its own lane in the
+// REWARD half (dyn2_env<REWARD, 2>).
 template <int A, int RLPE, int LPR>
 __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void k_step2(rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
@@ -1890,8 +1935,12 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
       // XCD (b % 8) of its k_kin1 wave (n1 = n_dyn_waves rounded up to 8)
       const int n1 = n_rw / RLPE, w = b % n1, sb = b / n1;
       dyn1_env<RLPE, RX_PART_REWARD>(a, w, ang, e, ep, RLPE == 1 ? 0 : sb);
-    } else
+    } else if constexpr (RLPE == 2) {
+      const int n1 = n_rw / 2, w = b % n1, sb = b / n1;  // as the single-agent REWARD half at 2 lanes
+      dyn2_env<RX_PART_REWARD, 2>(a, w, ang, e, ep, sb);
+    } else {
       dyn2_env<RX_PART_REWARD>(a, b, ang, e, ep);
+    }
     add_episode_stats(a, ep);
   } else {
     rays_dispatch<A, LPR>(a, b - n_rw);
@@ -2268,11 +2317,16 @@ static void launch_step2_lpr(const rx_kargs* a, dim3 grid, int n_rw, hipStream_t
 
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s) {
   if (n_agents == 2) {  // k_kin2, then k_step2<2> (REWARD waves padded to 8, as below)
-    const int n_rw2 = (a->n_dyn_waves + 7) / 8 * 8;
-    if (part == RX_SPLIT_KIN)
+    const int n_rw2 = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);
+    if (part == RX_SPLIT_KIN) {
       hipLaunchKernelGGL((k_dyn2<RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
-    else
-      launch_step2_lpr<2, 1>(a, dim3(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves)), n_rw2, s);
+    } else {
+      const dim3 grid(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves));
+      if (a->reward_lpe == 2)
+        launch_step2_lpr<2, 2>(a, grid, n_rw2, s);
+      else
+        launch_step2_lpr<2, 1>(a, grid, n_rw2, s);
+    }
     return (int)hipGetLastError();
   }
   const int n_rw = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);

@@ -480,6 +480,36 @@ def test_reward_lanes_per_env_are_exact(rx, golden, N, lpe):
     vb.close()
 
 
+@pytest.mark.parametrize("N,lpr", [(3000, 0), (8192, 0), (2048, 1)])
+def test_two_car_reward_lane_per_car_is_exact(rx, golden, N, lpr):
+    """k_step2<2>'s REWARD half with a lane per car (reward_lpe = 2 for two cars:
+    one closest-waypoint pass per wave instead of two, the pair swapping progress
+    and crash flags) against one lane per env: obs, rewards, dones, placement /
+    info and the whole state bit-identical over 300 steps of random play; episode
+    counts exact.  Ragged last wave at 3,000 envs."""
+    tracks = np.arange(N) % golden.n_tracks
+    base = dict(ray_lpr=lpr) if lpr else {}
+    va = _venv(rx, golden, tracks, n_agents=2, seed=7, autoreset="next_step", sched=dict(base, reward_lpe=1))
+    vb = _venv(rx, golden, tracks, n_agents=2, seed=7, autoreset="next_step", sched=dict(base, reward_lpe=2))
+    assert vb.schedule()["reward_lpe"] == 2 and vb.schedule()["split"] == 1
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(19)
+    for t in range(300):
+        a = torch.rand((N, 2, 2), device="cuda", generator=g) * 2.4 - 1.2
+        oa, ra, da = va.step_device(a, full_info=True)
+        ob, rb, db = vb.step_device(a, full_info=True)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        for k in ("reward64", "terminated", "truncated", "info", "ep_done"):
+            assert torch.equal(va.buf[k], vb.buf[k]), (t, k)
+    sa, sb = va.get_state(), vb.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    (ra_, la_, ca_), (rb_, lb_, cb_) = va.episode_stats(), vb.episode_stats()
+    assert ca_ == cb_ > 0 and la_ == lb_ and abs(ra_ - rb_) <= 1e-9 * max(1.0, abs(ra_))
+    va.close()
+    vb.close()
+
+
 def test_culled_raycast_on_golden_kats(rx, golden):
     """Track.raycast golden KATs (incl. no-hit, > 50 uncapped, grazing, far
     origins) through the culled kernel: sensor 5 (relative angle exactly 0)

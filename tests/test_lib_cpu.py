@@ -108,6 +108,8 @@ def test_schedule_config_is_validated_and_the_library_reads_no_environment():
     two[1] = 2
     assert L.rx_create(_lib.RxConfig(*two, *[2 if f == "dyn_lpe" else 0 for f in _lib.SCHED_FIELDS]), h) \
         == _lib.RX_EINVAL
+    assert L.rx_create(_lib.RxConfig(*two, *[4 if f == "reward_lpe" else 0 for f in _lib.SCHED_FIELDS]), h) \
+        == _lib.RX_EINVAL  # two cars: reward_lpe 1 or 2 (a lane per car)
     # every in-range value passes validation (on a CPU-only host rx_create then fails at the device query)
     import torch
     if not torch.cuda.is_available():
