@@ -474,7 +474,8 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   // fill the chip, so 2 or 4 lanes share one ray and split its leaves
   h->ray_lpr = 1;
   if (h->cfg.ray_order == 2 && h->dyn_lpe != 64) {
-    h->ray_lpr = (long long)N * A <= RX_RAY_LPR4_N ? 4 : ((long long)N * A <= RX_RAY_LPR2_N ? 2 : 1);
+    const long long pairs = (long long)N * A, lpr2_n = A == 2 ? RX_RAY2_LPR2_N : RX_RAY_LPR2_N;
+    h->ray_lpr = pairs <= RX_RAY_LPR4_N ? 4 : (pairs <= lpr2_n ? 2 : 1);
     if (c.ray_lpr != 0) h->ray_lpr = c.ray_lpr;
   }
   // few single-agent envs: REWARD (a latency chain of argmins) outlasts the

@@ -78,9 +78,18 @@ struct rx_track_view {
 #define RX_REWARD_LPE2_N 4096
 #endif
 // two-car envs: k_step2<2>'s REWARD half with a lane per car (one closest-waypoint
-// pass per wave instead of two) up to this many envs (0 = never; set by A/B)
+// pass per wave instead of two) up to this many envs.  Same-session A/B
+// (profiles/r04/ab_two_car_*.jsonl): 4,096 envs 67.2 -> 79.2 M env-steps/s,
+// 8,192 128.1 -> 134.7 M (with one lane per ray), 16,384 213.2 -> 220.3 M,
+// 65,536 389 -> 387 M (off there)
 #ifndef RX_REWARD2_LPE2_N
-#define RX_REWARD2_LPE2_N 0
+#define RX_REWARD2_LPE2_N 16384
+#endif
+// two-car envs: 2 lanes per ray only up to this many (env, car) pairs (the
+// single-agent RX_RAY_LPR2_N band is empty for them: with the REWARD half at a
+// lane per car, 8,192 envs run 134.7 M at 1 lane per ray vs 128.6 M at 2)
+#ifndef RX_RAY2_LPR2_N
+#define RX_RAY2_LPR2_N 8192
 #endif
 // Ray-wave dispatch order (rx_assign's placement of the ray-wave table, ray_order 2).
 // Class j of a 64-env group = its j-th wave of direction-sorted tasks (the cars of a

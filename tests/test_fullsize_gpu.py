@@ -159,19 +159,22 @@ def test_episode_statistics_all_shards_at_65536():
     v.close()
 
 
-@pytest.mark.parametrize("N,n_sub", [(8192, 2048), (4096, 1024)])
-def test_two_car_subset_bit_exact_vs_oracle(oracle_dev, N, n_sub):
-    """configs[3]'s env at 8,192 two-car envs (2 lanes per ray task: 16,384
-    cars) and at 4,096 (4 lanes per ray task), both on the split step k_kin2 +
-    k_step2<2>: a random subset == the oracle bit for bit over 200 steps.  On a reset the start-slot order is drawn on the device (the
+@pytest.mark.parametrize("N,n_sub,sched", [(8192, 2048, None), (4096, 1024, None), (8192, 1024, {"ray_lpr": 2, "reward_lpe": 1})])
+def test_two_car_subset_bit_exact_vs_oracle(oracle_dev, N, n_sub, sched):
+    """configs[3]'s env at 8,192 two-car envs (default: a lane per ray task and
+    the REWARD half at a lane per car) and at 4,096 (4 lanes per ray task), plus
+    8,192 on round 3's schedule (2 lanes per ray, one REWARD lane per env), all
+    on the split step k_kin2 + k_step2<2>: a random subset == the oracle bit
+    for bit over 200 steps.  On a reset the start-slot order is drawn on the device (the
     reference draws it from the global np.random, multi_racing_env.py:122-138):
     the oracle resets with the order the device chose, which must be one of the
     two slot assignments."""
     from rx.vector_env import RacingVectorEnv
     pool, widths = _seed1_pool(N)
-    v = RacingVectorEnv(pool, widths, n_agents=2, device="cuda", autoreset="next_step", seed=9)
+    v = RacingVectorEnv(pool, widths, n_agents=2, device="cuda", autoreset="next_step", seed=9, sched=sched)
     sch = v.schedule()
-    assert sch["split"] == 1 and sch["wide"] == 0 and sch["ray_lpr"] == (4 if 2 * N <= 8192 else 2), sch
+    want = dict(ray_lpr=4 if 2 * N <= 8192 else 1, reward_lpe=2) if sched is None else sched
+    assert sch["split"] == 1 and sch["wide"] == 0 and all(sch[k] == want[k] for k in want), sch
     tab = _oracle_table(v)
     idx = np.sort(np.random.default_rng(5).choice(N, n_sub, replace=False))
     n = len(idx)
