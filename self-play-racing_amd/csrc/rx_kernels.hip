@@ -42,6 +42,14 @@ struct Car {
 };
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// a wave-uniform double into an SGPR pair (a value loaded from a uniform address
+// the compiler cannot prove unclobbered otherwise occupies two VGPRs)
+__device__ __forceinline__ double uniform_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -973,8 +981,8 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   const double2* __restrict__ wp = reinterpret_cast<const double2*>(a.tr.wp) + wp0;
   const double2* __restrict__ nrm = reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
   const double* __restrict__ meta = a.tr.meta + 8 * k;
-  const double width = meta[3];
-  const double maxd = meta[4];
+  const double width = uniform_d(meta[3]);
+  const double maxd = uniform_d(meta[4]);
   if (lane >= we.count) return;
   const int p = we.perm_start + lane;  // working-state position (see dyn1_env)
   const int e = a.perm[p];             // env id: io rows, the start-slot draw

@@ -352,15 +352,20 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   constexpr bool KSPLIT = kGW == 8 && NT1 == 1;
   const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
   const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
-  const float mean = b.adv_stats[2 * a.m], sd = b.adv_stats[2 * a.m + 1];
+  // wave-uniform operands in SGPRs: scalar loads through the constant address
+  // space (a plain load through a pointer the compiler cannot prove unclobbered
+  // is a vector load, and its result would hold VGPRs across every pass)
+  auto sgpr = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+  auto sload = [](const float* p) { return *(const __attribute__((address_space(4))) float*)p; };
+  const float mean = sload(b.adv_stats + 2 * a.m), sd = sload(b.adv_stats + 2 * a.m + 1);
   const float invM = 1.0f / (float)b.mb;
   const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
   float var[kNA], lsc[kNA];
 #pragma unroll
   for (int j = 0; j < kNA; ++j) {
-    const float scale = expf(b.log_std[j]);
-    var[j] = scale * scale;
-    lsc[j] = logf(scale);
+    const float scale = expf(sload(b.log_std + j));
+    var[j] = sgpr(scale * scale);
+    lsc[j] = sgpr(logf(scale));
   }
   f4 acc2[NT2], acc1[NA1];  // dW2 / dW1 (+ db1) tiles of rows [16 rb, +16)
 #pragma unroll
