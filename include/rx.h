@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 19
+#define RX_ABI_VERSION 20
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -232,6 +232,21 @@ int rx_set_speed_weight(rx_env* h, double speed_weight);
  * MultiRacingEnv.reset (multi_racing_env.py:118-153).  Writes obs (and zeros
  * reward/terminated/truncated/done_f32 of the reset envs when given). */
 int rx_reset(rx_env* h, const uint8_t* mask, const rx_io* io, void* stream);
+
+/* ABI v20.  The two-car start-slot order from the reference's own RNG stream:
+ * MultiRacingEnv.reset draws it with np.random.shuffle(agent_order) on the
+ * global numpy RNG (multi_racing_env.py:127-128), one MT19937 output u per
+ * reset (j = u & 1: the two cars swap when j == 0), and SyncVectorEnv resets
+ * its envs in env order.  With draws set, the env that is the j-th to reset in
+ * a launch (env order: rx_reset's mask, or the next-step autoreset of rx_step)
+ * takes draws[cursor[0] + j], and the launch advances cursor[0] by its reset
+ * count.  draws: device uint32 [n_draws], the caller's upcoming MT19937 outputs
+ * (e.g. np.random.randint(0, 2**32, n, dtype=np.uint32) from a copy of the
+ * global state); cursor: device int64 [2], cursor[1] += the draws a launch
+ * needed beyond n_draws (those resets are then wrong: refill and redo).
+ * draws = NULL restores the device hash.  Two-car handles, next-step or no
+ * autoreset (same-step autoreset draws inside the step: RX_EINVAL). */
+int rx_set_start_draws(rx_env* h, const uint32_t* draws, int64_t n_draws, int64_t* cursor);
 
 /* One vectorised step.  Replaces SyncVectorEnv.step -> RecordEpisodeStatistics
  * -> RacingEnv.step (racing_env.py:104-167) / SelfPlayWrapper.step ->

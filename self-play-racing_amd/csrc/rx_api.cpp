@@ -93,6 +93,12 @@ struct rx_env {
   std::vector<rx_wave> ray_waves_h;  // host copy of the ray-wave table (rx_ray_waves)
   DevBuf<int32_t> slot_n;   // envs per slot (ray-major decode)
   DevBuf<uint32_t> resets;  // per-env reset count: keys the 2-car start-slot draw (graph-replay safe)
+  // rx_set_start_draws: the caller's MT19937 outputs and cursor; ranks of the resetting envs
+  const uint32_t* draws = nullptr;
+  int64_t n_draws = 0;
+  int64_t* draw_cursor = nullptr;
+  DevBuf<int32_t> draw_rank, draw_tmp;
+  DevBuf<int64_t> draw_base;
   int32_t n_dyn_waves = 0, n_ray_waves = 0;
   int32_t dyn_lpe = 1;
   int32_t ray_lpr = 1;  // lanes per ray task (ray_order 2, not wide): 64 / ray_lpr tasks a ray wave
@@ -392,6 +398,9 @@ int rx_destroy(rx_env* h) {
   h->cs_scratch.release();
   h->prof_buf.release();
   h->resets.release();
+  h->draw_rank.release();
+  h->draw_tmp.release();
+  h->draw_base.release();
   h->chunk_box_f.release();
   h->super_box_f.release();
   h->seg_f.release();
@@ -803,6 +812,17 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   // (same-step autoreset needs done before the observation; explicit resets
   // and small single-agent N use the one-kernel path).
   const int A = h->cfg.n_agents;
+  // rx_set_start_draws: rank the envs this launch's dynamics kernel resets (env order)
+  if (h->draws && A == 2 && (phases & RX_PHASE_DYNAMICS) &&
+      (mode == RX_MODE_RESET || h->cfg.autoreset == RX_AUTORESET_NEXT_STEP)) {
+    if ((rc = rx_launch_reset_rank(h->cfg.n_envs, mode, mask, a.st.env_flags, a.perm, h->draw_tmp.p, h->draw_rank.p,
+                                   h->draw_cursor, h->draw_base.p, h->n_draws, s)) != 0)
+      return fail(RX_EHIP, "k_reset_rank launch failed: %s", hipGetErrorString((hipError_t)rc));
+    a.draws = h->draws;
+    a.n_draws = h->n_draws;
+    a.draw_base = h->draw_base.p;
+    a.reset_rank = h->draw_rank.p;
+  }
   const bool split = h->split && mode == RX_MODE_STEP && (A == 2 || h->dyn_lpe == 1) &&
                      h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
   // Spatial re-sort, every sort_interval dynamics launches: that launch's
@@ -959,6 +979,34 @@ int rx_ray_waves(const rx_env* h, int32_t* out, int32_t cap, int32_t* n_waves) {
     out[4 * i + 3] = w.count;
   }
   *n_waves = (int32_t)n;
+  return RX_OK;
+}
+
+int rx_set_start_draws(rx_env* h, const uint32_t* draws, int64_t n_draws, int64_t* cursor) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (!draws) {
+    h->draws = nullptr, h->n_draws = 0, h->draw_cursor = nullptr;
+    return RX_OK;
+  }
+  if (h->cfg.n_agents != 2) return fail(RX_EINVAL, "rx_set_start_draws: single-agent resets draw nothing");
+  if (h->cfg.autoreset == RX_AUTORESET_SAME_STEP)
+    return fail(RX_EINVAL, "rx_set_start_draws: same-step autoreset draws inside the step (unsupported)");
+  if (n_draws < 0 || !cursor) return fail(RX_EINVAL, "rx_set_start_draws: need n_draws >= 0 and a cursor");
+  RX_HIP(hipSetDevice(h->cfg.device));
+  const size_t N = (size_t)h->cfg.n_envs;
+  if (h->draw_rank.n < N) {
+    h->draw_rank.release();
+    h->draw_tmp.release();
+    if (hipMalloc(&h->draw_rank.p, N * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&h->draw_tmp.p, N * sizeof(int32_t)) != hipSuccess)
+      return fail(RX_ENOMEM, "rx_set_start_draws: rank buffers");
+    h->draw_rank.n = h->draw_tmp.n = N;
+  }
+  if (!h->draw_base.p) {
+    if (hipMalloc(&h->draw_base.p, sizeof(int64_t)) != hipSuccess) return fail(RX_ENOMEM, "rx_set_start_draws");
+    h->draw_base.n = 1;
+  }
+  h->draws = draws, h->n_draws = n_draws, h->draw_cursor = cursor;
   return RX_OK;
 }
 

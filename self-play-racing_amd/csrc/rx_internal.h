@@ -160,6 +160,13 @@ struct rx_kargs {
   int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
   int32_t ray_tail_from;  // ray waves >= this one (the dispatch tail) hold 64 / ray_tail_lpr tasks each, cast at
   int32_t ray_tail_lpr;   // ray_tail_lpr lanes per ray (2 or 4); -1 = no tail split (rx_config.ray_tail)
+  // rx_set_start_draws (two-car envs): the start-slot order of the env that is the
+  // j-th to reset in this launch, in env order, comes from draws[*draw_base + j]
+  // (j = reset_rank[e], k_reset_rank) instead of the device hash; nullptr = hash
+  const uint32_t* draws;
+  int64_t n_draws;
+  const int64_t* draw_base;
+  const int32_t* reset_rank;
 };
 
 extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipStream_t s);
@@ -172,6 +179,13 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024
 extern "C" int rx_launch_rollout(const rx_kargs* a, const rx_rollout_io* r, int max_w, hipStream_t s);
+// rx_set_start_draws: ranks (env order) of the envs the next dynamics launch resets
+// (mode RX_MODE_RESET: mask[e] or all; RX_MODE_STEP: the next-step autoreset flag of
+// the env's working-state row), *base = cursor[0], cursor[0] += their count,
+// cursor[1] += the draws missing when the count overruns n_draws
+extern "C" int rx_launch_reset_rank(int N, int mode, const uint8_t* mask, const uint8_t* env_flags, const int32_t* perm,
+                                    int32_t* tmp, int32_t* rank, int64_t* cursor, int64_t* base, int64_t n_draws,
+                                    hipStream_t s);
 extern "C" int rx_launch_agent_rows(int N, int D, int q, const float* obs, const float* rew, float* obs_out,
                                     float* rew_out, hipStream_t s);
 extern "C" int rx_launch_gae(int T, int N, const float* r, const float* v, const float* d, const float* nv,

@@ -1248,7 +1248,15 @@ __device__ __forceinline__ void dyn2_env(const rx_kargs& a, int wave, double* an
   if (!REW && do_reset) {  // multi_racing_env.py:118-153; start slot from the device RNG
     have_sc[0] = have_sc[1] = false;  // angles are reset below
     const uint64_t h = splitmix64(a.seed ^ splitmix64(((uint64_t)a.reset_count[e]++ << 32) ^ (uint64_t)e));
-    const int first = (int)(h & 1ull);  // agent_order[0] after np.random.shuffle([0, 1])
+    // agent_order[0] after np.random.shuffle([0, 1]) (multi_racing_env.py:127-128): with
+    // rx_set_start_draws the shuffle's own draw -- one MT19937 output u, j = u & 1,
+    // swap when j == 0 -- of the env's turn in the reference's env-order reset
+    // sequence; otherwise the device hash
+    int first = (int)(h & 1ull);
+    if (a.draws) {
+      const int64_t j = *a.draw_base + a.reset_rank[e];
+      first = (j < a.n_draws && (a.draws[j] & 1u)) ? 0 : 1;
+    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const double offset = ((double)((first == q) ? 0 : 1) - 0.5) * 3.5;
@@ -2408,6 +2416,58 @@ __global__ __launch_bounds__(256) void k_agent_rows(int N, int D, int q, const f
     obs_out[i] = obs[(size_t)(2 * e + q) * D + d];
   }
   if (i < N) rew_out[i] = rew[2 * i + q];
+}
+
+// k_reset_rank (rx_set_start_draws): one workgroup.  Pass 1 lays the reset flags
+// out in env order (RX_MODE_STEP: a working-state row's next-step autoreset flag
+// goes to its env perm[p]); pass 2 ranks them -- thread t counts a contiguous run
+// of envs, an LDS scan over the 1,024 counts gives each run's offset -- so the
+// j-th resetting env in env order gets rank j, as the reference's SyncVectorEnv
+// loop draws them.  Thread 0 hands the launch its base and advances the cursor.
+__global__ __launch_bounds__(1024) void k_reset_rank(int N, int mode, const uint8_t* __restrict__ mask,
+                                                     const uint8_t* __restrict__ env_flags,
+                                                     const int32_t* __restrict__ perm, int32_t* __restrict__ tmp,
+                                                     int32_t* __restrict__ rank, int64_t* cursor, int64_t* base,
+                                                     int64_t n_draws) {
+  __shared__ int32_t cnt[1024];
+  const int t = threadIdx.x;
+  if (mode == RX_MODE_RESET) {
+    for (int e = t; e < N; e += 1024) tmp[e] = mask ? (mask[e] != 0) : 1;
+  } else {
+    for (int p = t; p < N; p += 1024) tmp[perm[p]] = (env_flags[p] & RX_EF_PENDING_RESET) != 0;
+  }
+  __syncthreads();
+  const int run = (N + 1023) / 1024, e0 = t * run, e1 = min(N, e0 + run);
+  int c = 0;
+  for (int e = e0; e < e1; ++e) c += tmp[e];
+  cnt[t] = c;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = t >= o ? cnt[t - o] : 0;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  int r = cnt[t] - c;
+  for (int e = e0; e < e1; ++e) {
+    const int f = tmp[e];
+    rank[e] = f ? r : -1;
+    r += f;
+  }
+  if (t == 1023) {
+    const int64_t b = cursor[0], total = cnt[1023];
+    *base = b;
+    cursor[0] = b + total;
+    if (b + total > n_draws) cursor[1] += b + total - max(b, n_draws);
+  }
+}
+
+extern "C" int rx_launch_reset_rank(int N, int mode, const uint8_t* mask, const uint8_t* env_flags, const int32_t* perm,
+                                    int32_t* tmp, int32_t* rank, int64_t* cursor, int64_t* base, int64_t n_draws,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(k_reset_rank, dim3(1), dim3(1024), 0, s, N, mode, mask, env_flags, perm, tmp, rank, cursor, base,
+                     n_draws);
+  return (int)hipGetLastError();
 }
 
 extern "C" int rx_launch_agent_rows(int N, int D, int q, const float* obs, const float* rew, float* obs_out,

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -31,7 +31,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
-           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves",
+           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_set_start_draws",
            "rx_rollout_steps", "rx_selfplay_rollout_steps")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
@@ -181,6 +181,7 @@ def load(build_if_missing=True):
     L.rx_profile_read.argtypes = [_P, _P, _P]
     L.rx_profile_waves.argtypes = [_P, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, _P]
     L.rx_ray_waves.argtypes = [_P, _P, ctypes.c_int32, _P]
+    L.rx_set_start_draws.argtypes = [_P, _P, ctypes.c_int64, _P]
     for name in EXPORTS:
         if name not in ("rx_last_error", "rx_abi_version", "rx_ppo_workspace_floats", "rx_ppo_workspace_doubles",
                         "rx_ppo_update_workspace_floats", "rx_adam_workspace_floats",

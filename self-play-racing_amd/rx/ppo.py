@@ -209,7 +209,11 @@ class PPO:
         every update (default "auto" = eager: the launches of one step cost
         less host time than their kernels' GPU time, measured down to 16 envs,
         so a capture would only add its one-time cost)."""
-        with torch.no_grad():
+        venv = getattr(self.envs, "venv", self.envs)
+        T, n = obs.shape[0], obs.shape[1]
+        # numpy start draws (two-car envs, config["start_draws"] = "numpy"): one
+        # session for the whole rollout, at most one reset per env every other step
+        with torch.no_grad(), venv.start_draw_session(T * n // 2 + n):
             # eager by default: with the cached per-step ctypes structs the host
             # keeps ahead of the GPU even at 16 envs, and a capture costs ~0.2 s
             if self._want_graph("graph_rollout", False):

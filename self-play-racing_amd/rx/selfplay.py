@@ -89,6 +89,10 @@ class SelfPlayVectorEnv:
     def episode_stats(self, reset=True):
         return self.venv.episode_stats(reset)
 
+    def _launched(self, stream=None):
+        """A replayed rollout graph moved the two-car handle's working state."""
+        self.venv._launched(stream)
+
     def close(self):
         self.venv.close()
 
@@ -111,6 +115,8 @@ class SelfPlayPPO(PPO):
         lo, n = rdist.shard(c["num_envs"])
         fn = env_fn if lo == 0 else (lambda i: env_fn(lo + i))
         venv = build_vector_env(fn, n, c["seed"] + rdist.rank(), self.device)
+        if c.get("start_draws", "hash") == "numpy":  # the reference's np.random start-slot stream
+            venv.use_numpy_start_draws()
         return SelfPlayVectorEnv(venv, 0, seed=c["seed"] + rdist.rank())
 
     def snapshot_agent(self):

@@ -17,6 +17,7 @@ step after a terminal one ignores the action, resets the env and reports
 reward 0, terminated = truncated = False (unpinned, gymnasium
 is not installed here).
 """
+import contextlib
 import ctypes
 import time
 
@@ -46,6 +47,46 @@ class _EnvProxy:
 
     def __init__(self, idx):
         self.idx = idx
+
+
+class _NumpyStartDraws:
+    """The two-car start-slot order from the global numpy RNG, as the reference
+    draws it: MultiRacingEnv.reset calls np.random.shuffle(agent_order) on a
+    2-list (multi_racing_env.py:127-128), one MT19937 output u per reset (the cars
+    swap when u & 1 == 0), and SyncVectorEnv resets its envs in env order.  A
+    session copies the upcoming outputs to the device (from a copy of the global
+    state), the launches take them in that order (rx_set_start_draws), and the
+    end advances the global state by exactly the number taken."""
+
+    def __init__(self, env):
+        self.env = env
+        self.cursor = torch.zeros(2, dtype=torch.int64, device=env.device)
+        self.buf = None
+        self.active = False
+        self.state0 = None
+
+    def begin(self, cap):
+        cap = max(int(cap), 1)
+        self.state0 = np.random.get_state()
+        u = np.random.randint(0, 2**32, size=cap, dtype=np.uint32)
+        np.random.set_state(self.state0)
+        if self.buf is None or self.buf.numel() < cap:
+            self.buf = torch.empty(cap, dtype=torch.int32, device=self.env.device)
+        self.buf[:cap].copy_(torch.from_numpy(u.view(np.int32)))
+        self.cursor.zero_()
+        _lib.check(self.env.L.rx_set_start_draws(self.env._h, _lib.ptr(self.buf), cap, _lib.ptr(self.cursor)),
+                   "rx_set_start_draws")
+        self.active = True
+
+    def end(self):
+        self.active = False
+        torch.cuda.synchronize(self.env.device)
+        used, over = (int(x) for x in self.cursor.cpu().numpy())
+        np.random.set_state(self.state0)
+        if used:
+            np.random.randint(0, 2**32, size=used, dtype=np.uint32)  # the reference's draws, consumed
+        if over:
+            raise _lib.RxError(f"start draws: {over} resets beyond the session's {self.buf.numel()} draws")
 
 
 class RacingVectorEnv:
@@ -144,6 +185,7 @@ class RacingVectorEnv:
                                 np.tile(self.single_action_space.high, (N, 1)), shape=(N, 2), dtype=np.float32)
         self.envs = [_EnvProxy(i) for i in range(N)]
         self.counters = None
+        self._draws = None  # use_numpy_start_draws
         self._io_cache = {}
         self._episode_start = np.full(N, time.perf_counter())
         self._closed = False
@@ -322,6 +364,35 @@ class RacingVectorEnv:
             raise ValueError(f"actions must have {self.num_envs}x{A}x2 elements, got shape {tuple(a.shape)}")
         return a.contiguous()
 
+    # ------------------------------------------------------------ start draws
+    def use_numpy_start_draws(self, on=True):
+        """Two-car envs: draw each reset's start-slot order from the global numpy
+        RNG exactly as the reference does (np.random.shuffle in MultiRacingEnv.reset,
+        multi_racing_env.py:127-128, envs in env order) instead of the device hash.
+        Every reset / step / rollout then synchronises once at its end to advance
+        np.random by the draws it took."""
+        if self.n_agents != 2:
+            raise ValueError("start-slot draws exist for two-car envs only")
+        if on:
+            self._draws = getattr(self, "_draws", None) or _NumpyStartDraws(self)
+        else:
+            self._draws = None
+            _lib.check(self.L.rx_set_start_draws(self._h, None, 0, None), "rx_set_start_draws")
+
+    @contextlib.contextmanager
+    def start_draw_session(self, cap):
+        """Brackets launches that may reset envs (at most ``cap`` resets in all) when
+        numpy start draws are on; nested sessions join the outer one."""
+        d = getattr(self, "_draws", None)
+        if d is None or d.active:
+            yield
+            return
+        d.begin(cap)
+        try:
+            yield
+        finally:
+            d.end()
+
     # ------------------------------------------------------------ device path
     def reset_device(self, mask=None, obs_out=None, stream=None):
         """Reset all envs (or where ``mask``, a device uint8/bool [N]); returns obs."""
@@ -329,7 +400,8 @@ class RacingVectorEnv:
         if mask is not None:
             m = mask.to(self.device, torch.uint8).contiguous()
         io = self._io(obs=obs_out, full=True)
-        _lib.check(self.L.rx_reset(self._h, _lib.ptr(m), io, _lib.stream_ptr(stream)), "rx_reset")
+        with self.start_draw_session(self.num_envs):
+            _lib.check(self.L.rx_reset(self._h, _lib.ptr(m), io, _lib.stream_ptr(stream)), "rx_reset")
         self._launched(stream)
         return obs_out if obs_out is not None else self.buf["obs"]
 
@@ -343,10 +415,11 @@ class RacingVectorEnv:
         a = self._as_actions(actions)
         io = self._io(actions=a, obs=obs_out, reward=reward_out, done=done_out, full=full_info)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)  # resolved once per step
-        if phases == 3:
-            _lib.check(self.L.rx_step(self._h, io, s.cuda_stream), "rx_step")
-        else:
-            _lib.check(self.L.rx_step_phases(self._h, io, int(phases), s.cuda_stream), "rx_step_phases")
+        with self.start_draw_session(self.num_envs):
+            if phases == 3:
+                _lib.check(self.L.rx_step(self._h, io, s.cuda_stream), "rx_step")
+            else:
+                _lib.check(self.L.rx_step_phases(self._h, io, int(phases), s.cuda_stream), "rx_step_phases")
         self._launched(s)
         return (obs_out if obs_out is not None else self.buf["obs"],
                 reward_out if reward_out is not None else self.buf["reward"],

@@ -122,6 +122,40 @@ def test_graph_rollout_equals_eager_across_updates(fused_rollout):
             assert torch.equal(x, y)
 
 
+def test_selfplay_graph_rollout_equals_eager():
+    """Self-play (configs[3]'s wiring, frozen pool opponent): the captured rollout
+    (graph_rollout = True) == the eager one over two rollouts, buffers and the
+    two-car env state bit for bit."""
+    from rx.configs import self_play_config
+    from rx.envs import MultiRacingEnv
+    from rx.selfplay import SelfPlayPPO
+    from rx.track import gen_tracks
+    outs = []
+    for graph in (True, False):
+        config = self_play_config(num_envs=64, num_steps=16, graph_rollout=graph)
+        random.seed(1)
+        np.random.seed(1)
+        torch.manual_seed(1)
+        pool = gen_tracks(num_tracks=64, seed=1)
+        widths = [np.random.randint(6, 10) for _ in range(64)]
+        t = SelfPlayPPO(lambda i: MultiRacingEnv(2, 11, pool, i, widths), config, device="cuda")
+        t.opponent_pool.append(t.snapshot_agent())
+        t.update_opponent()
+        bufs = t._buffers()
+        nobs = t.envs.buf["obs"].clone()
+        nd = torch.zeros(64, device="cuda")
+        seq = []
+        for _ in range(2):
+            out = t.collect_rollout(*bufs, nobs, nd)
+            nobs, nd = out[6], out[7]
+            seq.append([x.clone() for x in out[:8]])
+            seq.append([torch.from_numpy(v) for _, v in sorted(t.envs.venv.get_state().items())])
+        outs.append(seq)
+    for ua, ub in zip(*outs):
+        for x, y in zip(ua, ub):
+            assert torch.equal(x, y)
+
+
 def test_gae_in_ppo_is_reference_formula():
     trainer, c = _train_single_style(num_envs=16, num_steps=8)
     g = torch.Generator(device="cuda").manual_seed(0)
