@@ -113,6 +113,10 @@ typedef struct {
                               64-task waves becomes ray_tail_lpr waves of 64 / ray_tail_lpr tasks.  Only
                               with 1 lane per ray elsewhere.  0 auto, -1 none, 1 .. 16 */
   int32_t ray_tail_lpr;    /* 0 auto (2), 2 or 4 */
+  /* ABI v20: the dynamics kernel re-sorts each block's ray tasks by direction every task_sort
+     launches (and after every spatial re-sort); in between the ray waves keep the previous
+     order.  0 auto (2 up to 16,384 (env, car) pairs, 1 above), 1 .. 16 */
+  int32_t task_sort;
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -180,14 +184,14 @@ int rx_sensor_angles(const rx_env* h, double* out);
  * reference has no counterpart (its SyncVectorEnv steps envs in order). */
 int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort_shift);
 
-/* Diagnostics (ABI v17, v19): the launch schedule rx_assign resolved from rx_config
+/* Diagnostics (ABI v17, v19, v20): the launch schedule rx_assign resolved from rx_config
  * for this handle, out int32 [RX_SCHEDULE_W] = split step (0/1), wide kernels
  * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
  * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
  * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
- * classes, tail lanes per ray, first tail wave (-1 = none).  Host only, no
+ * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval.  Host only, no
  * device call. */
-#define RX_SCHEDULE_W 14
+#define RX_SCHEDULE_W 15
 int rx_schedule(const rx_env* h, int32_t* out);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env

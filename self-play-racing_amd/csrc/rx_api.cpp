@@ -106,6 +106,7 @@ struct rx_env {
   int32_t argmin_window = 2;
   int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
   int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
+  int32_t task_sort = 1;                   // ray-task direction sort every task_sort dynamics launches
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -118,6 +119,10 @@ struct rx_env {
   int32_t sort_bins = 0, sort_shift = 0;
   bool sort_on = false;
   uint64_t dyn_calls = 0;
+  // ray-task direction sort (ray_order 2): every RX_TASK_SORT_INTERVAL dynamics
+  // launches, and always on the first launch after a block's membership changed
+  bool tasks_stale = true;
+  uint64_t task_calls = 0;
   // ray_order 2: direction-sorted (agent, ray) task ids, rewritten by k_dyn every step
   DevBuf<int32_t> tasks;
   // split step (k_kin1 + k_step2): cos / sin of the stepped angles; RX_SPLIT=0 disables
@@ -318,6 +323,8 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
+  if (cfg->task_sort < 0 || cfg->task_sort > 16)
+    return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
     return fail(RX_EINVAL, "n_agents = 2: dyn_lpe > 1 is a single-agent schedule, and reward_lpe is 1 or 2 "
                            "(a lane per car)");
@@ -381,7 +388,8 @@ int rx_schedule(const rx_env* h, int32_t* out) {
   const int32_t v[RX_SCHEDULE_W] = {h->split ? 1 : 0, h->dyn_lpe == 64 ? 1 : 0, h->dyn_lpe, h->ray_lpr, h->reward_lpe,
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
-                                    h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from};
+                                    h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
+                                    h->task_sort};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -495,6 +503,9 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   // ray-wave class order and the tail split (ABI v19; scheduling only)
   h->ray_dispatch = c.ray_dispatch == 0 ? RX_RAY_DISPATCH : (c.ray_dispatch < 0 ? 0 : c.ray_dispatch);
   h->ray_tail_lpr = c.ray_tail_lpr == 0 ? RX_RAY_TAIL_LPR : c.ray_tail_lpr;
+  // few (env, car) pairs: the ray waves are short and the sort is up to 40 % of
+  // k_kin's wave, so every other launch keeps the previous task order
+  h->task_sort = c.task_sort != 0 ? c.task_sort : ((long long)N * A <= RX_TASK_SORT2_PAIRS ? 2 : 1);
   h->ray_tail = c.ray_tail == 0 ? RX_RAY_TAIL : (c.ray_tail < 0 ? 0 : c.ray_tail);
   if (h->cfg.ray_order != 2 || h->ray_lpr != 1 || h->ray_dispatch == 0 || h->dyn_lpe == 64) h->ray_tail = 0;
   h->ray_tail_from = -1;
@@ -657,6 +668,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->n_dyn_waves = (int32_t)dyn.size();
   h->n_ray_waves = (int32_t)ray.size();
   h->assigned = true;
+  h->tasks_stale = true;
   h->sort_pending = false;
   h->sort_hist_done = false;  // the histogram was re-uploaded as zeros above (or sorting is off)
   if (h->bound && h->st.track) RX_HIP(hipMemcpy(h->st.track, track_of_env, N * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -830,6 +842,15 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   // working-state rows -- runs after the step's raycast (the ray tasks name
   // positions), so the new order applies from the next step.
   const bool dyn = (phases & RX_PHASE_DYNAMICS) != 0;
+  // the ray-task order only steers which rays share a wave (results never depend
+  // on it): a launch may reuse the previous one's while the blocks hold the same envs
+  if (dyn && a.tasks_out) {
+    if (h->tasks_stale || (h->task_calls % (uint64_t)h->task_sort) == 0)
+      h->tasks_stale = false;
+    else
+      a.tasks_out = nullptr;
+    ++h->task_calls;
+  }
   if (dyn && h->cfg.sort_interval > 0 && h->sort_on && (h->dyn_calls++ % h->cfg.sort_interval) == 0) {
     a.sort_keys = h->keys_in.p;
     // The histogram is zero unless sort_hist_done, when it holds the counts of
@@ -882,6 +903,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
   }
   if (h->sort_pending && (phases & RX_PHASE_RAYS)) {
     h->sort_pending = false;
+    h->tasks_stale = true;  // the re-sort moves envs between blocks
     rx_state work = h->work, tmp = h->work_tmp;
     const int hist_done = h->sort_hist_done ? 1 : 0;
     h->sort_hist_done = false;

@@ -109,6 +109,15 @@ struct rx_track_view {
 #ifndef RX_RAY_TAIL_LPR
 #define RX_RAY_TAIL_LPR 2
 #endif
+// rx_config.task_sort automatic value: the ray-task direction sort every other
+// dynamics launch up to this many (env, car) pairs, every launch above.  Same-session
+// A/B (profiles/r04/ab_task_sort.txt): 4,096 single-agent envs 129.8 / 128.9 ->
+// 132.3 / 132.7 M env-steps/s (k_kin1 6.2 -> 3.6 us), 8,192 two-car envs 135.1 / 136.7
+// -> 137.2 / 138.8 M; 65,536 envs 833 -> 804-810 M (every 4th / 8th: 761 / 715 M) and
+// 65,536 two-car envs -0.5 %: the stale order costs more ray work than the sort
+#ifndef RX_TASK_SORT2_PAIRS
+#define RX_TASK_SORT2_PAIRS 16384
+#endif
 // at most this many single-agent envs: one env per dynamics wave and one ray
 // per raycast wave (k_rays_wide), brute force over the lanes -- the kernels
 // are latency chains there, and 64 lanes shorten them
