@@ -325,6 +325,7 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
     return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
+  if (!tri(cfg->fused_act)) return fail(RX_EINVAL, "fused_act must be 0 (auto), 1 or -1 (got %d)", cfg->fused_act);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
     return fail(RX_EINVAL, "n_agents = 2: dyn_lpe > 1 is a single-agent schedule, and reward_lpe is 1 or 2 "
                            "(a lane per car)");
@@ -382,6 +383,13 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
   return RX_OK;
 }
 
+// the split step applies (k_kin + k_step2): STEP mode, next-step or no autoreset,
+// single-agent envs at one lane per env
+static bool split_step(const rx_env* h, int mode) {
+  return h->split && mode == RX_MODE_STEP && (h->cfg.n_agents == 2 || h->dyn_lpe == 1) &&
+         h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
+}
+
 int rx_schedule(const rx_env* h, int32_t* out) {
   if (!h || !out) return fail(RX_EINVAL, "rx_schedule: null argument");
   if (!h->assigned) return fail(RX_ESTATE, "rx_schedule before rx_assign");
@@ -389,7 +397,9 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort};
+                                    h->task_sort,
+                                    (split_step(h, RX_MODE_STEP) && h->cfg.n_agents == 1 && h->D == 15 &&
+                                     h->cfg.fused_act >= 0) ? 1 : 0};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -804,7 +814,10 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
 #endif
 }
 
-static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
+// act (rx_rollout_steps, split step, single agent): the step's policy runs inside
+// the k_kin launch (k_kin1_act) and writes the actions io->actions points at
+static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3,
+                  const rx_policy_io* act = nullptr) {
   if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
   if (!h) return fail(RX_EINVAL, "null handle");
   if (!io) return fail(RX_EINVAL, "io is null");
@@ -835,8 +848,9 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     a.draw_base = h->draw_base.p;
     a.reset_rank = h->draw_rank.p;
   }
-  const bool split = h->split && mode == RX_MODE_STEP && (A == 2 || h->dyn_lpe == 1) &&
-                     h->cfg.autoreset != RX_AUTORESET_SAME_STEP && h->cs_scratch.p;
+  const bool split = split_step(h, mode);
+  if (act && !(split && A == 1 && (phases & RX_PHASE_DYNAMICS)))
+    return fail(RX_EINVAL, "launch: a fused policy needs the single-agent split step");
   // Spatial re-sort, every sort_interval dynamics launches: that launch's
   // REWARD half (or k_dyn) writes the sort keys; the sort -- which moves the
   // working-state rows -- runs after the step's raycast (the ray tasks name
@@ -868,7 +882,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     if (dyn) {
       a.sort_keys = nullptr;
       prof_arm(h, a, RX_KERNEL_KIN);
-      if ((rc = rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
+      if ((rc = act ? rx_launch_kin_act(&a, act, s) : rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
         return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
       a.tasks_out = nullptr;
       a.sort_keys = keys;
@@ -1087,20 +1101,25 @@ int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t
   if (!r->params || !r->log_std || !r->eps || !r->obs || !r->actions || !r->logprobs || !r->values || !r->rewards ||
       !r->dones || !r->next_obs || !r->next_done)
     return fail(RX_EINVAL, "rx_rollout_steps: null rollout buffer");
+  if (precision != RX_PREC_FP32 && precision != RX_PREC_BF16)
+    return fail(RX_EINVAL, "rx_rollout_steps: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", precision);
   const int64_t N = h->cfg.n_envs, D = h->D;
+  // on the split step the policy runs inside the k_kin launch (k_kin1_act): two
+  // launches per step instead of three, the same arithmetic
+  const bool fuse = split_step(h, RX_MODE_STEP) && D == 15 && h->cfg.fused_act >= 0;
   for (int32_t t = 0; t < r->T; ++t) {
     const bool last = t + 1 == r->T;
     const rx_policy_io pio{r->obs_dim, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
                            r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
                            nullptr, 0};
-    int rc = rx_policy_act(&pio, stream);
-    if (rc) return rc;
+    int rc;
+    if (!fuse && (rc = rx_policy_act(&pio, stream))) return rc;
     rx_io s = *io;
     s.actions = r->actions + t * N * 2;
     s.obs = last ? r->next_obs : r->obs + (t + 1) * N * D;
     s.reward = r->rewards + t * N;
     s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;
-    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
+    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream, 3, fuse ? &pio : nullptr)) != 0) return rc;
   }
   return RX_OK;
 }
@@ -1117,32 +1136,41 @@ int rx_selfplay_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r
       !r->dones || !r->next_obs || !r->next_done || !sp->opp_params || !sp->opp_log_std || !sp->opp_eps ||
       !sp->env_actions || !sp->env_obs || !sp->env_reward || !sp->sink)
     return fail(RX_EINVAL, "rx_selfplay_rollout_steps: null buffer");
+  if (h->D != 19) return fail(RX_EINVAL, "rx_selfplay_rollout_steps: obs_dim %d (19)", h->D);
+  if ((precision != RX_PREC_FP32 && precision != RX_PREC_BF16) ||
+      (sp->opp_precision != RX_PREC_FP32 && sp->opp_precision != RX_PREC_BF16))
+    return fail(RX_EINVAL, "rx_selfplay_rollout_steps: precision %d / opponent %d", precision, sp->opp_precision);
   const int64_t N = h->cfg.n_envs, D = h->D;
   const int q = sp->agent, o = 1 - q;
+  hipStream_t hs = (hipStream_t)stream;
   for (int32_t t = 0; t < r->T; ++t) {
     const bool last = t + 1 == r->T;
-    // the frozen opponent on its rows of the env's observation buffer (wrappers.py:36-39)
+    // ONE launch for both policies (k_selfplay_act): the frozen opponent's actor on
+    // its rows of the env's observation buffer (wrappers.py:36-39), actions into its
+    // slot of the env's action buffer; the learning agent on obs[t] -- the caller's
+    // rows at t = 0 (they may predate an env rebuild), afterwards its rows of the
+    // env's buffer, which the launch also copies into obs[t] together with the
+    // agent's reward of step t - 1 -- actions into the rollout row and its env slot
     const rx_policy_io opp{(int32_t)D, N, sp->env_obs + o * D, sp->opp_eps + t * N * 2, sp->opp_params,
-                           sp->opp_log_std, sp->env_actions + 2 * o, sp->sink, sp->sink + N, 2 * D, 4,
+                           sp->opp_log_std, sp->env_actions + 2 * o, nullptr, sp->sink, 2 * D, 4,
                            sp->opp_precision, nullptr, 0};
-    int rc = rx_policy_act(&opp, stream);
-    if (rc) return rc;
-    // the learning agent on obs[t]: actions into the rollout row and the env's action slot
-    const rx_policy_io pio{(int32_t)D, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
-                           r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
-                           sp->env_actions + 2 * q, 4};
-    if ((rc = rx_policy_act(&pio, stream))) return rc;
+    const rx_policy_io pio{(int32_t)D, N, t == 0 ? r->obs : sp->env_obs + q * D, r->eps + t * N * 2, r->params,
+                           r->log_std, r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N,
+                           t == 0 ? 0 : 2 * D, 0, precision, sp->env_actions + 2 * q, 4};
+    int rc = rx_launch_selfplay_act(&pio, &opp, t == 0 ? nullptr : r->obs + t * N * D, sp->env_reward,
+                                    t == 0 ? nullptr : r->rewards + (t - 1) * N, q, hs);
+    if (rc) return fail(RX_EHIP, "self-play policy launch failed: %s", hipGetErrorString((hipError_t)rc));
     rx_io s = *io;
     s.actions = sp->env_actions;
     s.obs = sp->env_obs;
     s.reward = sp->env_reward;
     s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;  // dones['__all__'] (wrappers.py:51)
     if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
-    if ((rc = rx_launch_agent_rows((int)N, (int)D, q, sp->env_obs, sp->env_reward,
-                                   last ? r->next_obs : r->obs + (t + 1) * N * D, r->rewards + t * N,
-                                   (hipStream_t)stream)) != 0)
-      return fail(RX_EHIP, "agent-row copy launch failed: %s", hipGetErrorString((hipError_t)rc));
   }
+  // the last step's agent rows: next_obs and rewards[T - 1]
+  const int rc = rx_launch_agent_rows((int)N, (int)D, q, sp->env_obs, sp->env_reward, r->next_obs,
+                                      r->rewards + (r->T - 1) * N, hs);
+  if (rc) return fail(RX_EHIP, "agent-row copy launch failed: %s", hipGetErrorString((hipError_t)rc));
   return RX_OK;
 }
 

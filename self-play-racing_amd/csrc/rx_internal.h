@@ -184,6 +184,8 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
+// the split step's k_kin1 with the rollout policy in front (single agent, obs 15: k_kin1_act)
+extern "C" int rx_launch_kin_act(const rx_kargs* a, const rx_policy_io* pio, hipStream_t s);
 // persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024
@@ -213,6 +215,9 @@ extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, flo
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
 extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);
+// both self-play policies of a rollout step in one launch (obs_dim 19; k_selfplay_act)
+extern "C" int rx_launch_selfplay_act(const rx_policy_io* ag, const rx_policy_io* op, float* obs_out,
+                                      const float* rew_src, float* rew_out, int agent, hipStream_t s);
 extern "C" int rx_launch_adv_stats(const rx_ppo_batch* b, int n_mb, float* stats, double* moments, hipStream_t s);
 extern "C" int rx_adv_chunks(int mb);
 extern "C" int rx_launch_adv_stats_ws(const rx_ppo_batch* b, int n_mb, double* ws, float* stats, double* moments,

@@ -32,6 +32,27 @@
 #include "rx_internal.h"
 #include "rx_policy.h"
 
+// Profiling build only (-DRX_PPO_STAMPS, tools/ppo_stamps.py): per-wave
+// s_memtime stamps at k_ppo_grad's phase boundaries into a device array read
+// by rx_ppo_stamps_read (exported by that build only).  The product library has
+// no stamps.
+#ifdef RX_PPO_STAMPS
+constexpr int kStampW = 24, kStampMaxWaves = 8192;
+__device__ unsigned long long g_ppo_stamps[kStampMaxWaves * kStampW];
+#define PPO_STAMP(j)                                                                                       \
+  do {                                                                                                     \
+    const int sw_ = ((int)(blockIdx.y * gridDim.x + blockIdx.x) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6)); \
+    if ((threadIdx.x & 63) == 0 && sw_ < kStampMaxWaves && (j) < kStampW)                                \
+      g_ppo_stamps[sw_ * kStampW + (j)] = __builtin_amdgcn_s_memtime();                                   \
+  } while (0)
+#else
+#define PPO_STAMP(j) \
+  do {               \
+  } while (0)
+#endif
+
+#include "rx_policy_mfma.h"
+
 namespace {
 
 using rx_policy::kH;   // hidden width (agent/ppo.py:20-29)
@@ -62,73 +83,12 @@ constexpr int kTS = kRP + 2;  // LDS row stride of the [hidden][row] transposes 
 
 using rx_policy::Lay;
 using rx_policy::normal_logp;
-using f4 = float __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f4 mma(float a, float b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// bf16 precision (rx_ppo_batch / rx_policy_io .precision = RX_PREC_BF16,
-// config["policy_dtype"] = "bf16"): the same products on
-// v_mfma_f32_16x16x32_bf16, operands rounded to bf16, f32 accumulation.
-// Lane l holds A[row l & 15][k = 8(l >> 4) + j] and B[k][col l & 15], j < 8.
-// A k-step of 32 hidden units is ordered so that its B fragment is lane-local
-// in the transposed register layout: slot (q, j) <-> hidden unit
-// h = 32s + 16(j >> 2) + 4q + (j & 3), i.e. tile 2s + (j >> 2), register j & 3.
-using bf8 = __bf16 __attribute__((ext_vector_type(8)));
-constexpr int kF32 = RX_PREC_FP32, kBF16 = RX_PREC_BF16;
-
-__device__ __forceinline__ f4 mma16(bf8 a, bf8 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ bf8 to_bf8(float4 lo, float4 hi) {
-  bf8 v;
-  v[0] = (__bf16)lo.x, v[1] = (__bf16)lo.y, v[2] = (__bf16)lo.z, v[3] = (__bf16)lo.w;
-  v[4] = (__bf16)hi.x, v[5] = (__bf16)hi.y, v[6] = (__bf16)hi.z, v[7] = (__bf16)hi.w;
-  return v;
-}
-__device__ __forceinline__ bf8 to_bf8(const f4& lo, const f4& hi) {
-  return to_bf8(make_float4(lo[0], lo[1], lo[2], lo[3]), make_float4(hi[0], hi[1], hi[2], hi[3]));
-}
-
 // 8 consecutive floats of an LDS row (8-byte aligned) as a bf16 fragment
 __device__ __forceinline__ bf8 rows8(const float* p) {
   const float2 a = *reinterpret_cast<const float2*>(p), b = *reinterpret_cast<const float2*>(p + 2),
                c = *reinterpret_cast<const float2*>(p + 4), d = *reinterpret_cast<const float2*>(p + 6);
   return to_bf8(make_float4(a.x, a.y, b.x, b.y), make_float4(c.x, c.y, d.x, d.y));
 }
-
-template <int D>
-struct Geo {
-  static constexpr int KS1 = (D + 3) / 4;   // layer-1 k-steps: d = 4s + q, zero beyond D (15 -> 4, 19 -> 5)
-  static constexpr int DP = 4 * KS1 + 1;    // LDS row stride of W1 (odd)
-  static constexpr int NT1 = (D + 16) / 16;  // dW1 column tiles including the ones column d = D (1 / 2)
-  static constexpr int XS = 16 * NT1 + 1;   // LDS row stride of the per-wave [row][d] input tile
-  // input fragment per lane: fp32 x[s] = X[row][4s + q] (s < KS1); bf16 x[j] = X[row][8q + j] (j < 8)
-  template <int PREC>
-  static constexpr int XN = PREC == kBF16 ? 8 : KS1;
-  template <int PREC>
-  __device__ static constexpr int d_of(int s, int q) { return PREC == kBF16 ? 8 * q + s : 4 * s + q; }
-};
-
-// Profiling build only (-DRX_PPO_STAMPS, tools/ppo_stamps.py): per-wave
-// s_memtime stamps at k_ppo_grad's phase boundaries into a device array read
-// by rx_ppo_stamps_read (exported by that build only).  The product library has
-// no stamps.
-#ifdef RX_PPO_STAMPS
-constexpr int kStampW = 24, kStampMaxWaves = 8192;
-__device__ unsigned long long g_ppo_stamps[kStampMaxWaves * kStampW];
-#define PPO_STAMP(j)                                                                                       \
-  do {                                                                                                     \
-    const int sw_ = ((int)(blockIdx.y * gridDim.x + blockIdx.x) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6)); \
-    if ((threadIdx.x & 63) == 0 && sw_ < kStampMaxWaves && (j) < kStampW)                                \
-      g_ppo_stamps[sw_ * kStampW + (j)] = __builtin_amdgcn_s_memtime();                                   \
-  } while (0)
-#else
-#define PPO_STAMP(j) \
-  do {               \
-  } while (0)
-#endif
 
 struct ppo_args {
   rx_ppo_batch b;
@@ -138,22 +98,6 @@ struct ppo_args {
   double* kl_partial;   // [n_wg]
 };
 
-// Weights of one trunk, read either from the flat parameter buffer (global,
-// L2-resident) or from the workgroup's LDS copy (same element order, padded
-// row strides).  o = output unit, i / d = input unit.
-struct WGlobal {
-  const float* __restrict__ W1;  // [64][D]
-  const float* __restrict__ b1;
-  const float* __restrict__ W2;  // [64][64]
-  const float* __restrict__ b2;
-  const float* __restrict__ W3;  // [n_out][64]
-  const float* __restrict__ b3;
-  int D;
-  __device__ float w1(int o, int d) const { return d < D ? W1[o * D + d] : 0.0f; }
-  __device__ float4 w2row4(int o, int i0) const { return *reinterpret_cast<const float4*>(W2 + o * kH + i0); }
-  __device__ float w2(int o, int i) const { return W2[o * kH + i]; }
-  __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
-};
 struct WLds {
   const float* W1;  // [64][DP], zero beyond D
   const float* b1;
@@ -168,142 +112,46 @@ struct WLds {
   __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
 };
 
-// Forward of one trunk for the wave's 16 rows: x = the lane's input fragment
-// (Geo::d_of).  H1 / H2 tiles in the transposed register layout; y = head
-// pre-activations: lane (q = 0, l15) holds output j in y[j].
-template <int D, int NOUT, int PREC, class Wt>
-__device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>::template XN<PREC>], f4 (&H1)[4],
-                                            f4 (&H2)[4], f4& y, int l15, int q, int stamp = -1) {
-  constexpr int KS1 = Geo<D>::KS1;
-  const int j3 = l15 < NOUT ? l15 : 0;
-  const float on = l15 < NOUT ? 1.0f : 0.0f;
-  if constexpr (PREC == kBF16) {
-    const bf8 bx = to_bf8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]));
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {  // layer 1: one k-step (d = 8q + j < 32)
-      const int o = 16 * mt + l15;
-      const float4 lo = make_float4(w.w1(o, 8 * q), w.w1(o, 8 * q + 1), w.w1(o, 8 * q + 2), w.w1(o, 8 * q + 3));
-      const float4 hi = make_float4(w.w1(o, 8 * q + 4), w.w1(o, 8 * q + 5), w.w1(o, 8 * q + 6), w.w1(o, 8 * q + 7));
-      const f4 z = mma16(to_bf8(lo, hi), bx, f4{0.0f, 0.0f, 0.0f, 0.0f});
-#pragma unroll
-      for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
-    }
-    const bf8 bh[2] = {to_bf8(H1[0], H1[1]), to_bf8(H1[2], H1[3])};
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        z = mma16(to_bf8(w.w2row4(16 * mt + l15, 32 * s + 4 * q), w.w2row4(16 * mt + l15, 32 * s + 16 + 4 * q)),
-                  bh[s], z);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
-    }
-    y = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float v[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = on * w.w3(j3, 32 * s + 16 * (jj >> 2) + 4 * q + (jj & 3));
-      y = mma16(to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7])),
-                to_bf8(H2[2 * s], H2[2 * s + 1]), y);
-    }
-  } else {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < KS1; ++s) z = mma(w.w1(16 * mt + l15, 4 * s + q), x[s], z);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + w.b1[16 * mt + 4 * q + r]);
-    }
-    if (stamp >= 0) PPO_STAMP(stamp);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float4 a = w.w2row4(16 * mt + l15, 16 * t + 4 * q);
-        z = mma(a.x, H1[t][0], z);
-        z = mma(a.y, H1[t][1], z);
-        z = mma(a.z, H1[t][2], z);
-        z = mma(a.w, H1[t][3], z);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + w.b2[16 * mt + 4 * q + r]);
-    }
-    if (stamp >= 0) PPO_STAMP(stamp + 1);
-    // head on the VALU (NOUT <= 2 of an MFMA tile's 16 output rows would be
-    // used): lane (q, l15) sums its own hidden units h = 16t + 4q + r in the
-    // order t, r, then the 4 q-lanes of the row combine as (p0 + p1) + (p2 + p3)
-    // (xor 16, then xor 32; k_rollout repeats this order).  Every lane of the
-    // row ends with output j in y[j].
-    y = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < NOUT; ++j) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc = fmaf(w.w3(j, 16 * t + 4 * q + r), H2[t][r], acc);
-      acc += __shfl_xor(acc, 16, 64);
-      acc += __shfl_xor(acc, 32, 64);
-      y[j] = acc;
-    }
-    (void)j3;
-    (void)on;
-  }
-}
-
-// Rollout policy step (agent/ppo.py:105-110, get_action_and_value on obs[t]):
-// per row  action = clamp(eps * std + mu, -1, 1)   (Normal.sample() = normal_() * std + mu)
-//          logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs).
-// eps [N][2] is drawn by the caller with torch's normal_() so the sampling
-// stream is torch's.  Wave = 16 rows of one trunk, weights straight from the
-// (L2-resident) parameter buffer.
 template <int D, int PREC>
 __global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P) {
-  using L = Lay<D>;
-  constexpr int XN = Geo<D>::template XN<PREC>;
-  const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   // a workgroup's 4 waves run ONE trunk (even workgroups actor, odd critic) on
   // 4 consecutive 16-row blocks, so a CU's L1 holds one trunk's 21 KB of weights
   const bool critic = blockIdx.x & 1;
   const int64_t rb = (int64_t)(blockIdx.x >> 1) * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t row = rb * 16 + l15;
-  if (rb * 16 >= io.n) return;
-  const bool live = row < io.n;
-  const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
-  float x[XN];
-#pragma unroll
-  for (int s = 0; s < XN; ++s) {
-    const int d = Geo<D>::template d_of<PREC>(s, q);
-    x[s] = (live && d < D) ? io.obs[row * os + d] : 0.0f;
+  policy_rows<D, PREC>(io, P, critic, rb);
+}
+
+// One self-play rollout step's policies in ONE launch (rx_selfplay_rollout_steps):
+// workgroup kind b % 3 = the learning agent's actor, its critic, the frozen
+// opponent's actor (its log-prob and value are never read, so it has no critic
+// workgroups) -- each exactly k_policy_act's rows.  The agent's critic
+// workgroups also copy the agent's observation rows they read into the
+// rollout's obs[t] and the previous step's agent reward into rewards[t - 1]
+// (what k_agent_rows did after each step), when copy.obs_out is set.
+struct selfplay_copy {
+  float* obs_out;        // [N][D] rollout rows, or nullptr
+  const float* rew_src;  // the env's [N][2] rewards
+  float* rew_out;        // [N]
+  int32_t agent;
+};
+template <int D, int PA, int PO>
+__global__ __launch_bounds__(kT) void k_selfplay_act(rx_policy_io ag, rx_policy_io op, selfplay_copy cp) {
+  const int kind = (int)blockIdx.x % 3;
+  const int64_t rb = (int64_t)(blockIdx.x / 3) * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (kind == 2) {
+    policy_rows<D, PO>(op, op.params, false, rb);
+    return;
   }
-  f4 H1[4], H2[4], y;
-  if (!critic) {
-    const WGlobal w{P + L::aW1, P + L::ab1, P + L::aW2, P + L::ab2, P + L::aW3, P + L::ab3, D};
-    mlp_forward<D, kNA, PREC>(w, x, H1, H2, y, l15, q);
-    if (q != 0 || !live) return;
-    float logp = 0.0f;
-#pragma unroll
-    for (int j = 0; j < kNA; ++j) {
-      const float mu = rx_policy::tanh_fast(y[j] + P[L::ab3 + j]);
-      const float scale = expf(io.log_std[j]);
-      const float var = scale * scale;
-      const float smp = io.eps[row * kNA + j] * scale + mu;  // mul_(std).add_(mu): two roundings
-      const float a = fminf(fmaxf(smp, -1.0f), 1.0f);
-      io.actions[row * as + j] = a;
-      if (io.actions2) io.actions2[row * (io.act2_stride > 0 ? io.act2_stride : kNA) + j] = a;
-      logp += normal_logp(a - mu, var, logf(scale));
-    }
-    io.logprobs[row] = logp;
-  } else {
-    const WGlobal w{P + L::cW1, P + L::cb1, P + L::cW2, P + L::cb2, P + L::cW3, P + L::cb3, D};
-    mlp_forward<D, 1, PREC>(w, x, H1, H2, y, l15, q);
-    if (q != 0 || !live) return;
-    io.values[row] = y[0] + P[L::cb3];
+  policy_rows<D, PA>(ag, ag.params, kind == 1, rb);
+  if (kind != 1 || !cp.obs_out || rb * 16 >= ag.n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t os = ag.obs_stride > 0 ? ag.obs_stride : D;
+  const int64_t r0 = rb * 16, nr = min((int64_t)16, ag.n - r0);
+  for (int i = lane; i < nr * D; i += 64) {
+    const int64_t r = r0 + i / D;
+    cp.obs_out[r * D + i % D] = ag.obs[r * os + i % D];
   }
+  if (lane < nr) cp.rew_out[r0 + lane] = cp.rew_src[(r0 + lane) * 2 + cp.agent];
 }
 
 // LDS words of k_ppo_grad's workgroup
@@ -1076,6 +924,23 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
   }
   hipLaunchKernelGGL(k_ppo_reduce, dim3(rx_ppo_reduce_blocks(b->obs_dim)), dim3(1024), 0, s, partial, klp, n_wg, P, Pp,
                      b->mb, b->kl_target, scale, grad, stop, kl_at_stop, kl_out, np, na);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_launch_selfplay_act(const rx_policy_io* ag, const rx_policy_io* op, float* obs_out,
+                                      const float* rew_src, float* rew_out, int agent, hipStream_t s) {
+  const int64_t blocks16 = (ag->n + 15) / 16;
+  const int n_wg = (int)(3 * ((blocks16 + 3) / 4));
+  const selfplay_copy cp{obs_out, rew_src, rew_out, agent};
+  const bool ba = ag->precision == kBF16, bo = op->precision == kBF16;
+  if (ba && bo)
+    hipLaunchKernelGGL((k_selfplay_act<19, kBF16, kBF16>), dim3(n_wg), dim3(kT), 0, s, *ag, *op, cp);
+  else if (ba)
+    hipLaunchKernelGGL((k_selfplay_act<19, kBF16, kF32>), dim3(n_wg), dim3(kT), 0, s, *ag, *op, cp);
+  else if (bo)
+    hipLaunchKernelGGL((k_selfplay_act<19, kF32, kBF16>), dim3(n_wg), dim3(kT), 0, s, *ag, *op, cp);
+  else
+    hipLaunchKernelGGL((k_selfplay_act<19, kF32, kF32>), dim3(n_wg), dim3(kT), 0, s, *ag, *op, cp);
   return (int)hipGetLastError();
 }
 
