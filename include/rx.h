@@ -117,9 +117,6 @@ typedef struct {
      launches (and after every spatial re-sort); in between the ray waves keep the previous
      order.  0 auto (2 up to 16,384 (env, car) pairs, 1 above), 1 .. 16 */
   int32_t task_sort;
-  /* ABI v20: rx_rollout_steps on the split step runs each step's policy inside the k_kin launch
-     (k_kin1_act: two launches per step instead of three).  0 auto (on), 1 on, -1 off */
-  int32_t fused_act;
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -192,10 +189,9 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
  * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
  * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
  * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
- * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval, policy
- * fused into k_kin by rx_rollout_steps (0/1).  Host only, no
+ * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval.  Host only, no
  * device call. */
-#define RX_SCHEDULE_W 16
+#define RX_SCHEDULE_W 15
 int rx_schedule(const rx_env* h, int32_t* out);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env

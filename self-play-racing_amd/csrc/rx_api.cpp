@@ -325,7 +325,6 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
     return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
-  if (!tri(cfg->fused_act)) return fail(RX_EINVAL, "fused_act must be 0 (auto), 1 or -1 (got %d)", cfg->fused_act);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
     return fail(RX_EINVAL, "n_agents = 2: dyn_lpe > 1 is a single-agent schedule, and reward_lpe is 1 or 2 "
                            "(a lane per car)");
@@ -397,9 +396,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort,
-                                    (split_step(h, RX_MODE_STEP) && h->cfg.n_agents == 1 && h->D == 15 &&
-                                     h->cfg.fused_act >= 0) ? 1 : 0};
+                                    h->task_sort};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -814,10 +811,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
 #endif
 }
 
-// act (rx_rollout_steps, split step, single agent): the step's policy runs inside
-// the k_kin launch (k_kin1_act) and writes the actions io->actions points at
-static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3,
-                  const rx_policy_io* act = nullptr) {
+static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, void* stream, int phases = 3) {
   if (phases < 1 || phases > 3) return fail(RX_EINVAL, "phases must be 1, 2 or 3 (got %d)", phases);
   if (!h) return fail(RX_EINVAL, "null handle");
   if (!io) return fail(RX_EINVAL, "io is null");
@@ -849,8 +843,6 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     a.reset_rank = h->draw_rank.p;
   }
   const bool split = split_step(h, mode);
-  if (act && !(split && A == 1 && (phases & RX_PHASE_DYNAMICS)))
-    return fail(RX_EINVAL, "launch: a fused policy needs the single-agent split step");
   // Spatial re-sort, every sort_interval dynamics launches: that launch's
   // REWARD half (or k_dyn) writes the sort keys; the sort -- which moves the
   // working-state rows -- runs after the step's raycast (the ray tasks name
@@ -882,7 +874,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     if (dyn) {
       a.sort_keys = nullptr;
       prof_arm(h, a, RX_KERNEL_KIN);
-      if ((rc = act ? rx_launch_kin_act(&a, act, s) : rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
+      if ((rc = rx_launch_split(&a, A, RX_SPLIT_KIN, s)) != 0)
         return fail(RX_EHIP, "k_kin1 launch failed: %s", hipGetErrorString((hipError_t)rc));
       a.tasks_out = nullptr;
       a.sort_keys = keys;
@@ -1104,22 +1096,19 @@ int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t
   if (precision != RX_PREC_FP32 && precision != RX_PREC_BF16)
     return fail(RX_EINVAL, "rx_rollout_steps: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", precision);
   const int64_t N = h->cfg.n_envs, D = h->D;
-  // on the split step the policy runs inside the k_kin launch (k_kin1_act): two
-  // launches per step instead of three, the same arithmetic
-  const bool fuse = split_step(h, RX_MODE_STEP) && D == 15 && h->cfg.fused_act >= 0;
   for (int32_t t = 0; t < r->T; ++t) {
     const bool last = t + 1 == r->T;
     const rx_policy_io pio{r->obs_dim, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
                            r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
                            nullptr, 0};
-    int rc;
-    if (!fuse && (rc = rx_policy_act(&pio, stream))) return rc;
+    int rc = rx_policy_act(&pio, stream);
+    if (rc) return rc;
     rx_io s = *io;
     s.actions = r->actions + t * N * 2;
     s.obs = last ? r->next_obs : r->obs + (t + 1) * N * D;
     s.reward = r->rewards + t * N;
     s.done_f32 = last ? r->next_done : r->dones + (t + 1) * N;
-    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream, 3, fuse ? &pio : nullptr)) != 0) return rc;
+    if ((rc = launch(h, &s, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
   }
   return RX_OK;
 }

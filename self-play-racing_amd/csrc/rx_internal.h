@@ -184,8 +184,6 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
-// the split step's k_kin1 with the rollout policy in front (single agent, obs 15: k_kin1_act)
-extern "C" int rx_launch_kin_act(const rx_kargs* a, const rx_policy_io* pio, hipStream_t s);
 // persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024

@@ -28,7 +28,6 @@
 #include "rx_internal.h"
 #include "rx_math.h"
 #include "rx_policy.h"
-#include "rx_policy_mfma.h"
 
 #define RX_TWO_PI 6.283185307179586  // 2*np.pi, environment/car.py:54
 #define RX_MAX_SPEED 30.0
@@ -890,38 +889,6 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const unsigned long long t7 = __builtin_amdgcn_s_memtime();
   if (a.io.counters && (threadIdx.x & 63) == 0) a.io.counters[16 + 12 * wave + 9] = t7;
 #endif
-}
-
-// k_kin1 with the rollout step's policy in front (rx_rollout_steps, single agent,
-// split step): a workgroup of 8 waves per 64-env block.  Waves 0-3 run the actor
-// and waves 4-7 the critic on 16 of the block's envs each -- k_policy_act's
-// per-row arithmetic (policy_rows), reading obs[t] and eps[t] and writing
-// actions[t], logprobs[t], values[t] at the env's row -- then, after the
-// workgroup barrier, wave 0 steps the block exactly as k_kin1 does, reading the
-// actions just written.  One launch and one dependent chain fewer per step.
-template <int D, int PREC>
-__global__ __launch_bounds__(512) void k_kin1_act(rx_kargs a, rx_policy_io pio) {
-  const int blk = uniform((int)blockIdx.x);
-  if (blk >= a.n_dyn_waves) return;
-  const int w = uniform((int)(threadIdx.x >> 6));
-  {
-    const rx_wave we = a.dyn_waves[blk];
-    const int r0 = 16 * (w & 3);
-    policy_rows<D, PREC>(pio, pio.params, w >= 4, 0, a.perm + uniform(we.perm_start) + r0,
-                         min(16, uniform(we.count) - r0));
-  }
-  __shared__ int32_t tcnt[kTaskSectors];
-  __shared__ int32_t tstage[64 * 16];
-  __syncthreads();  // the block's actions are in actions[t] (workgroup scope: same CU)
-  if (w != 0) return;
-  const bool sorting = a.tasks_out != nullptr;
-  if (sorting) tcnt[threadIdx.x & 63] = 0;
-  const unsigned long long prof_t0 = prof_start(a);
-  double ang[1], ep[3] = {0.0, 0.0, 0.0};
-  int e = -1;
-  dyn1_env<1, RX_PART_KIN>(a, blk, ang, e, ep);
-  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[blk].perm_start), e, ang, tcnt, tstage);
-  prof_end(a, blk, prof_t0);
 }
 
 // ============================================================ k_dyn, A == 2
@@ -2393,14 +2360,6 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
     launch_step2_lpr<1, 2>(a, grid, n_rw, s);
   else
     launch_step2_lpr<1, 1>(a, grid, n_rw, s);
-  return (int)hipGetLastError();
-}
-
-extern "C" int rx_launch_kin_act(const rx_kargs* a, const rx_policy_io* pio, hipStream_t s) {
-  if (pio->precision == RX_PREC_BF16)
-    hipLaunchKernelGGL((k_kin1_act<15, RX_PREC_BF16>), dim3(a->n_dyn_waves), dim3(512), 0, s, *a, *pio);
-  else
-    hipLaunchKernelGGL((k_kin1_act<15, RX_PREC_FP32>), dim3(a->n_dyn_waves), dim3(512), 0, s, *a, *pio);
   return (int)hipGetLastError();
 }
 

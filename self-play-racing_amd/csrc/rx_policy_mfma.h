@@ -1,7 +1,6 @@
 // The actor-critic MLP forward on the matrix cores, shared by the policy
-// launches of rx_ppo.hip (k_policy_act, k_selfplay_act, k_ppo_grad's forward)
-// and the rollout kernels of rx_kernels.hip (k_kin1_act), so every launch that
-// evaluates the policy does exactly the same arithmetic (DESIGN.md §3:
+// launches of rx_ppo.hip (k_policy_act, k_selfplay_act, k_ppo_grad's forward),
+// so every launch that evaluates the policy does exactly the same arithmetic (DESIGN.md §3:
 // v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain; the layouts below fix
 // every summation order).  agent/ppo.py:11-62, :105-110.
 #pragma once
@@ -175,15 +174,13 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
 // (L2-resident) parameter buffer.
 template <int D, int PREC>
 __device__ __forceinline__ void policy_rows(const rx_policy_io& io, const float* __restrict__ P, bool critic,
-                                            int64_t rb, const int32_t* rowmap = nullptr, int nmap = 0) {
+                                            int64_t rb) {
   using L = Lay<D>;
   constexpr int XN = Geo<D>::template XN<PREC>;
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
-  // rows rb*16 + l15, or (rowmap) the wave's nmap rows rowmap[l15]: the same
-  // per-row arithmetic whichever rows share the wave (an MFMA column is one row)
-  if (rowmap ? nmap <= 0 : rb * 16 >= io.n) return;
-  const bool live = rowmap ? l15 < nmap : rb * 16 + l15 < io.n;
-  const int64_t row = rowmap ? (live ? (int64_t)rowmap[l15] : 0) : rb * 16 + l15;
+  const int64_t row = rb * 16 + l15;
+  if (rb * 16 >= io.n) return;
+  const bool live = row < io.n;
   const int64_t os = io.obs_stride > 0 ? io.obs_stride : D, as = io.act_stride > 0 ? io.act_stride : kNA;
   float x[XN];
 #pragma unroll

@@ -48,17 +48,16 @@ class RxConfig(ctypes.Structure):
                 ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)] + \
                [(k, ctypes.c_int32) for k in ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window",
                                                "seg_filter", "box_quadrants", "ray_dispatch", "ray_tail",
-                                               "ray_tail_lpr", "task_sort", "fused_act")]
+                                               "ray_tail_lpr", "task_sort")]
 
 
 # rx_config launch-schedule fields (ABI v17, v19, v20): 0 = auto, -1 = off / none (include/rx.h).
 # Scheduling only: every value gives bit-identical results.
-SCHEDULE_W = 16  # rx_schedule: resolved schedule (include/rx.h)
+SCHEDULE_W = 15  # rx_schedule: resolved schedule (include/rx.h)
 SCHEDULE_KEYS = ("split", "wide", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                 "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort",
-                 "fused_act")
+                 "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort")
 SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "fused_act")
+                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort")
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
