@@ -1839,8 +1839,20 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
 // dispatch tail (rx_config.ray_tail: the waves at and after a.ray_tail_from,
 // 64 / ray_tail_lpr tasks each, rx_assign) -- at ray_tail_lpr lanes per ray.
 // Only one-lane-per-ray schedules have a tail.
+// RX_RAY_PRIO (A/B build): the ray waves dispatched in the last
+// (100 - RX_RAY_PRIO_FROM) % of the table (the centre classes, whose chains end
+// the launch) take issue priority RX_RAY_PRIO over the waves sharing their SIMD
+#ifndef RX_RAY_PRIO
+#define RX_RAY_PRIO 0
+#endif
+#ifndef RX_RAY_PRIO_FROM
+#define RX_RAY_PRIO_FROM 70
+#endif
 template <int A, int LPR>
 __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
+#if RX_RAY_PRIO > 0
+  if (wave * 100 >= a.n_ray_waves * RX_RAY_PRIO_FROM) __builtin_amdgcn_s_setprio(RX_RAY_PRIO);
+#endif
   if constexpr (LPR == 1) {
     if (a.ray_tail_from >= 0 && wave >= a.ray_tail_from) {
       if (a.ray_tail_lpr == 4)

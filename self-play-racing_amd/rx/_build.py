@@ -18,7 +18,7 @@ INCLUDE = os.path.join(REPO, "include")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "librx.so")
 SOURCES = ["rx_kernels.hip", "rx_sort.hip", "rx_optim.hip", "rx_ppo.hip", "rx_api.cpp"]
-HEADERS = ["rx_internal.h", "rx_math.h", "rx_sincos_table.h", "rx_policy.h"]
+HEADERS = ["rx_internal.h", "rx_math.h", "rx_sincos_table.h", "rx_policy.h", "rx_policy_mfma.h"]
 
 ARCH = os.environ.get("RX_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no implicit FMA anywhere (bit-exact with the reference's
