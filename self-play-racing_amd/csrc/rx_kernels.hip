@@ -1839,20 +1839,24 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
 // dispatch tail (rx_config.ray_tail: the waves at and after a.ray_tail_from,
 // 64 / ray_tail_lpr tasks each, rx_assign) -- at ray_tail_lpr lanes per ray.
 // Only one-lane-per-ray schedules have a tail.
-// RX_RAY_PRIO (A/B build): the ray waves dispatched in the last
-// (100 - RX_RAY_PRIO_FROM) % of the table (the centre classes, whose chains end
-// the launch) take issue priority RX_RAY_PRIO over the waves sharing their SIMD
+// Single-agent envs: the ray waves dispatched in the last (100 - RX_RAY_PRIO_FROM) %
+// of the table (the centre classes, whose chains end the launch) take issue
+// priority RX_RAY_PRIO over the waves sharing their SIMD.  Scheduling only.
+// Same-session A/B (profiles/r04/ab_ray_prio_{1,2}.txt, ab_ray_prio_sizes.txt):
+// 65,536 envs 827.6-830.0 -> 837.4-844.7 M env-steps/s (k_step2 67.5 -> 65.3-66.7 us),
+// 4,096 envs +2.8 %, 16,384 +2 %; from 50 / 60 % of the table -5 / -4 %, priority 2-3
+// no better than 1; two-car envs -5.5 % at 8,192 (off there)
 #ifndef RX_RAY_PRIO
-#define RX_RAY_PRIO 0
+#define RX_RAY_PRIO 1
 #endif
 #ifndef RX_RAY_PRIO_FROM
 #define RX_RAY_PRIO_FROM 70
 #endif
 template <int A, int LPR>
 __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
-#if RX_RAY_PRIO > 0
-  if (wave * 100 >= a.n_ray_waves * RX_RAY_PRIO_FROM) __builtin_amdgcn_s_setprio(RX_RAY_PRIO);
-#endif
+  if constexpr (A == 1 && RX_RAY_PRIO > 0) {
+    if (wave * 100 >= a.n_ray_waves * RX_RAY_PRIO_FROM) __builtin_amdgcn_s_setprio(RX_RAY_PRIO);
+  }
   if constexpr (LPR == 1) {
     if (a.ray_tail_from >= 0 && wave >= a.ray_tail_from) {
       if (a.ray_tail_lpr == 4)
