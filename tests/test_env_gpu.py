@@ -453,6 +453,34 @@ def test_ray_tail_split_is_exact(rx, golden, n_agents, N, tail, tail_lpr, dispat
     vb.close()
 
 
+@pytest.mark.parametrize("n_agents,N,interval", [(1, 4100, 7), (1, 8256, 16), (2, 3000, 3)])
+def test_task_sort_interval_is_exact(rx, golden, n_agents, N, interval):
+    """rx_config.task_sort (ABI v20): the ray-task direction sort every `interval`
+    dynamics launches (in between the ray waves reuse the previous order; every
+    spatial re-sort forces a new one) against a sort every launch: obs, rewards,
+    dones and the state bit-identical over 300 steps of random play with
+    autoresets, single-agent and two-car."""
+    tracks = np.arange(N) % golden.n_tracks
+    va = _venv(rx, golden, tracks, n_agents=n_agents, seed=6, autoreset="next_step", sched=dict(task_sort=1))
+    vb = _venv(rx, golden, tracks, n_agents=n_agents, seed=6, autoreset="next_step", sched=dict(task_sort=interval))
+    assert va.schedule()["task_sort"] == 1 and vb.schedule()["task_sort"] == interval
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(21)
+    shape = (N, 2) if n_agents == 1 else (N, 2, 2)
+    for t in range(300):
+        a = torch.rand(shape, device="cuda", generator=g) * 2 - 1
+        if n_agents == 1:
+            a[:, 1].abs_()
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    sa, sb = va.get_state(), vb.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    va.close()
+    vb.close()
+
+
 @pytest.mark.parametrize("lpe", [2, 4])
 @pytest.mark.parametrize("N", [4100, 8256])
 def test_reward_lanes_per_env_are_exact(rx, golden, N, lpe):
