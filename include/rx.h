@@ -97,8 +97,10 @@ typedef struct {
   int32_t wide_n;          /* wide kernels (a wave per env / per ray) up to this many single-agent envs:
                               0 auto (2,048), -1 never, > 0 the threshold */
   int32_t dyn_lpe;         /* k_dyn1 lanes per env: 0 auto, or 1, 2, 4, 64 */
-  int32_t ray_lpr;         /* lanes per ray task (ray_order 2): 0 auto (4 / 2 / 1 by env count), or 1, 2, 4 */
-  int32_t reward_lpe;      /* k_step2 REWARD lanes per env (single agent): 0 auto (2 up to 4,096 envs), or 1, 2, 4 */
+  int32_t ray_lpr;         /* lanes per ray task (ray_order 2): 0 auto (4 / 2 / 1 by (env, car) pairs; two cars:
+                              4 / 1), or 1, 2, 4 */
+  int32_t reward_lpe;      /* k_step2 REWARD lanes per env: 0 auto (single agent: 2 up to 4,096 envs; two cars:
+                              2 = a lane per car up to 16,384 envs), or 1, 2, 4 (two cars: 1 or 2) */
   int32_t argmin_window;   /* closest-waypoint scan half-width around the previous one: 0 auto (2), -1 none,
                               1 .. 32 */
   int32_t seg_filter;      /* float32 pre-filter before each exact segment test: 0 auto (on), 1 on, -1 off */
