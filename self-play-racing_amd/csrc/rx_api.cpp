@@ -112,6 +112,7 @@ struct rx_env {
   std::vector<double> rel_angles_h;
   // spatial sort (scheduling only)
   DevBuf<uint32_t> keys_in;              // [N] bin per perm position (REWARD half)
+  DevBuf<uint32_t> keys_off;             // [N] the position's rank within its bin (the count's atomic)
   bool sort_pending = false;             // keys written, the re-sort runs after this step's raycast
   bool sort_hist_done = false;           // the REWARD half of the keys' launch also counted the bins
   DevBuf<uint32_t> sort_hist, sort_cursor;  // [sort_bins]
@@ -424,6 +425,7 @@ int rx_destroy(rx_env* h) {
   for (void* m : h->work_mem) (void)hipFree(m);
   h->work_mem.clear();
   h->keys_in.release();
+  h->keys_off.release();
   h->sort_hist.release();
   h->sort_cursor.release();
   h->sort_base.release();
@@ -652,6 +654,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       std::vector<uint32_t> zk(std::max<size_t>((size_t)N, (size_t)total), 0u);
       if ((rc = upload(h->sort_base, base.data(), base.size()))) return rc;
       if ((rc = upload(h->keys_in, zk.data(), (size_t)N))) return rc;
+      if ((rc = upload(h->keys_off, zk.data(), (size_t)N))) return rc;
       if ((rc = upload(h->sort_hist, zk.data(), (size_t)total))) return rc;
       if ((rc = upload(h->sort_cursor, zk.data(), (size_t)total))) return rc;
       h->sort_bins = (int32_t)total;
@@ -882,6 +885,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
       // launch fewer per re-sort: rx_sort_envs skips k_sort_hist)
       if (keys && A == 1) {
         a.sort_hist = h->sort_hist.p;
+        a.sort_off = h->keys_off.p;
         h->sort_hist_done = true;
       }
       prof_arm(h, a, phases == 3 ? RX_KERNEL_STEP2 : RX_KERNEL_REWARD);
@@ -913,7 +917,7 @@ static int launch(rx_env* h, const rx_io* io, int mode, const uint8_t* mask, voi
     rx_state work = h->work, tmp = h->work_tmp;
     const int hist_done = h->sort_hist_done ? 1 : 0;
     h->sort_hist_done = false;
-    if ((rc = rx_sort_envs(h->keys_in.p, h->cfg.n_envs, A, h->sort_hist.p, h->sort_cursor.p, h->sort_bins,
+    if ((rc = rx_sort_envs(h->keys_in.p, h->keys_off.p, h->cfg.n_envs, A, h->sort_hist.p, h->sort_cursor.p, h->sort_bins,
                            h->perm[0].p, h->perm[1].p, &work, &tmp, s, hist_done)) != 0)
       return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
   }

@@ -135,6 +135,7 @@ struct rx_kargs {
   const uint8_t* reset_mask;  // RX_MODE_RESET: [N] or nullptr (= all)
   uint32_t* sort_keys;        // [N] k_dyn writes the sort bin (sort_base[slot] + (waypoint >> sort_shift)) at its perm position, or nullptr
   uint32_t* sort_hist;        // with sort_keys: the REWARD half also counts the bins (the re-sort then skips k_sort_hist), or nullptr
+  uint32_t* sort_off;         // with sort_hist: [N] the position's rank within its bin (the count atomic's return + lane rank)
   const int32_t* sort_base;   // [n_tracks] first sort bin of each slot (ascending with the slot id)
   int32_t sort_shift;         // waypoints per sort bin = 1 << sort_shift
   // ray_order 2: k_dyn writes the direction-sorted (agent, ray) task ids of
@@ -208,6 +209,32 @@ __device__ __forceinline__ void rx_adam_scalars(const rx_adam_config& cfg, float
   out[0] = (float)(-(lr / (1.0 - pow(cfg.beta1, s))));
   out[1] = (float)sqrt(1.0 - pow(cfg.beta2, s));
 }
+// The re-sort's bin count for the wave's calling lanes (one per env, key =
+// its bin): lanes grouped by bin (ballot), then ONE vector atomic in which
+// every group leader adds its group size to hist[bin]; the returned old count
+// plus the lane's rank inside its group is the env's rank within its bin --
+// the scatter's offset, so k_sort_scatter needs no atomics of its own.
+__device__ __forceinline__ uint32_t rx_bin_count(uint32_t* hist, uint32_t key) {
+  const int lane = (int)(threadIdx.x & 63);
+  unsigned long long pending = __ballot(1);
+  uint32_t cnt = 0, rank = 0;
+  int leader_of_mine = lane;
+  while (pending) {  // wave-uniform: one iteration per distinct bin of the wave
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
+    const unsigned long long m = __ballot(key == lb);
+    if (key == lb) {
+      leader_of_mine = leader;
+      rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    if (lane == leader) cnt = (uint32_t)__builtin_popcountll(m);
+    pending &= ~m;
+  }
+  uint32_t old = 0;
+  if (cnt) old = atomicAdd(&hist[key], cnt);
+  old = (uint32_t)__builtin_amdgcn_ds_bpermute(leader_of_mine << 2, (int)old);
+  return old + rank;
+}
 extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                               const double* lr, const uint8_t* stop, float* ws, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
@@ -234,7 +261,7 @@ extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* 
 #define RX_SORT_MAX_BINS 65536
 // and moves the working state rows with their envs (perm, work -> perm_tmp,
 // tmp -> back); rx_state_sync: working copy <-> the caller's arrays
-extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
+extern "C" int rx_sort_envs(const uint32_t* keys, uint32_t* off, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
                             int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
                             hipStream_t s, int hist_done = 0);
 extern "C" int rx_launch_permutation(int64_t n, uint64_t seed, int64_t* out, hipStream_t s);

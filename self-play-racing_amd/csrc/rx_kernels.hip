@@ -399,16 +399,8 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
   w = w < 0 ? 0 : (w > W ? W : w);
   const uint32_t key = (uint32_t)(a.sort_base[k] + (w >> a.sort_shift));
   a.sort_keys[pos] = key;
-  if (a.sort_hist) {  // the re-sort's histogram (k_sort_hist's grouping): one atomic per distinct bin of the wave
-    unsigned long long pending = __ballot(1);  // the wave's lanes that reached here (one per env)
-    while (pending) {
-      const int leader = __builtin_ctzll(pending);
-      const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
-      const unsigned long long m = __ballot(key == lb);
-      if ((int)(threadIdx.x & 63) == leader) atomicAdd(&a.sort_hist[lb], (uint32_t)__builtin_popcountll(m));
-      pending &= ~m;
-    }
-  }
+  if (a.sort_hist)  // the re-sort's histogram and each env's rank in its bin (k_sort_hist's work)
+    a.sort_off[pos] = rx_bin_count(a.sort_hist, key);
 }
 
 // ray_order 2: the (agent, ray) tasks of a dynamics wave's envs (64 track

@@ -9,17 +9,19 @@
 // of one slot are contiguous, slot groups keep their place in the perm, and
 // the whole key space is <= RX_SORT_MAX_BINS (rx_assign picks the shift).  A
 // counting sort over that small key space, four launches:
-//   k_sort_hist     per wave: lanes grouped by bin (ballot), one atomic per group
+//   k_sort_hist     per wave: lanes grouped by bin (ballot), the group leaders'
+//                   counts added in one vector atomic whose return values give
+//                   every env its rank within its bin (rx_bin_count; the
+//                   single-agent split step's REWARD half does this itself)
 //   k_sort_scan     one workgroup: exclusive scan of the histogram -> cursors,
 //                   histogram cleared for the next sort
-//   k_sort_scatter  per wave: the same grouping, one cursor atomic per group,
-//                   lane rank within its group -> new position; the env id and
-//                   its whole state row move there (into the shadow copy)
+//   k_sort_scatter  new position = cursor[bin] + rank (no atomics); the env id
+//                   and its whole state row move there (into the shadow copy)
 //   k_state_copy    shadow -> working copy (coalesced), so every launch keeps
 //                   reading the same buffers (HIP-graph replay safe)
 // The envs of a wave are track neighbours (the previous sort), so a wave sees
-// only a handful of bins: a few atomics per wave.  Order inside a bin follows
-// the atomic order of the waves (not fixed run to run; nothing depends on it).
+// only a handful of bins.  Order inside a bin follows the atomic order of the
+// waves (not fixed run to run; nothing depends on it).
 //
 // rx_state_sync: the caller's bound arrays (env order) <-> the working copy.
 #include <hip/hip_runtime.h>
@@ -31,26 +33,11 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kScanThreads = 1024;
 
-__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
-
-// popcount of the bits of m below this lane
-__device__ __forceinline__ int rank_below(unsigned long long m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 __global__ __launch_bounds__(kBlock) void k_sort_hist(const uint32_t* __restrict__ keys, int n,
-                                                       uint32_t* __restrict__ hist) {
+                                                       uint32_t* __restrict__ hist, uint32_t* __restrict__ off) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  const bool v = i < n;
-  const uint32_t b = v ? keys[i] : 0u;
-  unsigned long long pending = __ballot(v);
-  while (pending) {  // wave-uniform loop: one iteration per distinct bin of the wave
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
-    const unsigned long long m = __ballot(v && b == lb);
-    if (lane_id() == leader) atomicAdd(&hist[lb], (uint32_t)__builtin_popcountll(m));
-    pending &= ~m;
-  }
+  if (i >= n) return;
+  off[i] = rx_bin_count(hist, keys[i]);
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_sort_scan(uint32_t* __restrict__ hist,
@@ -102,27 +89,15 @@ __device__ __forceinline__ void move_row(const rx_state& src, int i, const rx_st
 }
 
 template <int A>
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restrict__ keys, int n,
-                                                          uint32_t* __restrict__ cursor,
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ off, int n,
+                                                          const uint32_t* __restrict__ cursor,
                                                           const int32_t* __restrict__ perm,
                                                           int32_t* __restrict__ perm_tmp, rx_state work,
                                                           rx_state tmp) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  const bool v = i < n;
-  const uint32_t b = v ? keys[i] : 0u;
-  unsigned long long pending = __ballot(v);
-  uint32_t dst = 0;
-  while (pending) {
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
-    const unsigned long long m = __ballot(v && b == lb);
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(&cursor[lb], (uint32_t)__builtin_popcountll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-    if (v && b == lb) dst = base + (uint32_t)rank_below(m);
-    pending &= ~m;
-  }
-  if (!v) return;
+  if (i >= n) return;
+  const uint32_t dst = cursor[keys[i]] + off[i];
   perm_tmp[dst] = perm[i];
   move_row<A>(work, i, tmp, (int)dst);
 }
@@ -181,21 +156,21 @@ __global__ __launch_bounds__(kBlock) void k_feistel_perm(int64_t n, int h, uint6
 
 }  // namespace
 
-extern "C" int rx_sort_envs(const uint32_t* keys, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
+extern "C" int rx_sort_envs(const uint32_t* keys, uint32_t* off, int n, int A, uint32_t* hist, uint32_t* cursor, int nbins,
                             int32_t* perm, int32_t* perm_tmp, const rx_state* work, const rx_state* tmp,
                             hipStream_t s, int hist_done) {
   if (n <= 0) return 0;
   if (nbins <= 0 || nbins > RX_SORT_MAX_BINS || (A != 1 && A != 2)) return (int)hipErrorInvalidValue;
   const int grid = (n + kBlock - 1) / kBlock;
   // hist_done: the step's REWARD half counted the bins while writing the keys
-  if (!hist_done) hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist);
+  if (!hist_done) hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist, off);
   hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanThreads), 0, s, hist, cursor, nbins);
   if (A == 1) {
-    hipLaunchKernelGGL(k_sort_scatter<1>, dim3(grid), dim3(kBlock), 0, s, keys, n, cursor, perm, perm_tmp, *work,
+    hipLaunchKernelGGL(k_sort_scatter<1>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, cursor, perm, perm_tmp, *work,
                        *tmp);
     hipLaunchKernelGGL(k_state_copy<1>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
   } else {
-    hipLaunchKernelGGL(k_sort_scatter<2>, dim3(grid), dim3(kBlock), 0, s, keys, n, cursor, perm, perm_tmp, *work,
+    hipLaunchKernelGGL(k_sort_scatter<2>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, cursor, perm, perm_tmp, *work,
                        *tmp);
     hipLaunchKernelGGL(k_state_copy<2>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
   }
