@@ -65,27 +65,63 @@ __global__ __launch_bounds__(kScanThreads) void k_sort_scan(uint32_t* __restrict
   }
 }
 
+// one env's state row (position i of a working copy), held in registers
+template <int A>
+struct Row {
+  double f[A][8];
+  int32_t fs[A];
+  uint8_t fl[A];
+  int32_t steps, epl;
+  uint8_t ef;
+  double epr;
+  __device__ __forceinline__ void load(const rx_state& src, int i) {
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+      const int si = A * i + q;
+      f[q][0] = src.x[si];
+      f[q][1] = src.y[si];
+      f[q][2] = src.angle[si];
+      f[q][3] = src.vx[si];
+      f[q][4] = src.vy[si];
+      f[q][5] = src.progress[si];
+      f[q][6] = src.last_progress[si];
+      f[q][7] = src.last_steering[si];
+      fl[q] = src.flags[si];
+      fs[q] = src.finished_step ? src.finished_step[si] : 0;
+    }
+    steps = src.steps[i];
+    ef = src.env_flags[i];
+    epr = src.ep_return[i];
+    epl = src.ep_length[i];
+  }
+  __device__ __forceinline__ void store(const rx_state& dst, int j) const {
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+      const int di = A * j + q;
+      dst.x[di] = f[q][0];
+      dst.y[di] = f[q][1];
+      dst.angle[di] = f[q][2];
+      dst.vx[di] = f[q][3];
+      dst.vy[di] = f[q][4];
+      dst.progress[di] = f[q][5];
+      dst.last_progress[di] = f[q][6];
+      dst.last_steering[di] = f[q][7];
+      dst.flags[di] = fl[q];
+      if (dst.finished_step) dst.finished_step[di] = fs[q];
+    }
+    dst.steps[j] = steps;
+    dst.env_flags[j] = ef;
+    dst.ep_return[j] = epr;
+    dst.ep_length[j] = epl;
+  }
+};
+
 // one env's state row: working-state element i (position) -> j
 template <int A>
 __device__ __forceinline__ void move_row(const rx_state& src, int i, const rx_state& dst, int j) {
-#pragma unroll
-  for (int q = 0; q < A; ++q) {
-    const int si = A * i + q, di = A * j + q;
-    dst.x[di] = src.x[si];
-    dst.y[di] = src.y[si];
-    dst.angle[di] = src.angle[si];
-    dst.vx[di] = src.vx[si];
-    dst.vy[di] = src.vy[si];
-    dst.progress[di] = src.progress[si];
-    dst.last_progress[di] = src.last_progress[si];
-    dst.last_steering[di] = src.last_steering[si];
-    dst.flags[di] = src.flags[si];
-    if (src.finished_step) dst.finished_step[di] = src.finished_step[si];
-  }
-  dst.steps[j] = src.steps[i];
-  dst.env_flags[j] = src.env_flags[i];
-  dst.ep_return[j] = src.ep_return[i];
-  dst.ep_length[j] = src.ep_length[i];
+  Row<A> r;
+  r.load(src, i);
+  r.store(dst, j);
 }
 
 template <int A>
@@ -102,10 +138,68 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const uint32_t* __restr
   move_row<A>(work, i, tmp, (int)dst);
 }
 
+// Up to kFusedBins bins the scan runs inside the scatter: every workgroup
+// scans the whole histogram in LDS (at most 32 KB, read from L2) and takes its
+// cursors from there -- one launch and its kernel boundary fewer per re-sort;
+// k_state_copy then clears the histogram (every scatter workgroup has read it).
+constexpr int kFusedBins = 8192;
+
+template <int A>
+__global__ __launch_bounds__(kBlock) void k_sort_scatter_scan(const uint32_t* __restrict__ keys,
+                                                               const uint32_t* __restrict__ off, int n,
+                                                               const uint32_t* __restrict__ hist, int nbins,
+                                                               const int32_t* __restrict__ perm,
+                                                               int32_t* __restrict__ perm_tmp, rx_state work,
+                                                               rx_state tmp) {
+  __shared__ uint32_t cur[kFusedBins];
+  __shared__ uint32_t wtot[kBlock / 64];
+  const int t = threadIdx.x, i = blockIdx.x * kBlock + t;
+  const bool v = i < n;
+  // the env's key, rank, id and state row are loaded first: their latency overlaps the scan
+  uint32_t key = 0, rk = 0;
+  int32_t id = 0;
+  Row<A> r;
+  if (v) {
+    key = keys[i];
+    rk = off[i];
+    id = perm[i];
+    r.load(work, i);
+  }
+  for (int b = t; b < nbins; b += kBlock) cur[b] = hist[b];
+  __syncthreads();
+  const int per = (nbins + kBlock - 1) / kBlock;
+  const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
+  uint32_t s = 0;
+  for (int b = b0; b < b1; ++b) s += cur[b];
+  const int lane = t & 63, w = t >> 6;
+  uint32_t inc = s;  // inclusive scan of the thread sums within the wave, then over the wave totals
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - s;
+  for (int k = 0; k < w; ++k) run += wtot[k];
+  for (int b = b0; b < b1; ++b) {  // this thread's chunk of bins -> exclusive cursors
+    const uint32_t c = cur[b];
+    cur[b] = run;
+    run += c;
+  }
+  __syncthreads();
+  if (!v) return;
+  const uint32_t dst = cur[key] + rk;
+  perm_tmp[dst] = id;
+  r.store(tmp, (int)dst);
+}
+
+// shadow -> working copy; with hist, also clears the histogram (fused-scan re-sort)
 template <int A>
 __global__ __launch_bounds__(kBlock) void k_state_copy(int n, const int32_t* __restrict__ perm_tmp,
-                                                        int32_t* __restrict__ perm, rx_state tmp, rx_state work) {
+                                                        int32_t* __restrict__ perm, rx_state tmp, rx_state work,
+                                                        uint32_t* __restrict__ hist, int nbins) {
   const int j = blockIdx.x * kBlock + threadIdx.x;
+  for (int b = j; b < nbins; b += (int)gridDim.x * kBlock) hist[b] = 0u;
   if (j >= n) return;
   perm[j] = perm_tmp[j];
   move_row<A>(tmp, j, work, j);
@@ -164,15 +258,27 @@ extern "C" int rx_sort_envs(const uint32_t* keys, uint32_t* off, int n, int A, u
   const int grid = (n + kBlock - 1) / kBlock;
   // hist_done: the step's REWARD half counted the bins while writing the keys
   if (!hist_done) hipLaunchKernelGGL(k_sort_hist, dim3(grid), dim3(kBlock), 0, s, keys, n, hist, off);
+  if (nbins <= kFusedBins) {
+    if (A == 1) {
+      hipLaunchKernelGGL(k_sort_scatter_scan<1>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, hist, nbins, perm,
+                         perm_tmp, *work, *tmp);
+      hipLaunchKernelGGL(k_state_copy<1>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work, hist, nbins);
+    } else {
+      hipLaunchKernelGGL(k_sort_scatter_scan<2>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, hist, nbins, perm,
+                         perm_tmp, *work, *tmp);
+      hipLaunchKernelGGL(k_state_copy<2>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work, hist, nbins);
+    }
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(kScanThreads), 0, s, hist, cursor, nbins);
   if (A == 1) {
     hipLaunchKernelGGL(k_sort_scatter<1>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, cursor, perm, perm_tmp, *work,
                        *tmp);
-    hipLaunchKernelGGL(k_state_copy<1>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
+    hipLaunchKernelGGL(k_state_copy<1>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work, nullptr, 0);
   } else {
     hipLaunchKernelGGL(k_sort_scatter<2>, dim3(grid), dim3(kBlock), 0, s, keys, off, n, cursor, perm, perm_tmp, *work,
                        *tmp);
-    hipLaunchKernelGGL(k_state_copy<2>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work);
+    hipLaunchKernelGGL(k_state_copy<2>, dim3(grid), dim3(kBlock), 0, s, n, perm_tmp, perm, *tmp, *work, nullptr, 0);
   }
   return (int)hipGetLastError();
 }

@@ -319,6 +319,37 @@ def test_culling_and_sort_are_exact(rx, golden, chunk, sort, order, sup):
         assert torch.equal(ob, oc) and torch.equal(rb, rc) and torch.equal(db, dc), t
 
 
+@pytest.mark.parametrize("n_widths", [1, 5])
+def test_resort_both_scan_paths_are_exact(rx, golden, n_widths):
+    """The re-sort takes its bin cursors from a scan inside the scatter up to
+    8,192 bins (rx_sort.hip kFusedBins) and from k_sort_scan above; widths varied
+    per env make 21 x 5 (geometry, width) slots, ~35 k bins, so both paths run.
+    Against an unsorted env: outputs bit-identical over 160 steps (10 re-sorts at
+    sort_interval 16), the wave order a permutation."""
+    N = 4200
+    tracks = np.arange(N) % golden.n_tracks
+    ws = [golden.tracks[k]["width"] + (i // golden.n_tracks) % n_widths for i, k in enumerate(tracks)]
+    from rx.track import DEFAULT_CONTROL_POINTS
+    cps = [DEFAULT_CONTROL_POINTS if golden.tracks[k]["label"] == "default" else golden.tracks[k]["cp"] for k in tracks]
+    va = rx.RacingVectorEnv(cps, ws, sched=_PATH_SCHED, autoreset="next_step", sort_interval=0)
+    vb = rx.RacingVectorEnv(cps, ws, sched=_PATH_SCHED, autoreset="next_step", sort_interval=16)
+    bins = vb.env_order()[1]
+    assert (bins <= 8192) == (n_widths == 1) and bins > 0, bins
+    assert torch.equal(va.reset_device(), vb.reset_device())
+    g = torch.Generator(device="cuda").manual_seed(31)
+    for t in range(160):
+        a = torch.rand((N, 2), device="cuda", generator=g) * 2 - 1
+        a[:, 1].abs_()
+        oa, ra, da = va.step_device(a)
+        ob, rb, db = vb.step_device(a)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    perm = vb.env_order()[0]
+    assert np.array_equal(np.sort(perm), np.arange(N))
+    sa, sb = va.get_state(), vb.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+
+
 def test_resort_histogram_survives_split_phase_sequences(rx, golden):
     """The split step's REWARD half counts the re-sort bins as it writes the keys
     (rx_api.cpp sort_hist_done).  Keys requested again before their sort ran --
