@@ -601,7 +601,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cull-chunk", type=int, default=8, help="raycast chunk culling (0 = brute force)")
-    ap.add_argument("--sort-interval", type=int, default=16, help="spatial env re-sort period (0 = never)")
+    ap.add_argument("--sort-interval", type=int, default=None,
+                    help="spatial env re-sort period (0 = never; default rx.vector_env.default_sort_interval)")
     ap.add_argument("--ray-order", type=int, default=2,
                     help="raycast lane order (0 env-major, 1 ray-major, 2 direction-sorted tasks)")
     ap.add_argument("--cull-super", type=int, default=8, help="chunks per super-chunk box (0 = one-level culling)")
@@ -895,7 +896,7 @@ def main():
                                    "11 sensors, uniform random actions resident in HBM, next-step autoreset)",
                        "envs_per_gpu": E, "global_envs": n_total, "track_slots": n_slots,
                        "stream_groups": G, "envs_per_launch": n,
-                       "raycast_cull_chunk": args.cull_chunk, "sort_interval": args.sort_interval,
+                       "raycast_cull_chunk": args.cull_chunk, "sort_interval": env0.sort_interval,
                        "ray_order": args.ray_order, "cull_super": args.cull_super,
                        "schedule": schedule, "sched_overrides": sched or None,
                        "library": os.path.relpath(_lib_path(), ROOT),

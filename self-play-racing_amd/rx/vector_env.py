@@ -89,6 +89,15 @@ class _NumpyStartDraws:
             raise _lib.RxError(f"start draws: {over} resets beyond the session's {self.buf.numel()} draws")
 
 
+def default_sort_interval(n_envs, n_agents):
+    """Dynamics launches between spatial re-sorts (rx.h sort_interval) when the
+    caller names none: 8 for single-agent envs above 32,768 (a re-sort is two
+    launches, ~13 us at 65,536 envs, and keeps the ray waves' culling tight), 16
+    elsewhere (at 4,096-16,384 envs and for two-car envs the sort costs more than
+    the coherence it restores; profiles/r04/probe_sort_interval.txt)."""
+    return 8 if n_agents == 1 and n_envs > 32768 else 16
+
+
 class RacingVectorEnv:
     """N envs (A = 1: RacingEnv, A = 2: MultiRacingEnv) on one device.
 
@@ -101,7 +110,7 @@ class RacingVectorEnv:
 
     def __init__(self, control_points, widths, n_agents=1, n_sensors=11, device=None, autoreset="next_step",
                  seed=0, speed_weight=8.0, max_steps=3000, half_cone=None, track_set=None, cull_chunk=8,
-                 sort_interval=16, ray_order=None, cull_super=8, sched=None):
+                 sort_interval=None, ray_order=None, cull_super=8, sched=None):
         self.L = _lib.load()
         self.device = torch.device(device) if device is not None else _default_device()
         if self.device.type != "cuda":
@@ -112,6 +121,9 @@ class RacingVectorEnv:
         self.num_envs = N
         self.n_agents = A = int(n_agents)
         self.n_sensors = R = int(n_sensors)
+        if sort_interval is None:
+            sort_interval = default_sort_interval(N, A)
+        self.sort_interval = int(sort_interval)
         if ray_order is None:  # direction-sorted ray tasks (rx.h ray_order 2) cover up to 16 sensors
             ray_order = 2 if R <= 16 else 1
         self.D = R + 4 + 4 * (A - 1)
@@ -165,7 +177,7 @@ class RacingVectorEnv:
                 raise ValueError(f"unknown launch-schedule keys {sorted(bad)} (known: {_lib.SCHED_FIELDS})")
             self.sched = sched
             cfg = _lib.RxConfig(N, A, R, self.max_steps, _AUTORESET[autoreset], dev.index or 0, int(seed) & (2**64 - 1),
-                                float(half_cone), self.speed_weight, int(cull_chunk), int(sort_interval),
+                                float(half_cone), self.speed_weight, int(cull_chunk), self.sort_interval,
                                 int(ray_order), int(cull_super), *[int(sched.get(k, 0)) for k in _lib.SCHED_FIELDS])
             h = _lib._P()
             _lib.check(self.L.rx_create(cfg, h), "rx_create")

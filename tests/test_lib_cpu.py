@@ -128,3 +128,15 @@ def test_schedule_config_is_validated_and_the_library_reads_no_environment():
     for knob in (b"RX_SEG_FILTER", b"RX_SPLIT", b"RX_RAY_LPR", b"RX_REWARD_LPE", b"RX_DYN1_LPE", b"RX_WIDE_N",
                  b"RX_ARGMIN_WINDOW", b"RX_BOX_QUAD", b"RX_KIN_WPB", b"RX_RAYS_WPB", b"RX_RAYS_LDS"):
         assert knob not in strings, knob
+
+
+def test_default_sort_interval():
+    """rx.vector_env.default_sort_interval: re-sort every 8 dynamics launches for
+    single-agent envs above 32,768, every 16 elsewhere (profiles/r04/probe_sort_interval.txt)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
+    from rx.vector_env import default_sort_interval
+    assert default_sort_interval(65536, 1) == 8
+    assert default_sort_interval(32768, 1) == 16
+    assert default_sort_interval(4096, 1) == 16
+    assert default_sort_interval(65536, 2) == 16
