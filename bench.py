@@ -634,6 +634,11 @@ def main():
     ap.add_argument("--sync", choices=("spin", "block"), default="spin",
                     help="how the host waits at the timed region's edges: spin on the streams' queues, then "
                          "torch.cuda.synchronize() (default), or the blocking synchronize alone")
+    ap.add_argument("--graph", choices=("on", "off"), default="on",
+                    help="on (default, one stream group): the timed region replays ONE HIP graph holding exactly "
+                         "--steps production steps (each one rx_step: k_kin1 + k_step2, the re-sorts where they "
+                         "fall), captured untimed before the refill steps -- the launch path of the captured PPO "
+                         "rollout; off: one rx_step call per step from Python")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, reports its device and "
                          "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
@@ -793,6 +798,22 @@ def main():
     refill = max(0, min(args.refill, untimed))
     for _ in range(untimed - refill):
         one_step()
+    # the timed steps as one HIP graph (--graph on): captured here, before the refill
+    # steps bring the GPU back to its loaded clock; capturing executes nothing (the
+    # library's host-side schedule -- re-sort and task-order launches -- is recorded
+    # as it falls for these steps), the timed region replays it exactly once
+    step_graph = None
+    if args.graph == "on" and G == 1:
+        torch.cuda.synchronize(dev)
+        step_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(step_graph, stream=torch.cuda.Stream(device=dev)):
+            for _ in range(args.steps):
+                one_step()
+        torch.cuda.synchronize(dev)
+        # one untimed replay (K more burn-in steps of the same work): a graph's first
+        # launch also uploads it, which would otherwise sit at the timed region's edge
+        step_graph.replay()
+        torch.cuda.synchronize(dev)
     ep_untimed = [0.0, 0.0, 0]
     if refill:
         gc.collect()
@@ -806,7 +827,10 @@ def main():
         sync_all()
         ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- timed region: production steps only (one rx_step per step, no instrumentation)
-    elapsed = timed(one_step, args.steps, collect=refill == 0)
+    if step_graph is not None:
+        elapsed = timed(lambda ev=None: step_graph.replay(), 1, collect=refill == 0)
+    else:
+        elapsed = timed(one_step, args.steps, collect=refill == 0)
     ep = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- instrumented region (after, same state distribution): per-kernel durations of the
     # production launches (k_kin1, k_step2) on every other step; on the others the dynamics
@@ -901,11 +925,14 @@ def main():
                        "schedule": schedule, "sched_overrides": sched or None,
                        "library": os.path.relpath(_lib_path(), ROOT),
                        "parallelism": f"env shards x{world}, no collective in the step"},
-            "steady_state": {"untimed_steps_before_timing": untimed,
+            "steady_state": {"untimed_steps_before_timing": untimed + (args.steps if step_graph is not None else 0),
                              "episodes_ended_before_timing": ep_untimed[2],
                              "episodes_ended_in_timed_region": ep[2],
                              "timed_region": "production steps only: one rx_step (k_kin1 + k_step2) per step, "
-                                             "no instrumentation"},
+                                             "no instrumentation",
+                             "launch": (f"one HIP graph replay of the {args.steps} steps (captured and replayed "
+                                        "once untimed)"
+                                        if step_graph is not None else "one rx_step call per step from Python")},
             # dominant kernel of the production step: k_step2 (REWARD half beside the raycast)
             "roofline": {"bound": "hbm", "kernel": "k_step2", "achieved": round(step2_gbs, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step2_gbs / HBM_PEAK_GBS,

@@ -3,7 +3,7 @@
 # bench command, 1,000 steady-state steps, the rocprofv3 summary of the driver's command, and
 # the configs[1] / configs[3] PPO iterations (tools/bench_ppo.py).
 set -u
-OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/r04z; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/${CLOSE_DIR:-r04z}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
   > $OUT/pytest_gpu.txt 2>&1 || { tail -60 $OUT/pytest_gpu.txt; exit 1; }
 tail -3 $OUT/pytest_gpu.txt
