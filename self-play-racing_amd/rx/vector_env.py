@@ -417,6 +417,12 @@ class RacingVectorEnv:
         self._launched(stream)
         return obs_out if obs_out is not None else self.buf["obs"]
 
+    def _step_call(self, io, phases, s):
+        if phases == 3:
+            _lib.check(self.L.rx_step(self._h, io, s.cuda_stream), "rx_step")
+        else:
+            _lib.check(self.L.rx_step_phases(self._h, io, int(phases), s.cuda_stream), "rx_step_phases")
+
     def step_device(self, actions, obs_out=None, reward_out=None, done_out=None, full_info=False, stream=None,
                     phases=3):
         """One step of every env from device actions; returns (obs, reward, done_f32) tensors.
@@ -427,11 +433,12 @@ class RacingVectorEnv:
         a = self._as_actions(actions)
         io = self._io(actions=a, obs=obs_out, reward=reward_out, done=done_out, full=full_info)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)  # resolved once per step
-        with self.start_draw_session(self.num_envs):
-            if phases == 3:
-                _lib.check(self.L.rx_step(self._h, io, s.cuda_stream), "rx_step")
-            else:
-                _lib.check(self.L.rx_step_phases(self._h, io, int(phases), s.cuda_stream), "rx_step_phases")
+        d = self._draws
+        if d is None or d.active:  # no draw session to open (the per-step host path stays short)
+            self._step_call(io, phases, s)
+        else:
+            with self.start_draw_session(self.num_envs):
+                self._step_call(io, phases, s)
         self._launched(s)
         return (obs_out if obs_out is not None else self.buf["obs"],
                 reward_out if reward_out is not None else self.buf["reward"],
