@@ -806,7 +806,8 @@ def main():
     if args.graph == "on" and G == 1:
         torch.cuda.synchronize(dev)
         step_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(step_graph, stream=torch.cuda.Stream(device=dev)):
+        # thread_local: a process group's watchdog thread may query its events meanwhile
+        with torch.cuda.graph(step_graph, stream=torch.cuda.Stream(device=dev), capture_error_mode="thread_local"):
             for _ in range(args.steps):
                 one_step()
         torch.cuda.synchronize(dev)
