@@ -28,3 +28,8 @@ TR=$(find /tmp/drvprof -name '*kernel_trace.csv' | head -1)
 python3 tools/kstats_by_grid.py "$TR" $OUT/bench_driver20_kernel_stats_by_grid.csv > /dev/null || exit 1
 head -12 $OUT/bench_driver20_kernel_stats.csv | cut -c1-160
 echo R04Z_DONE
+# the N-rank bench path rehearsed on this one GPU (2 self-launched gloo ranks: a path check, not a scaling number)
+timeout -k 10 600 python -u bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --no-cpu-baseline --no-time-to-90 \
+  > $OUT/bench_2rank_gloo.jsonl 2> $OUT/bench_2rank_gloo.err || { tail -30 $OUT/bench_2rank_gloo.err; exit 1; }
+tail -c 400 $OUT/bench_2rank_gloo.jsonl; echo
+echo R04Z_RANKS_DONE
