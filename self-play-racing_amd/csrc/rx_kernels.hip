@@ -436,6 +436,10 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+#ifdef RX_DYN_STAMPS  // profiling build: the sort's own phases (ranks | scan + scatter | row copy)
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
   const int c0 = cnt[lane];
   int c = c0;
 #pragma unroll
@@ -456,6 +460,14 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
+#ifdef RX_DYN_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+  if (a.io.counters && lane == 0 && blockDim.x == 64) {  // k_kin1: one wave per workgroup
+    a.io.counters[16 + 12 * (int)blockIdx.x + 10] = ts1;
+    a.io.counters[16 + 12 * (int)blockIdx.x + 11] = ts2;
+  }
+#endif
   int32_t* out = a.tasks_out + (size_t)perm_start * AR;
   for (int i = lane; i < total; i += 64) out[i] = stage[i];
 }
