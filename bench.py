@@ -301,18 +301,20 @@ def time_to_90(configs, seeds=(1, 2, 3)):
     the training time excludes."""
     from tools.time_to_success import run as tts
     out = []
-    for ne, ns, shuffle in configs:
+    for cfg in configs:
+        ne, ns, shuffle = cfg[:3]
+        pdt = cfg[3] if len(cfg) > 3 else "fp32"
         runs = []
         for sd in seeds:
             r = tts(num_envs=ne, num_steps=ns, eval_every=1, device_shuffle=shuffle == "device", max_minutes=1.0,
-                    quiet=True, seed=sd)
+                    quiet=True, seed=sd, policy_dtype=pdt)
             runs.append({"seed": sd, "value_s": r["value_s"], "build_s": r["build_s"],
                          "reached_at_step": r["reached_at_step"], "updates": len(r["curve"]),
                          "success_rate": r["curve"][-1].get("success_rate") if r["curve"] else None})
         vals = sorted(x["value_s"] for x in runs if x["value_s"] is not None)
         dist = {"min": vals[0], "median": vals[len(vals) // 2] if len(vals) % 2 else
                 round(0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2]), 4), "max": vals[-1]} if vals else None
-        out.append({"num_envs": ne, "num_steps": ns, "shuffle": shuffle, "value_s": dist,
+        out.append({"num_envs": ne, "num_steps": ns, "shuffle": shuffle, "policy_dtype": pdt, "value_s": dist,
                     "reached": f"{len(vals)}/{len(runs)} seeds", "runs": runs})
     return {"metric": "PPO wall-clock to 90% success rate", "unit": "s", "higher_is_better": False,
             "protocol": "evaluate.py: 40 tracks (seed 42) x 5 runs, widths by run, <= 2000 steps, stochastic "
@@ -895,7 +897,8 @@ def main():
         sp = selfplay_leg(dev, args.selfplay_envs, args.ppo_steps, args.selfplay_updates)
     tt90 = None
     if world == 1 and not args.no_time_to_90:
-        tt90 = time_to_90([(16, 2048, "numpy"), (4096, 128, "device")])
+        # configs[1] is named "PPO bf16": its 4,096-env entry runs in both precisions
+        tt90 = time_to_90([(16, 2048, "numpy"), (4096, 128, "device"), (4096, 128, "device", "bf16")])
 
     if rank == 0:
         value = n_total * args.steps / elapsed

@@ -16,6 +16,7 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -60,23 +61,41 @@ def run_workers(jobs, timeout_s):
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
     env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "self-play-racing_amd"),
                                          env.get("PYTHONPATH", "")]).rstrip(os.pathsep)
+    # stdout / stderr go to temporary files, not pipes: a child that writes more than a
+    # pipe buffer (repeated warnings) cannot block against the parent, and every wait
+    # below has a real deadline
     procs = []
-    for cp, width, budget, seed in jobs:
-        arg = json.dumps({"cp": np.asarray(cp, dtype=np.float64).tolist(), "width": float(width),
-                          "budget_s": float(budget), "seed": int(seed)})
-        procs.append(subprocess.Popen([sys.executable, "-m", "oracle.cpu_baseline"], cwd=ROOT, env=env,
-                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                      text=True))
-        procs[-1].stdin.write(arg)
-        procs[-1].stdin.close()
-    out = []
-    for p in procs:
-        o, e = p.stdout.read(), p.stderr.read()
-        rc = p.wait(timeout=timeout_s)
-        if rc != 0:
-            raise RuntimeError(f"cpu_baseline worker exited with {rc}: {e[-2000:]}")
-        r = json.loads(o.strip().splitlines()[-1])
-        out.append((int(r["steps"]), float(r["seconds"])))
+    deadline = time.monotonic() + timeout_s
+    try:
+        for cp, width, budget, seed in jobs:
+            arg = json.dumps({"cp": np.asarray(cp, dtype=np.float64).tolist(), "width": float(width),
+                              "budget_s": float(budget), "seed": int(seed)})
+            fo, fe = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
+            p = subprocess.Popen([sys.executable, "-m", "oracle.cpu_baseline"], cwd=ROOT, env=env,
+                                 stdin=subprocess.PIPE, stdout=fo, stderr=fe, text=True)
+            procs.append((p, fo, fe))
+            p.stdin.write(arg)
+            p.stdin.close()
+        out = []
+        for p, fo, fe in procs:
+            try:
+                rc = p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                raise RuntimeError(f"cpu_baseline worker still running after {timeout_s} s") from None
+            fo.seek(0)
+            fe.seek(0)
+            o, e = fo.read(), fe.read()
+            if rc != 0:
+                raise RuntimeError(f"cpu_baseline worker exited with {rc}: {e[-2000:]}")
+            r = json.loads(o.strip().splitlines()[-1])
+            out.append((int(r["steps"]), float(r["seconds"])))
+    finally:
+        for p, fo, fe in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+            fo.close()
+            fe.close()
     return out
 
 

@@ -874,11 +874,13 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   if (wave >= a.n_dyn_waves) return;
   // ray-task sort: per wave 64 sector counters and a staging row of its <= 64 x 16 task ids
   // (k_kin1 runs one wave per workgroup, k_dyn1 four)
+  // dynamic LDS, task_sort_lds_bytes: sized only when the launch sorts (the
+  // static rows cost occupancy on the resets / same-step launches, which never sort)
   constexpr int NW = PART == RX_PART_KIN ? 1 : 4;
-  __shared__ int32_t tcnt[NW][kTaskSectors];
-  __shared__ int32_t tstage[NW][64 * 16];
+  extern __shared__ int32_t task_lds[];
   const int wl = NW == 1 ? 0 : (int)(threadIdx.x >> 6);
-  int32_t* cnt = tcnt[wl];
+  int32_t* cnt = task_lds + wl * (kTaskSectors + 64 * 16);
+  int32_t* stage = cnt + kTaskSectors;
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
   const unsigned long long prof_t0 = prof_start(a);
@@ -886,7 +888,7 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   int e = -1;  // set on the lane that finishes an env (sub 0)
   dyn1_env<LPE, PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
-  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, tstage[wl]);
+  if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, stage);
   prof_end(a, wave, prof_t0);
 #ifdef RX_DYN_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
@@ -1387,10 +1389,10 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
   constexpr int NW = PART == RX_PART_KIN ? 1 : 4;  // k_kin2: one wave per workgroup
-  __shared__ int32_t tcnt[NW][kTaskSectors];
-  __shared__ int32_t tstage[NW][64 * 32];
+  extern __shared__ int32_t task_lds[];  // task_sort_lds_bytes (as k_dyn1)
   const int wl = NW == 1 ? 0 : (int)(threadIdx.x >> 6);
-  int32_t* cnt = tcnt[wl];
+  int32_t* cnt = task_lds + wl * (kTaskSectors + 64 * 32);
+  int32_t* stage = cnt + kTaskSectors;
   const bool sorting = a.tasks_out != nullptr;
   if (sorting) cnt[threadIdx.x & 63] = 0;
   const unsigned long long prof_t0 = prof_start(a);
@@ -1398,7 +1400,7 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
   int e = -1;
   dyn2_env<PART>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
-  if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, tstage[wl]);
+  if (sorting) sort_block_tasks<2>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, stage);
   prof_end(a, wave, prof_t0);
 }
 
@@ -2339,6 +2341,12 @@ __global__ __launch_bounds__(256) void k_gae_scan(int T, int N, const float* __r
 }  // namespace
 
 // ------------------------------------------------------------ launchers
+// dynamic LDS of k_dyn1 / k_dyn2 (k_kin1 / k_kin2): per wave the sort's sector
+// counters and its staging row of 64 x 16 A task ids, only when the launch sorts
+static size_t task_sort_lds_bytes(const rx_kargs* a, int n_agents, int waves_per_wg) {
+  if (!a->tasks_out) return 0;
+  return (size_t)waves_per_wg * (kTaskSectors + 64 * 16 * n_agents) * sizeof(int32_t);
+}
 // k_step2<A, RLPE, LPR> for the handle's schedule (a->reward_lpe, a->ray_lpr:
 // 1, 2 or 4 each, validated by rx_assign)
 template <int A, int RLPE>
@@ -2355,7 +2363,7 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
   if (n_agents == 2) {  // k_kin2, then k_step2<2> (REWARD waves padded to 8, as below)
     const int n_rw2 = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);
     if (part == RX_SPLIT_KIN) {
-      hipLaunchKernelGGL((k_dyn2<RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
+      hipLaunchKernelGGL((k_dyn2<RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 2, 1), s, *a);
     } else {
       const dim3 grid(n_rw2 + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves));
       if (a->reward_lpe == 2)
@@ -2369,7 +2377,7 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
-    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
+    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 1, 1), s, *a);
     return (int)hipGetLastError();
   }
   // RX_SPLIT_REWARD: the REWARD half alone; RX_SPLIT_REWARD_RAYS: both halves in one launch
@@ -2387,16 +2395,17 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   const dim3 blk(256);
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
+    const size_t lds = task_sort_lds_bytes(a, n_agents, 4);
     if (n_agents == 1 && a->dyn_lpe == 64)
-      hipLaunchKernelGGL((k_dyn1<64, RX_PART_FULL>), grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<64, RX_PART_FULL>), grd, blk, lds, s, *a);
     else if (n_agents == 1 && a->dyn_lpe == 4)
-      hipLaunchKernelGGL((k_dyn1<4, RX_PART_FULL>), grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<4, RX_PART_FULL>), grd, blk, lds, s, *a);
     else if (n_agents == 1 && a->dyn_lpe == 2)
-      hipLaunchKernelGGL((k_dyn1<2, RX_PART_FULL>), grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<2, RX_PART_FULL>), grd, blk, lds, s, *a);
     else if (n_agents == 1)
-      hipLaunchKernelGGL((k_dyn1<1, RX_PART_FULL>), grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn1<1, RX_PART_FULL>), grd, blk, lds, s, *a);
     else
-      hipLaunchKernelGGL((k_dyn2<RX_PART_FULL>), grd, blk, 0, s, *a);
+      hipLaunchKernelGGL((k_dyn2<RX_PART_FULL>), grd, blk, lds, s, *a);
   }
   if ((phases & RX_PHASE_RAYS) && a->wide) {
     const dim3 wg((a->n_wide_tasks + 3) / 4);

@@ -116,16 +116,21 @@ class SelfPlayPPO(PPO):
         fn = env_fn if lo == 0 else (lambda i: env_fn(lo + i))
         venv = build_vector_env(fn, n, c["seed"] + rdist.rank(), self.device)
         if c.get("start_draws", "hash") == "numpy":  # the reference's np.random start-slot stream
+            if rdist.world() > 1:
+                # every rank would replay the SAME np.random stream for its own env shard, not
+                # the reference's single stream over the global env order
+                raise ValueError("start_draws='numpy' needs world size 1: the reference's single "
+                                 "np.random start-slot stream cannot be split over ranks (use 'hash')")
             venv.use_numpy_start_draws()
         return SelfPlayVectorEnv(venv, 0, seed=c["seed"] + rdist.rank())
 
     def snapshot_agent(self):
         """A frozen copy of the current policy (agent/self_play_ppo.py:31-44 builds a
         fresh Agent and loads a deep copy of the state dict).  Here: ONE deepcopy of
-        the module -- its parameters are views of the flat parameter buffer, so the
-        copy is one device-to-device copy of that buffer (and of the gradient buffer)
-        with the same views -- instead of a CPU orthogonal init, 13 pageable host to
-        device copies (each one a stream sync) and 13 state-dict copies."""
+        the module -- each parameter and buffer is cloned on the device (one
+        device-to-device copy each; gradients are not copied) -- instead of a CPU
+        orthogonal init, 13 pageable host-to-device copies (each one a stream sync)
+        and 13 state-dict copies."""
         snap = copy.deepcopy(self.agent)
         snap.eval()
         for p in snap.parameters():

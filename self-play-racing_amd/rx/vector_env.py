@@ -67,6 +67,12 @@ class _NumpyStartDraws:
 
     def begin(self, cap):
         cap = max(int(cap), 1)
+        if self.buf is not None:  # between sessions the handle holds 0 draws: a reset there overruns
+            torch.cuda.synchronize(self.env.device)
+            stray = int(self.cursor[1].item())
+            if stray:
+                raise _lib.RxError(f"start draws: {stray} resets ran outside a start-draw session (their start "
+                                   "slots did not come from np.random)")
         self.state0 = np.random.get_state()
         u = np.random.randint(0, 2**32, size=cap, dtype=np.uint32)
         np.random.set_state(self.state0)
@@ -85,6 +91,13 @@ class _NumpyStartDraws:
         np.random.set_state(self.state0)
         if used:
             np.random.randint(0, 2**32, size=used, dtype=np.uint32)  # the reference's draws, consumed
+        # until the next session the handle holds NO draws with a zeroed cursor: a reset
+        # launched outside a session (a direct rx_step / rx_reset) takes nothing from the
+        # buffer, is counted in cursor[1], and the next begin() raises instead of handing
+        # out already-consumed outputs again
+        self.cursor.zero_()
+        _lib.check(self.env.L.rx_set_start_draws(self.env._h, _lib.ptr(self.buf), 0, _lib.ptr(self.cursor)),
+                   "rx_set_start_draws")
         if over:
             raise _lib.RxError(f"start draws: {over} resets beyond the session's {self.buf.numel()} draws")
 

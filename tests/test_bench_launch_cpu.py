@@ -70,3 +70,21 @@ def test_cpu_baseline_workers_are_torch_free_and_exit_cleanly():
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["torch_loaded"] is False and out["steps"] > 0
+
+
+def test_cpu_baseline_worker_timeout_is_enforced():
+    """A worker that outlives the deadline is killed and reported (ADVICE r04:
+    the waits used to come after blocking pipe reads, so the timeout never applied)."""
+    import time
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
+    from rx.track import gen_tracks
+    from oracle.cpu_baseline import run_workers
+    import numpy as np
+    import pytest
+    np.random.seed(1)
+    pool = gen_tracks(1, seed=1)
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="still running"):
+        run_workers([(pool[0], 7, 60.0, 0)], timeout_s=3)
+    assert time.monotonic() - t0 < 30

@@ -157,3 +157,22 @@ def test_single_agent_and_same_step_refuse_draws():
     v2.use_numpy_start_draws()
     with pytest.raises(_lib.RxError):
         v2.reset_device()
+
+
+def test_reset_outside_a_session_is_counted_and_raised():
+    """between sessions the handle holds no draws.  A reset launched
+    straight through the C API (no session) takes nothing from the consumed
+    buffer -- np.random does not move -- and the next session refuses to start."""
+    from rx import _lib
+    N = 64
+    v = _env(N, seed=3)
+    np.random.seed(11)
+    v.reset_device()  # one session: N draws consumed
+    st = np.random.get_state()
+    io = v._io(full=True)
+    _lib.check(v.L.rx_reset(v._h, None, io, _lib.stream_ptr()), "rx_reset")  # straight through the C API
+    torch.cuda.synchronize()
+    a = np.random.get_state()
+    assert a[2] == st[2] and np.array_equal(a[1], st[1])  # nothing drawn from np.random
+    with pytest.raises(_lib.RxError, match="outside a start-draw session"):
+        v.reset_device()

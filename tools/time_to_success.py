@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "self-play-racing_amd"))
 
 
 def run(num_envs=16, num_steps=2048, total_timesteps=5_000_000, eval_every=5, target=0.9, max_minutes=15.0, seed=1,
-        device_shuffle=False, quiet=False):
+        device_shuffle=False, quiet=False, policy_dtype="fp32"):
     """Train (train.py train_single through rx) and evaluate every ``eval_every``
     updates; returns the result dict (value_s = training seconds to target)."""
     from rx.configs import base_config
@@ -37,7 +37,7 @@ def run(num_envs=16, num_steps=2048, total_timesteps=5_000_000, eval_every=5, ta
     from rx.track import gen_tracks
 
     config = base_config(num_envs=num_envs, num_steps=num_steps, total_timesteps=total_timesteps,
-                         seed=seed, shuffle="device" if device_shuffle else "numpy")
+                         seed=seed, shuffle="device" if device_shuffle else "numpy", policy_dtype=policy_dtype)
     random.seed(config["seed"])
     np.random.seed(config["seed"])
     torch.manual_seed(config["seed"])
@@ -84,7 +84,7 @@ def run(num_envs=16, num_steps=2048, total_timesteps=5_000_000, eval_every=5, ta
             "value_s": reached["train_s"] if reached else None,
             "reached_at_step": reached["global_step"] if reached else None,
             "config": {"num_envs": num_envs, "num_steps": num_steps, "total_timesteps": total_timesteps,
-                       "shuffle": config.get("shuffle", "numpy"),
+                       "shuffle": config.get("shuffle", "numpy"), "policy_dtype": policy_dtype,
                        "eval": "evaluate.py protocol: 40 tracks (seed 42) x 5 runs, widths by run, max 2000 steps, "
                                "stochastic policy", "eval_every_updates": eval_every},
             "build_s": round(build_s, 3), "curve": curve}
@@ -100,10 +100,12 @@ def main():
     ap.add_argument("--max-minutes", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--device-shuffle", action="store_true", help="config shuffle='device' (torch.randperm)")
+    ap.add_argument("--device-shuffle", action="store_true", help="config shuffle='device' (rx_random_permutation)")
+    ap.add_argument("--policy-dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="config policy_dtype: bf16 runs the policy / PPO kernels on bf16 MFMA operands")
     args = ap.parse_args()
     out = run(args.num_envs, args.num_steps, args.total_timesteps, args.eval_every, args.target, args.max_minutes,
-              args.seed, args.device_shuffle)
+              args.seed, args.device_shuffle, policy_dtype=args.policy_dtype)
     print(json.dumps(out), flush=True)
     if args.out:
         with open(args.out, "w") as f:
