@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 20
+#define RX_ABI_VERSION 21
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -119,6 +119,11 @@ typedef struct {
      launches (and after every spatial re-sort); in between the ray waves keep the previous
      order.  0 auto (2 up to 16,384 (env, car) pairs, 1 above), 1 .. 16 */
   int32_t task_sort;
+  /* ABI v21: rx_steps runs consecutive single-agent split steps as multi-step windows (k_window: a
+     workgroup per 64-env block for all steps between two spatial re-sorts) where the schedule allows
+     (one lane per ray and per env in REWARD, ray_order 2, task_sort 1); elsewhere, or with -1, it
+     enqueues the per-step launches of rx_step.  0 auto (on), 1 on, -1 off.  Scheduling only. */
+  int32_t window;
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -191,9 +196,11 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
  * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
  * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
  * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
- * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval.  Host only, no
+ * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval, rx_steps
+ * multi-step windows (0/1, ABI v21), dynamics launches so far (the re-sort cadence counter: the
+ * launch with count % sort_interval == 0 writes the re-sort keys; ABI v21).  Host only, no
  * device call. */
-#define RX_SCHEDULE_W 15
+#define RX_SCHEDULE_W 17
 int rx_schedule(const rx_env* h, int32_t* out);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env
@@ -260,6 +267,24 @@ int rx_set_start_draws(rx_env* h, const uint32_t* draws, int64_t n_draws, int64_
  * autoreset semantics. */
 int rx_step(rx_env* h, const rx_io* io, void* stream);
 
+/* ABI v21.  n_steps consecutive steps from one call, each equal to an rx_step of
+ * the io rows at that step (bit for bit: the same kernels' arithmetic on the same
+ * rows).  Step s reads actions + s * strides->actions and writes obs + s *
+ * strides->obs, reward + s * strides->reward, ... (element strides; a stride of 0
+ * writes every step into the same rows, which then hold the last step's outputs;
+ * strides = NULL: all 0).  ep_stats and counters accumulate.  The actions of all
+ * n_steps steps must be in device memory when the call is made: open-loop
+ * action sequences (the env-throughput benchmark: a bank of random actions) --
+ * a policy-in-the-loop rollout is rx_rollout_steps.  With rx_config.window on
+ * (default) the steps between two spatial re-sorts of a single-agent split-step
+ * handle run as ONE k_window launch: no kernel boundary per step
+ * and no chip-wide drain per step.  Replaces n_steps iterations of
+ * SyncVectorEnv.step (agent/ppo.py:112) with precomputed actions. */
+typedef struct {
+  int64_t actions, obs, reward, reward64, terminated, truncated, done_f32, info, ep_done;
+} rx_io_strides;
+int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* strides, void* stream);
+
 /* rx_step split into its two kernels, for per-kernel timing with stream
  * events: phases bit 0 = dynamics/reward/done/autoreset (k_dyn), bit 1 =
  * raycast observations (k_rays).  rx_step == phases 3.  Running bit 1 alone
@@ -284,7 +309,8 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
 #define RX_KERNEL_KIN 2    /* k_kin1: first kernel of the split step */
 #define RX_KERNEL_STEP2 3  /* k_step2: REWARD half + raycast in one launch (split step) */
 #define RX_KERNEL_REWARD 4 /* k_step2 with the REWARD half only (rx_step_phases dynamics) */
-#define RX_KERNEL_KINDS 5
+#define RX_KERNEL_WINDOW 5 /* k_window: a multi-step window of rx_steps (its duration covers all its steps) */
+#define RX_KERNEL_KINDS 6
 int rx_profile(rx_env* h, int32_t enable);
 int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count);
 /* Diagnostics (ABI v18): the raw per-wave stamps of recorded launch `launch`

@@ -107,6 +107,9 @@ struct rx_env {
   int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
   int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
   int32_t task_sort = 1;                   // ray-task direction sort every task_sort dynamics launches
+  bool window = false;                     // rx_steps runs k_window (multi-step windows), rx_assign's choice
+  int32_t window_cap = 0;                  // k_window workgroups resident at once (occupancy x CUs)
+  DevBuf<rx_kargs> win_args;               // k_window's per-step argument blocks [RX_WIN_MAX_STEPS]
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -324,6 +327,7 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
+  if (!tri(cfg->window)) return fail(RX_EINVAL, "window must be 0 (auto), 1 or -1 (got %d)", cfg->window);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
     return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
@@ -397,7 +401,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort};
+                                    h->task_sort, h->window ? 1 : 0, (int32_t)h->dyn_calls};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -412,6 +416,7 @@ int rx_destroy(rx_env* h) {
                   &h->slot_n, &h->tasks})
     b->release();
   h->cs_scratch.release();
+  h->win_args.release();
   h->prof_buf.release();
   h->resets.release();
   h->draw_rank.release();
@@ -677,6 +682,24 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->ray_waves_h = ray;
   h->n_dyn_waves = (int32_t)dyn.size();
   h->n_ray_waves = (int32_t)ray.size();
+  // rx_steps' multi-step windows (k_window): the single-agent split-step schedule at one lane
+  // per env and per ray with the direction sort every launch, and every block's workgroup
+  // resident at once (a workgroup that waits for a free slot would run its whole window after
+  // the others: the launch would take twice as long)
+  h->window = false;
+  if (c.window >= 0 && A == 1 && h->split && h->cfg.ray_order == 2 && h->ray_lpr == 1 && h->reward_lpe == 1 &&
+      h->task_sort == 1 && h->dyn_lpe == 1 && R <= 16 && h->cfg.autoreset != RX_AUTORESET_SAME_STEP) {
+    if (h->window_cap == 0) {
+      RX_HIP(hipSetDevice(h->cfg.device));
+      h->window_cap = rx_window_capacity(h->cfg.device);
+    }
+    h->window = h->n_dyn_waves <= h->window_cap;
+    if (h->window && !h->win_args.p) {  // here, not in rx_steps: no allocation may happen inside a graph capture
+      if (hipMalloc(&h->win_args.p, RX_WIN_MAX_STEPS * sizeof(rx_kargs)) != hipSuccess)
+        return fail(RX_ENOMEM, "rx_assign: window argument blocks");
+      h->win_args.n = RX_WIN_MAX_STEPS;
+    }
+  }
   h->assigned = true;
   h->tasks_stale = true;
   h->sort_pending = false;
@@ -1050,6 +1073,83 @@ int rx_step(rx_env* h, const rx_io* io, void* stream) { return launch(h, io, RX_
 
 int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream) {
   return launch(h, io, RX_MODE_STEP, nullptr, stream, phases);
+}
+
+// ABI v21: n_steps steps from one call.  With h->window (rx_assign) the steps run as
+// k_window launches, one per stretch of steps between two spatial re-sorts: the last
+// step of a stretch writes the sort keys (and counts the bins) exactly where the
+// per-step path would (dyn_calls % sort_interval == 0), and the re-sort follows it.
+static rx_io io_at(const rx_io* io, const rx_io_strides& st, int64_t s) {
+  rx_io o = *io;
+  o.actions = io->actions + s * st.actions;
+  o.obs = io->obs + s * st.obs;
+  if (io->reward) o.reward = io->reward + s * st.reward;
+  if (io->reward64) o.reward64 = io->reward64 + s * st.reward64;
+  if (io->terminated) o.terminated = io->terminated + s * st.terminated;
+  if (io->truncated) o.truncated = io->truncated + s * st.truncated;
+  if (io->done_f32) o.done_f32 = io->done_f32 + s * st.done_f32;
+  if (io->info) o.info = io->info + s * st.info;
+  if (io->ep_done) o.ep_done = io->ep_done + s * st.ep_done;
+  return o;
+}
+
+int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* strides, void* stream) {
+  if (!h) return fail(RX_EINVAL, "null handle");
+  if (!io) return fail(RX_EINVAL, "io is null");
+  if (n_steps < 0) return fail(RX_EINVAL, "n_steps must be >= 0 (got %d)", n_steps);
+  if (!io->obs || !io->actions) return fail(RX_EINVAL, "io->obs and io->actions are required");
+  if (h->n_tracks <= 0 || !h->assigned || !h->bound)
+    return fail(RX_ESTATE, "rx_steps needs rx_upload_tracks, rx_assign and rx_bind_state");
+  const rx_io_strides st = strides ? *strides : rx_io_strides{};
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  int32_t k = 0;
+  while (k < n_steps) {
+    if (!h->window || h->sort_pending) {  // the per-step launches (a pending re-sort first runs in launch())
+      const rx_io o = io_at(io, st, k);
+      if ((rc = launch(h, &o, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
+      ++k;
+      continue;
+    }
+    // this window: up to and including the next step that writes the re-sort keys
+    int32_t len = std::min(n_steps - k, (int32_t)RX_WIN_MAX_STEPS);
+    bool keys = false;
+    const int iv = h->cfg.sort_interval;
+    if (iv > 0 && h->sort_on) {
+      const int64_t d = (int64_t)((iv - (int64_t)(h->dyn_calls % (uint64_t)iv)) % iv);  // steps before the key step
+      if (d < len) {
+        len = (int32_t)d + 1;
+        keys = true;
+      }
+    }
+    rx_kargs a{};
+    const rx_io o = io_at(io, st, k);
+    make_kargs(h, &o, RX_MODE_STEP, nullptr, a);
+    a.tasks_out = nullptr;  // the window's ray tasks live in LDS
+    if (keys) {
+      if (h->sort_hist_done) {  // counts of keys a previous launch wrote and no sort consumed
+        RX_HIP(hipMemsetAsync(h->sort_hist.p, 0, (size_t)h->sort_bins * sizeof(uint32_t), s));
+        h->sort_hist_done = false;
+      }
+      a.sort_keys = h->keys_in.p;
+      a.sort_hist = h->sort_hist.p;
+      a.sort_off = h->keys_off.p;
+    }
+    prof_arm(h, a, RX_KERNEL_WINDOW);
+    if ((rc = rx_launch_window(&a, &st, len, keys ? 1 : 0, h->win_args.p, s)) != 0)
+      return fail(RX_EHIP, "k_window launch failed: %s", hipGetErrorString((hipError_t)rc));
+    h->dyn_calls += (uint64_t)len;
+    h->task_calls += (uint64_t)len;
+    h->tasks_stale = true;  // the global task buffer holds no order of these states
+    if (keys) {
+      rx_state work = h->work, tmp = h->work_tmp;
+      if ((rc = rx_sort_envs(h->keys_in.p, h->keys_off.p, h->cfg.n_envs, 1, h->sort_hist.p, h->sort_cursor.p,
+                             h->sort_bins, h->perm[0].p, h->perm[1].p, &work, &tmp, s, 1)) != 0)
+        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
+    }
+    k += len;
+  }
+  return RX_OK;
 }
 
 // rx_rollout: the persistent small-N rollout (k_rollout) on a handle in the

@@ -185,6 +185,15 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
+// k_window: n_steps single-agent split steps in one launch, a workgroup per
+// dynamics block (rx_steps); keys_last: the last step writes the re-sort keys
+// k_window workgroups the device holds at once (occupancy API x CUs, less one
+// workgroup per CU where the SGPR count makes the API over-report: MI355X_MICROARCH.md)
+extern "C" int rx_window_capacity(int device);
+// args: device buffer of RX_WIN_MAX_STEPS argument blocks (k_window_args fills n_steps of them)
+#define RX_WIN_MAX_STEPS 64
+extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last,
+                                rx_kargs* args, hipStream_t s);
 // persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024

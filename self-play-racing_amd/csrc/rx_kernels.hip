@@ -415,8 +415,8 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
 // (the one k_rays casts from).  Scheduling only: no result depends on it.
 constexpr int kTaskSectors = 64;
 template <int A>
-__device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
-                                                 int32_t* cnt, int32_t* stage) {
+__device__ __forceinline__ int sort_block_tasks_lds(const rx_kargs& a, int p, const double* ang, int32_t* cnt,
+                                                    int32_t* stage) {
   constexpr int kMaxT = 16 * A;  // rx_assign enforces n_sensors <= 16 for ray_order 2
   const int R = a.n_sensors, AR = A * R;
   const int lane = threadIdx.x & 63;
@@ -468,7 +468,17 @@ __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_sta
     a.io.counters[16 + 12 * (int)blockIdx.x + 11] = ts2;
   }
 #endif
-  int32_t* out = a.tasks_out + (size_t)perm_start * AR;
+  return total;
+}
+
+// the block's sorted task ids from the LDS row to tasks_out[perm_start*A*R ..],
+// 64-lane contiguous stores (k_kin1 / k_dyn; k_window's ray tasks read the row in place)
+template <int A>
+__device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
+                                                 int32_t* cnt, int32_t* stage) {
+  const int total = sort_block_tasks_lds<A>(a, p, ang, cnt, stage);
+  const int lane = threadIdx.x & 63;
+  int32_t* out = a.tasks_out + (size_t)perm_start * (A * a.n_sensors);
   for (int i = lane; i < total; i += 64) out[i] = stage[i];
 }
 
@@ -1679,15 +1689,17 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
   } while (0)
 #endif
 
+// One ray wave: the wave record `we` (slot, tasks [task_start, task_start + count)
+// of `tasks`: the ray-wave table's record and the global task buffer in k_step2 /
+// k_rays; in k_window a record built from the block and the block's sorted task row
+// in LDS).  `wave` only indexes the profiling stamps.
 template <int A, int LPR>
-__device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
-  if (wave >= a.n_ray_waves) return;
+__device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
 #ifdef RX_RAY_STAMPS
   unsigned long long rstamp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   rstamp[6] = wall_clock64();
   RAY_STAMP(0);
 #endif
-  const rx_wave we = a.ray_waves[wave];
   const int lane = threadIdx.x & 63;
   const int k = uniform(we.track);
   const int wp0 = uniform(a.tr.wp_off[k]);
@@ -1706,7 +1718,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   const int task = we.task_start + (own ? tl : count - 1);
   int env_local = 0, q, ray, pos;
   if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
-    const int t = a.tasks[task];
+    const int t = tasks[task];
     const int iq = t / R;
     ray = t - iq * R;
     pos = iq / A;
@@ -1839,6 +1851,12 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
   }
   const int e = a.perm[pos];
   a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
+}
+
+template <int A, int LPR>
+__device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
+  if (wave >= a.n_ray_waves) return;
+  rays_wave<A, LPR>(a, a.ray_waves[wave], a.tasks, wave);
 }
 
 // A ray wave of the table: at the schedule's LPR lanes per ray, or -- for the
@@ -1984,6 +2002,134 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     rays_dispatch<A, LPR>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
+}
+
+// ============================================================ k_window
+// K consecutive single-agent split steps in ONE launch (rx_steps; DESIGN.md §3
+// "Multi-step window").  Inside a re-sort window the only cross-env dependency of
+// RacingEnv.step is none at all: step t + 1 of a 64-env dynamics block needs only
+// that block's step t (its state rows, its done flags).  So a workgroup owns one
+// block for all K steps and runs, per step,
+//   phase K : wave 0 = dyn1_env<1, KIN> (next-step autoreset, actions, kinematics,
+//             the non-ray obs columns) and the block's ray-task direction sort into
+//             an LDS row (never stored: the ray tasks read it in place);
+//   phase R : the block's REWARD (dyn1_env<1, REWARD>) and its ray waves (the
+//             sorted row in classes of 64 tasks), handed to the workgroup's waves
+//             from an LDS counter -- REWARD first, then the classes centre-first
+//             (their chains are the longest: longest-processing-time order);
+// with a workgroup barrier after each phase.  The device functions are those of
+// k_kin1 / k_step2, called on the same rows with the same operands, so every
+// output is bit-identical to K x rx_step (scheduling only; the ray-task order
+// inside the block never changes a result).  What changes is the schedule: no
+// launch boundary between steps and no chip-wide drain per step -- while one
+// block waits on its slowest ray wave, the other blocks sharing the CU run.
+// Every workgroup must be resident at once to keep that (rx_assign sizes the
+// waves per workgroup, RX_WIN_WAVES, so the grid fits); the only inter-workgroup
+// state is the episode-statistics / re-sort-count atomics.  The re-sort (which
+// moves envs between blocks) ends a window: the last step writes the sort keys
+// (and the bin counts), the host launches the re-sort after it.
+#ifndef RX_WIN_WAVES
+#define RX_WIN_WAVES 4  // waves per workgroup (one 64-env block)
+#endif
+#ifndef RX_WIN_MINW
+#define RX_WIN_MINW 6  // min waves per SIMD (80 VGPRs): 6 workgroups of 4 waves per CU >= 1,029 blocks at 65,536 envs
+#endif
+constexpr int kWinWaves = RX_WIN_WAVES;
+
+// phase R task t (0 = REWARD, 1 .. n = ray class) -> ray class, centre first:
+// 5, 4, 6, 3, 7, ... for 11 classes (|2j - (n - 1)| ascending, lower j first)
+__device__ __forceinline__ int win_class(int t, int n) {
+  const int c = (n - 1) >> 1;  // centre class (lower one for even n)
+  const int i = t - 1, h = (i + 1) >> 1;
+  return (n & 1) ? ((i & 1) ? c - h : c + h) : ((i & 1) ? c + h : c - h);
+}
+
+// The per-step argument blocks of a window: step s's = the launch's with the io
+// rows of step s and the re-sort keys on the last step only.  Written by
+// k_window_args (one lane per step) into a handle buffer before k_window runs;
+// k_window reads step s's block through the constant address space, so its
+// fields are scalar loads like kernel arguments -- a block copied inside the
+// kernel kept ~40 modified or hoisted fields live in SGPRs across the step loop
+// (349 SGPR spills).
+__global__ void k_window_args(rx_kargs a, rx_io_strides st, int n_steps, int keys_last, rx_kargs* out) {
+  const int s = threadIdx.x;
+  if (s >= n_steps) return;
+  rx_kargs o = a;
+  o.io.actions = a.io.actions + (ptrdiff_t)s * st.actions;
+  o.io.obs = a.io.obs + (ptrdiff_t)s * st.obs;
+  if (a.io.reward) o.io.reward = a.io.reward + (ptrdiff_t)s * st.reward;
+  if (a.io.reward64) o.io.reward64 = a.io.reward64 + (ptrdiff_t)s * st.reward64;
+  if (a.io.terminated) o.io.terminated = a.io.terminated + (ptrdiff_t)s * st.terminated;
+  if (a.io.truncated) o.io.truncated = a.io.truncated + (ptrdiff_t)s * st.truncated;
+  if (a.io.done_f32) o.io.done_f32 = a.io.done_f32 + (ptrdiff_t)s * st.done_f32;
+  if (a.io.info) o.io.info = a.io.info + (ptrdiff_t)s * st.info;
+  if (a.io.ep_done) o.io.ep_done = a.io.ep_done + (ptrdiff_t)s * st.ep_done;
+  const bool keys = keys_last && s == n_steps - 1;
+  o.sort_keys = keys ? a.sort_keys : nullptr;
+  o.sort_hist = keys ? a.sort_hist : nullptr;
+  out[s] = o;
+}
+
+typedef const __attribute__((address_space(4))) rx_kargs* rx_ckargs;
+
+__global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx_kargs* args, int n_steps) {
+  const int b = uniform((int)blockIdx.x);  // dynamics block
+  const int wv = uniform((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  __shared__ int32_t tcnt[kTaskSectors];
+  __shared__ int32_t tstage[64 * 16];  // the block's direction-sorted ray tasks (A = 1: <= 64 x 16)
+  __shared__ int32_t next_task;        // phase R work counter
+  const rx_kargs& a0 = *(const rx_kargs*)(rx_ckargs)args;
+  if (b >= a0.n_dyn_waves) return;
+  // the block's record through the constant address space: scalar loads, SGPR results
+  typedef const __attribute__((address_space(4))) int32_t* rx_cip;
+  const rx_cip dwp = (rx_cip)(const int32_t*)(a0.dyn_waves + b);
+  const int dw_track = dwp[0], dw_perm = dwp[1];
+  const int n_tasks = dwp[3] * a0.n_sensors;
+  const int n_cls = (n_tasks + 63) >> 6;
+  const unsigned long long prof_t0 = prof_start(a0);
+  for (int s = 0; s < n_steps; ++s) {
+    const rx_kargs& as = *(const rx_kargs*)((rx_ckargs)args + s);
+    // ---- phase K (wave 0)
+    if (wv == 0) {
+      tcnt[lane] = 0;
+      double ang[1], ep[3] = {0.0, 0.0, 0.0};
+      int e = -1;
+      dyn1_env<1, RX_PART_KIN>(as, b, ang, e, ep);
+      sort_block_tasks_lds<1>(as, e, ang, tcnt, tstage);
+      if (lane == 0) next_task = 0;
+    }
+    __syncthreads();
+    // ---- phase R: REWARD and the ray classes over the workgroup's waves
+#ifdef RX_WIN_STATIC  // bring-up variant: task t on wave t % kWinWaves
+    for (int t = wv; t <= n_cls; t += kWinWaves) {
+#else
+    for (;;) {
+      // the wave takes the next task with ONE unconditional atomic from all 64 lanes
+      // (the loop head is uniform, every lane active): the compiler folds it into a
+      // single ds_add_rtn of 64 whose old value, a multiple of 64, every lane reads
+      // back into an SGPR -- so the loop exit is a scalar branch.  `if (lane == 0) t =
+      // atomicAdd(..)` + a cross-lane read was structurized into a nested divergent
+      // loop whose back edge skipped the atomic: the REWARD task ran forever (hung
+      // at 4,096 envs in 64-step windows); lane == 0 ? 1 : 0 from every lane was
+      // correct but cost a 64-iteration scan per task.
+      const int t = __builtin_amdgcn_readfirstlane(atomicAdd(&next_task, 1)) >> 6;
+      if (t > n_cls) break;
+#endif
+      if (t == 0) {
+        double ang[1], ep[3] = {0.0, 0.0, 0.0};
+        int e = -1;
+        dyn1_env<1, RX_PART_REWARD>(as, b, ang, e, ep);
+        add_episode_stats(as, ep);
+      } else {
+        const int j = win_class(t, n_cls);
+        const rx_wave rw{dw_track, dw_perm, 64 * j, min(64, n_tasks - 64 * j)};
+        rays_wave<1, 1>(as, rw, tstage, b);
+      }
+    }
+    __syncthreads();
+  }
+  if (wv == 0) prof_end(a0, b, prof_t0);
 }
 
 // ============================================================ k_rollout
@@ -2421,6 +2567,21 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else
       hipLaunchKernelGGL(k_rays<2>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_window_capacity(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window, 64 * kWinWaves, 0) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return per_cu * cus;
+}
+
+extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last,
+                                rx_kargs* args, hipStream_t s) {
+  if (n_steps < 1 || n_steps > RX_WIN_MAX_STEPS) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
+  hipLaunchKernelGGL(k_window, dim3(a->n_dyn_waves), dim3(64 * kWinWaves), 0, s, (const rx_kargs*)args, n_steps);
   return (int)hipGetLastError();
 }
 

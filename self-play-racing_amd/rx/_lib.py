@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -32,8 +32,8 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
            "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_set_start_draws",
-           "rx_rollout_steps", "rx_selfplay_rollout_steps")
-RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
+           "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps")
+RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward", "k_window")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
 RX_PREC_FP32, RX_PREC_BF16 = 0, 1
@@ -48,16 +48,17 @@ class RxConfig(ctypes.Structure):
                 ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)] + \
                [(k, ctypes.c_int32) for k in ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window",
                                                "seg_filter", "box_quadrants", "ray_dispatch", "ray_tail",
-                                               "ray_tail_lpr", "task_sort")]
+                                               "ray_tail_lpr", "task_sort", "window")]
 
 
-# rx_config launch-schedule fields (ABI v17, v19, v20): 0 = auto, -1 = off / none (include/rx.h).
+# rx_config launch-schedule fields (ABI v17, v19, v20, v21): 0 = auto, -1 = off / none (include/rx.h).
 # Scheduling only: every value gives bit-identical results.
-SCHEDULE_W = 15  # rx_schedule: resolved schedule (include/rx.h)
+SCHEDULE_W = 17  # rx_schedule: resolved schedule (include/rx.h)
 SCHEDULE_KEYS = ("split", "wide", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                 "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort")
+                 "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort",
+                 "window", "dyn_calls")
 SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort")
+                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "window")
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
@@ -74,6 +75,14 @@ IO_FIELDS = ("actions", "obs", "reward", "reward64", "terminated", "truncated", 
 
 class RxIO(ctypes.Structure):
     _fields_ = [(k, _P) for k in IO_FIELDS]
+
+
+# rx_steps (ABI v21): per-step element strides of the io rows
+STRIDE_FIELDS = ("actions", "obs", "reward", "reward64", "terminated", "truncated", "done_f32", "info", "ep_done")
+
+
+class RxIOStrides(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in STRIDE_FIELDS]
 
 
 class RxAdamConfig(ctypes.Structure):
@@ -141,6 +150,7 @@ def load(build_if_missing=True):
     L.rx_reset.argtypes = [_P, _P, ctypes.POINTER(RxIO), _P]
     L.rx_step.argtypes = [_P, ctypes.POINTER(RxIO), _P]
     L.rx_step_phases.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, _P]
+    L.rx_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, ctypes.POINTER(RxIOStrides), _P]
     gae_args = [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _P, _P]
     L.rx_gae.argtypes = gae_args
     L.rx_gae_scan.argtypes = gae_args

@@ -457,6 +457,46 @@ class RacingVectorEnv:
                 reward_out if reward_out is not None else self.buf["reward"],
                 done_out if done_out is not None else self.buf["done_f32"])
 
+    def steps_device(self, actions, obs_out=None, reward_out=None, done_out=None, full_info=False, stream=None):
+        """K consecutive steps from ONE call (rx_steps, ABI v21) with the actions of
+        every step given up front: ``actions`` [K, N, (A,) 2] float32 on the device.
+        Equal to K step_device calls on actions[0], ..., actions[K-1] bit for bit.
+        ``obs_out`` / ``reward_out`` / ``done_out``: None = the env's own rows (each
+        step overwrites them: they end with the last step's outputs), or [K, ...]
+        buffers whose row k receives step k.  Returns the last step's (obs, reward,
+        done_f32).  Where the schedule allows (single-agent split step at one lane per
+        ray), the steps between two spatial re-sorts run as ONE k_window launch."""
+        dev_idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        on_dev = lambda t: t.is_cuda and t.device.index == dev_idx  # noqa: E731  ("cuda" == "cuda:0")
+        if not isinstance(actions, torch.Tensor) or not on_dev(actions) or \
+                actions.dtype != torch.float32 or not actions.is_contiguous():
+            raise ValueError("steps_device takes a contiguous float32 device tensor of actions [K, N, (A,) 2]")
+        A, N = self.n_agents, self.num_envs
+        per = N * A * 2
+        if actions.numel() % per or actions.numel() == 0:
+            raise ValueError(f"actions must hold K x {N}x{A}x2 elements, got shape {tuple(actions.shape)}")
+        K = actions.numel() // per
+        row = {"obs": N * A * self.D, "reward": N * A, "done": N}
+
+        def rows(t, name):
+            if t is None:
+                return None, 0
+            if not t.is_contiguous() or not on_dev(t) or t.numel() != K * row[name]:
+                raise ValueError(f"{name}_out must be a contiguous device tensor of {K} x {row[name]} elements")
+            return t, row[name]
+
+        obs_t, so = rows(obs_out, "obs")
+        rew_t, sr = rows(reward_out, "reward")
+        done_t, sd = rows(done_out, "done")
+        io = self._io(actions=actions, obs=obs_t, reward=rew_t, done=done_t, full=full_info)
+        st = _lib.RxIOStrides(actions=per, obs=so, reward=sr, done_f32=sd)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with self.start_draw_session(K * N):
+            _lib.check(self.L.rx_steps(self._h, io, int(K), ctypes.byref(st), s.cuda_stream), "rx_steps")
+        self._launched(s)
+        last = lambda t, n, name: self.buf[name] if t is None else t.view(K, -1)[K - 1]  # noqa: E731
+        return last(obs_t, so, "obs"), last(rew_t, sr, "reward"), last(done_t, sd, "done_f32")
+
     def episode_stats(self, reset=True):
         """(sum of returns, sum of lengths, count) of episodes that ended since the
         last call -- one device->host copy."""

@@ -57,6 +57,11 @@ def test_integration_binding_matches_vector_env():
         assert torch.equal(ob, ov) and torch.equal(rb, rv) and torch.equal(db, dv), t
         ends += int(db.sum())
     assert ends > 50
+    # rx_steps through the binding (ABI v21): 24 open-loop steps from one call each side
+    a = torch.rand((24, N, 2), device="cuda", generator=g) * scale + shift
+    ob, rb, db = step.steps(a)
+    ov, rv, dv = v.steps_device(a)
+    assert torch.equal(ob, ov) and torch.equal(rb, rv) and torch.equal(db, dv)
     v.close()
     keep_h = keep[0]
     assert ns["L"].rx_destroy(keep_h) == 0
