@@ -122,7 +122,8 @@ typedef struct {
   /* ABI v21: rx_steps runs consecutive single-agent split steps as multi-step windows (k_window: a
      workgroup per 64-env block for all steps between two spatial re-sorts) where the schedule allows
      (one lane per ray and per env in REWARD, ray_order 2, task_sort 1); elsewhere, or with -1, it
-     enqueues the per-step launches of rx_step.  0 auto (on), 1 on, -1 off.  Scheduling only. */
+     enqueues the per-step launches of rx_step.  0 auto (off: measured slower at 65,536 envs, the
+     slowest blocks' 8-step chains end the window -- DESIGN.md §3), 1 on, -1 off.  Scheduling only. */
   int32_t window;
 } rx_config;
 

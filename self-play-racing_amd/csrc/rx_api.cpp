@@ -687,7 +687,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   // resident at once (a workgroup that waits for a free slot would run its whole window after
   // the others: the launch would take twice as long)
   h->window = false;
-  if (c.window >= 0 && A == 1 && h->split && h->cfg.ray_order == 2 && h->ray_lpr == 1 && h->reward_lpe == 1 &&
+  if (c.window > 0 && A == 1 && h->split && h->cfg.ray_order == 2 && h->ray_lpr == 1 && h->reward_lpe == 1 &&
       h->task_sort == 1 && h->dyn_lpe == 1 && R <= 16 && h->cfg.autoreset != RX_AUTORESET_SAME_STEP) {
     if (h->window_cap == 0) {
       RX_HIP(hipSetDevice(h->cfg.device));

@@ -2034,6 +2034,9 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
 #ifndef RX_WIN_MINW
 #define RX_WIN_MINW 6  // min waves per SIMD (80 VGPRs): 6 workgroups of 4 waves per CU >= 1,029 blocks at 65,536 envs
 #endif
+#ifndef RX_WIN_PSORT
+#define RX_WIN_PSORT 1  // phase K's ray-task ranking spread over the workgroup's waves
+#endif
 constexpr int kWinWaves = RX_WIN_WAVES;
 
 // phase R task t (0 = REWARD, 1 .. n = ray class) -> ray class, centre first:
@@ -2079,6 +2082,10 @@ __global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx
   __shared__ int32_t tcnt[kTaskSectors];
   __shared__ int32_t tstage[64 * 16];  // the block's direction-sorted ray tasks (A = 1: <= 64 x 16)
   __shared__ int32_t next_task;        // phase R work counter
+#if RX_WIN_PSORT
+  __shared__ double sAng[64];  // phase K: the block's stepped angles and positions (-1: no env) for the ranking
+  __shared__ int32_t sPos[64];
+#endif
   const rx_kargs& a0 = *(const rx_kargs*)(rx_ckargs)args;
   if (b >= a0.n_dyn_waves) return;
   // the block's record through the constant address space: scalar loads, SGPR results
@@ -2090,7 +2097,56 @@ __global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx
   const unsigned long long prof_t0 = prof_start(a0);
   for (int s = 0; s < n_steps; ++s) {
     const rx_kargs& as = *(const rx_kargs*)((rx_ckargs)args + s);
-    // ---- phase K (wave 0)
+    // ---- phase K: wave 0 steps the block's kinematics
+#if RX_WIN_PSORT
+    // ... and every wave ranks the ray tasks of its share of the sensors (ray r on
+    // wave r % kWinWaves; the LDS counting sort of sort_block_tasks_lds with the
+    // ranking spread over the workgroup: 704 tasks on 4 x 64 lanes, not 64).  The
+    // order inside a sector is the atomics' order either way: scheduling only.
+    if (wv == 0) {
+      tcnt[lane] = 0;
+      double ang[1], ep[3] = {0.0, 0.0, 0.0};
+      int e = -1;
+      dyn1_env<1, RX_PART_KIN>(as, b, ang, e, ep);
+      sAng[lane] = ang[0];
+      sPos[lane] = e;
+      if (lane == 0) next_task = 0;
+    }
+    __syncthreads();
+    constexpr int kRW = (16 + kWinWaves - 1) / kWinWaves;  // rays per wave (n_sensors <= 16)
+    const int R = a0.n_sensors;
+    const int p_l = sPos[lane];
+    const double ang_l = sAng[lane];
+    const float inv = (float)kTaskSectors * 0.15915494309189535f;  // sectors per radian
+    int pk[kRW];
+#pragma unroll
+    for (int i = 0; i < kRW; ++i) {
+      const int r = wv + kWinWaves * i;
+      pk[i] = -1;
+      if (r < R && p_l >= 0) {
+        const float th = (float)(ang_l + as.rel_angles[r]);
+        const int sec = (int)__builtin_floorf(th * inv) & (kTaskSectors - 1);
+        pk[i] = (atomicAdd(&tcnt[sec], 1) << 6) | sec;
+      }
+    }
+    __syncthreads();
+    if (wv == 0) {  // sector counts -> exclusive offsets
+      const int c0 = tcnt[lane];
+      int c = c0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(c, o, 64);
+        if (lane >= o) c += v;
+      }
+      tcnt[lane] = c - c0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kRW; ++i)
+      if (pk[i] >= 0) tstage[tcnt[pk[i] & 63] + (pk[i] >> 6)] = p_l * R + wv + kWinWaves * i;  // task (A p + q) R + r
+    __syncthreads();
+#else
+    // ... and sorts its ray tasks (sort_block_tasks_lds)
     if (wv == 0) {
       tcnt[lane] = 0;
       double ang[1], ep[3] = {0.0, 0.0, 0.0};
@@ -2100,6 +2156,7 @@ __global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx
       if (lane == 0) next_task = 0;
     }
     __syncthreads();
+#endif
     // ---- phase R: REWARD and the ray classes over the workgroup's waves
 #ifdef RX_WIN_STATIC  // bring-up variant: task t on wave t % kWinWaves
     for (int t = wv; t <= n_cls; t += kWinWaves) {
@@ -2570,9 +2627,16 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   return (int)hipGetLastError();
 }
 
+// Dynamic LDS requested by every k_window workgroup beyond its static rows: it
+// only caps the workgroups a CU admits (the hardware packs workgroups onto CUs as
+// long as resources allow, it does not spread them evenly).  A/B knob.
+#ifndef RX_WIN_LDS_PAD
+#define RX_WIN_LDS_PAD 0
+#endif
 extern "C" int rx_window_capacity(int device) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window, 64 * kWinWaves, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window, 64 * kWinWaves, RX_WIN_LDS_PAD) != hipSuccess)
+    return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
 }
@@ -2581,7 +2645,8 @@ extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int 
                                 rx_kargs* args, hipStream_t s) {
   if (n_steps < 1 || n_steps > RX_WIN_MAX_STEPS) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
-  hipLaunchKernelGGL(k_window, dim3(a->n_dyn_waves), dim3(64 * kWinWaves), 0, s, (const rx_kargs*)args, n_steps);
+  hipLaunchKernelGGL(k_window, dim3(a->n_dyn_waves), dim3(64 * kWinWaves), RX_WIN_LDS_PAD, s, (const rx_kargs*)args,
+                     n_steps);
   return (int)hipGetLastError();
 }
 

@@ -132,7 +132,7 @@ def test_window_65536_subset_bit_exact_vs_oracle(oracle_dev):
     from tests.test_fullsize_gpu import REL1, _oracle_table
     N = 65536
     pool, widths = _seed1_pool(N)
-    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step")
+    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(window=1))
     assert v.schedule()["window"] == 1
     idx = np.sort(np.random.default_rng(23).choice(N, 2048, replace=False))
     tab = _oracle_table(v)
@@ -178,9 +178,9 @@ def test_window_graph_replay_equals_eager():
     pool, widths = _seed1_pool(16384)
     from rx.vector_env import RacingVectorEnv
     va = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(ray_lpr=1, reward_lpe=1,
-                                                                                          task_sort=1))
+                                                                                          task_sort=1, window=1))
     vb = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(ray_lpr=1, reward_lpe=1,
-                                                                                          task_sort=1))
+                                                                                          task_sort=1, window=1))
     assert va.schedule()["window"] == 1
     va.reset_device()
     vb.reset_device()

@@ -56,15 +56,30 @@ def main():
             torch.cuda.synchronize()
             res[w].append(N * K / (time.perf_counter() - t0))
     prof = {}
+    wg = None
     for w, v in envs.items():
         v.profile(1)
         v.steps_device(bank[args.burn:args.burn + 64])
         prof[w] = {k: [round(x[0] * 1e3, 2), x[1]] for k, x in v.profile_read().items()}
         v.profile(0)
+        if w == 1 and "k_window" in prof[w]:
+            durs, ends = [], []
+            for k in range(prof[w]["k_window"][1]):
+                st, en, kind, _ = v.profile_waves(k)
+                live = np.isfinite(st) & np.isfinite(en)
+                durs.append(en[live] - st[live])
+                ends.append(en[live])
+            d = np.concatenate(durs)
+            e = np.concatenate(ends)
+            wg = {"wg_dur_us_percentiles": [round(float(np.percentile(d, q)), 1) for q in (0, 10, 25, 50, 75, 90, 99, 100)],
+                  "wg_end_us_percentiles": [round(float(np.percentile(e, q)), 1) for q in (0, 10, 25, 50, 75, 90, 99, 100)],
+                  "hist_dur_us": np.histogram(d, bins=12)[0].tolist(),
+                  "hist_edges_us": [round(float(x), 1) for x in np.histogram(d, bins=12)[1]]}
     out = {"label": args.label, "envs": N, "steps": K, "schedule_on": envs[1].schedule(),
            "window_on_Msteps": [round(x / 1e6, 1) for x in res[1]],
            "window_off_Msteps": [round(x / 1e6, 1) for x in res[-1]],
-           "kernel_us_on": prof[1], "kernel_us_off": prof[-1]}
+           "kernel_us_on": prof[1], "kernel_us_off": prof[-1], "window_workgroups": wg,
+           "lib": os.environ.get("RX_LIB_PATH", "default")}
     print(json.dumps(out), flush=True)
 
 
