@@ -123,7 +123,9 @@ typedef struct {
      workgroup per 64-env block for all steps between two spatial re-sorts) where the schedule allows
      (one lane per ray and per env in REWARD, ray_order 2, task_sort 1); elsewhere, or with -1, it
      enqueues the per-step launches of rx_step.  0 auto (off: measured slower at 65,536 envs, the
-     slowest blocks' 8-step chains end the window -- DESIGN.md §3), 1 on, -1 off.  Scheduling only. */
+     slowest blocks' 8-step chains end the window -- DESIGN.md §3), 1 on, 2 k_flow (the window's steps
+     as a task graph over per-XCD ready queues: any wave runs any ready (step, block) task), -1 off.
+     Scheduling only. */
   int32_t window;
 } rx_config;
 
@@ -285,6 +287,9 @@ typedef struct {
   int64_t actions, obs, reward, reward64, terminated, truncated, done_f32, info, ep_done;
 } rx_io_strides;
 int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* strides, void* stream);
+/* Diagnostics (ABI v21): nonzero when a k_flow wave gave up waiting for a task (a bounded spin
+ * timed out: the launch's results are incomplete).  Synchronises the device. */
+int rx_flow_errors(rx_env* h, int32_t* out);
 
 /* rx_step split into its two kernels, for per-kernel timing with stream
  * events: phases bit 0 = dynamics/reward/done/autoreset (k_dyn), bit 1 =

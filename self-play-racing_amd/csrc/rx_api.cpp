@@ -107,9 +107,12 @@ struct rx_env {
   int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
   int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
   int32_t task_sort = 1;                   // ray-task direction sort every task_sort dynamics launches
-  bool window = false;                     // rx_steps runs k_window (multi-step windows), rx_assign's choice
+  int32_t window = 0;                      // rx_steps: 0 per-step launches, 1 k_window, 2 k_flow (rx_assign's choice)
   int32_t window_cap = 0;                  // k_window workgroups resident at once (occupancy x CUs)
-  DevBuf<rx_kargs> win_args;               // k_window's per-step argument blocks [RX_WIN_MAX_STEPS]
+  DevBuf<rx_kargs> win_args;               // k_window / k_flow per-step argument blocks [RX_WIN_MAX_STEPS]
+  int32_t flow_grid = 0;                   // k_flow one-wave workgroups (resident capacity)
+  DevBuf<int32_t> flow_q, flow_ctl, flow_cnt;  // k_flow queues [8][cap], control words, block arrival counters
+  int32_t flow_cap = 0;
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -327,7 +330,8 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
-  if (!tri(cfg->window)) return fail(RX_EINVAL, "window must be 0 (auto), 1 or -1 (got %d)", cfg->window);
+  if (cfg->window < -1 || cfg->window > 2)
+    return fail(RX_EINVAL, "window must be 0 (auto), 1 (k_window), 2 (k_flow) or -1 (got %d)", cfg->window);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
     return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
@@ -401,7 +405,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort, h->window ? 1 : 0, (int32_t)h->dyn_calls};
+                                    h->task_sort, h->window, (int32_t)h->dyn_calls};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -417,6 +421,9 @@ int rx_destroy(rx_env* h) {
     b->release();
   h->cs_scratch.release();
   h->win_args.release();
+  h->flow_q.release();
+  h->flow_ctl.release();
+  h->flow_cnt.release();
   h->prof_buf.release();
   h->resets.release();
   h->draw_rank.release();
@@ -686,18 +693,42 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   // per env and per ray with the direction sort every launch, and every block's workgroup
   // resident at once (a workgroup that waits for a free slot would run its whole window after
   // the others: the launch would take twice as long)
-  h->window = false;
+  h->window = 0;
   if (c.window > 0 && A == 1 && h->split && h->cfg.ray_order == 2 && h->ray_lpr == 1 && h->reward_lpe == 1 &&
       h->task_sort == 1 && h->dyn_lpe == 1 && R <= 16 && h->cfg.autoreset != RX_AUTORESET_SAME_STEP) {
-    if (h->window_cap == 0) {
-      RX_HIP(hipSetDevice(h->cfg.device));
-      h->window_cap = rx_window_capacity(h->cfg.device);
+    RX_HIP(hipSetDevice(h->cfg.device));
+    if (c.window == 1) {
+      if (h->window_cap == 0) h->window_cap = rx_window_capacity(h->cfg.device);
+      h->window = h->n_dyn_waves <= h->window_cap ? 1 : 0;
+    } else {
+      h->flow_grid = rx_flow_capacity(h->cfg.device);
+      h->window = h->flow_grid >= 8 ? 2 : 0;
     }
-    h->window = h->n_dyn_waves <= h->window_cap;
-    if (h->window && !h->win_args.p) {  // here, not in rx_steps: no allocation may happen inside a graph capture
+    // allocations here, not in rx_steps: none may happen inside a graph capture
+    if (h->window && !h->win_args.p) {
       if (hipMalloc(&h->win_args.p, RX_WIN_MAX_STEPS * sizeof(rx_kargs)) != hipSuccess)
         return fail(RX_ENOMEM, "rx_assign: window argument blocks");
       h->win_args.n = RX_WIN_MAX_STEPS;
+    }
+    if (h->window == 2) {  // k_flow queues: per XCD (block b on queue b % 8) every task of a 64-step window
+      int per_step[8] = {0};
+      for (size_t b = 0; b < dyn.size(); ++b) per_step[b % 8] += 2 + (dyn[b].count * R + 63) / 64;
+      int mx = 0;
+      for (int x = 0; x < 8; ++x) mx = std::max(mx, per_step[x]);
+      h->flow_cap = mx * RX_WIN_MAX_STEPS;
+      h->flow_q.release();
+      h->flow_cnt.release();
+      if (hipMalloc(&h->flow_q.p, (size_t)8 * h->flow_cap * sizeof(int32_t)) != hipSuccess ||
+          hipMalloc(&h->flow_cnt.p, dyn.size() * sizeof(int32_t)) != hipSuccess)
+        return fail(RX_ENOMEM, "rx_assign: k_flow queues");
+      h->flow_q.n = (size_t)8 * h->flow_cap;
+      h->flow_cnt.n = dyn.size();
+      if (!h->flow_ctl.p) {
+        if (hipMalloc(&h->flow_ctl.p, RX_FLOW_CTL * sizeof(int32_t)) != hipSuccess)
+          return fail(RX_ENOMEM, "rx_assign: k_flow control words");
+        RX_HIP(hipMemset(h->flow_ctl.p, 0, RX_FLOW_CTL * sizeof(int32_t)));
+        h->flow_ctl.n = RX_FLOW_CTL;
+      }
     }
   }
   h->assigned = true;
@@ -1125,7 +1156,7 @@ int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* s
     rx_kargs a{};
     const rx_io o = io_at(io, st, k);
     make_kargs(h, &o, RX_MODE_STEP, nullptr, a);
-    a.tasks_out = nullptr;  // the window's ray tasks live in LDS
+    if (h->window == 1) a.tasks_out = nullptr;  // k_window's ray tasks live in LDS (k_flow's in the task buffer)
     if (keys) {
       if (h->sort_hist_done) {  // counts of keys a previous launch wrote and no sort consumed
         RX_HIP(hipMemsetAsync(h->sort_hist.p, 0, (size_t)h->sort_bins * sizeof(uint32_t), s));
@@ -1136,8 +1167,13 @@ int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* s
       a.sort_off = h->keys_off.p;
     }
     prof_arm(h, a, RX_KERNEL_WINDOW);
-    if ((rc = rx_launch_window(&a, &st, len, keys ? 1 : 0, h->win_args.p, s)) != 0)
+    if (h->window == 2) {
+      const rx_flow f{h->flow_q.p, h->flow_ctl.p, h->flow_cnt.p, h->flow_cap, len};
+      if ((rc = rx_launch_flow(&a, &st, len, keys ? 1 : 0, h->win_args.p, &f, h->flow_grid, s)) != 0)
+        return fail(RX_EHIP, "k_flow launch failed: %s", hipGetErrorString((hipError_t)rc));
+    } else if ((rc = rx_launch_window(&a, &st, len, keys ? 1 : 0, h->win_args.p, s)) != 0) {
       return fail(RX_EHIP, "k_window launch failed: %s", hipGetErrorString((hipError_t)rc));
+    }
     h->dyn_calls += (uint64_t)len;
     h->task_calls += (uint64_t)len;
     h->tasks_stale = true;  // the global task buffer holds no order of these states
@@ -1149,6 +1185,16 @@ int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* s
     }
     k += len;
   }
+  return RX_OK;
+}
+
+int rx_flow_errors(rx_env* h, int32_t* out) {
+  if (!h || !out) return fail(RX_EINVAL, "rx_flow_errors: null argument");
+  *out = 0;
+  if (!h->flow_ctl.p) return RX_OK;
+  RX_HIP(hipSetDevice(h->cfg.device));
+  RX_HIP(hipDeviceSynchronize());
+  RX_HIP(hipMemcpy(out, h->flow_ctl.p + 256, sizeof(int32_t), hipMemcpyDeviceToHost));
   return RX_OK;
 }
 

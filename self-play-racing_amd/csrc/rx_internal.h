@@ -187,6 +187,22 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
 // k_window: n_steps single-agent split steps in one launch, a workgroup per
 // dynamics block (rx_steps); keys_last: the last step writes the re-sort keys
+// k_flow (rx_steps with rx_config.window = 2): the steps of a window as a task
+// graph over per-XCD ready queues.  q: [8][cap] task codes (-1 = not yet pushed);
+// ctl: per XCD x, at 32 x: head, tail (both in units of 64 per entry: one full-wave
+// atomic per pop / push), tasks of the window; ctl[256]: error flags (bounded-spin
+// timeouts; 0 = none); cnt: [n_blocks] arrival counters (64 per task).
+#define RX_FLOW_CTL 512
+struct rx_flow {
+  int32_t* q;
+  int32_t* ctl;
+  int32_t* cnt;
+  int32_t cap;      // queue entries per XCD
+  int32_t n_steps;  // steps of this window
+};
+extern "C" int rx_launch_flow(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last, rx_kargs* args,
+                              const rx_flow* f, int grid, hipStream_t s);
+extern "C" int rx_flow_capacity(int device);
 // k_window workgroups the device holds at once (occupancy API x CUs, less one
 // workgroup per CU where the SGPR count makes the API over-report: MI355X_MICROARCH.md)
 extern "C" int rx_window_capacity(int device);

@@ -56,6 +56,27 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
+// State accesses of the env device functions.  C = false: plain loads and stores.
+// C = true (k_flow: a block's steps run as tasks on waves of any CU of its XCD, so
+// the state rows are handed from workgroup to workgroup): every load and store of
+// handed-off bytes is a global_load / global_store with sc1 -- the hand-off form of
+// MI355X_MICROARCH.md "Valid forms" (row 1: sc1 stores, vmcnt(0) before the flag,
+// sc1 loads after the poll; the L1 of the reading CU is never consulted).
+template <bool C, class T>
+__device__ __forceinline__ T ldc(const T* p) {
+  if constexpr (C)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+template <bool C, class T, class U>
+__device__ __forceinline__ void stc(T* p, U v) {
+  if constexpr (C)
+    __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = (T)v;
+}
+
 // f32 np.clip with Python-float bounds (stays float32 under NEP 50)
 // Load of track-table data at a wave-uniform address through the constant
 // address space: the tables are never written by a kernel, and the cast lets
@@ -473,13 +494,13 @@ __device__ __forceinline__ int sort_block_tasks_lds(const rx_kargs& a, int p, co
 
 // the block's sorted task ids from the LDS row to tasks_out[perm_start*A*R ..],
 // 64-lane contiguous stores (k_kin1 / k_dyn; k_window's ray tasks read the row in place)
-template <int A>
+template <int A, bool C = false>
 __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
                                                  int32_t* cnt, int32_t* stage) {
   const int total = sort_block_tasks_lds<A>(a, p, ang, cnt, stage);
   const int lane = threadIdx.x & 63;
   int32_t* out = a.tasks_out + (size_t)perm_start * (A * a.n_sensors);
-  for (int i = lane; i < total; i += 64) out[i] = stage[i];
+  for (int i = lane; i < total; i += 64) stc<C>(out + i, stage[i]);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -539,7 +560,7 @@ struct rx_slot_lds {
   const double4* seg;
 };
 
-template <int LPE, int PART>
+template <int LPE, int PART, bool C = false>
 __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
                                          int sub_block = 0, const rx_slot_lds* sl = nullptr) {
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
@@ -569,29 +590,28 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   int e = REW ? -1 : a.perm[p];  // REWARD: loaded after the argmins
 
   const rx_state& S = a.st;
-  uint8_t ef = S.env_flags[p];
-  uint8_t fl = S.flags[p];
+  uint8_t ef = ldc<C>(S.env_flags + p);
+  uint8_t fl = ldc<C>(S.flags + p);
   // every per-env load up front, so their latencies overlap (not one round
   // trip per use) -- except in the REWARD half, which runs under the raycast
   // at the raycast's 64-VGPR budget: its values not needed by the argmins
   // (velocity, last progress, episode counters, steps) load after them, so
   // they are not live across the argmin loops (fewer spills)
-  Car c{S.x[p], S.y[p], REW ? 0.0 : S.angle[p], REW ? 0.0 : S.vx[p], REW ? 0.0 : S.vy[p], S.progress[p],
+  Car c{ldc<C>(S.x + p), ldc<C>(S.y + p), REW ? 0.0 : ldc<C>(S.angle + p), REW ? 0.0 : ldc<C>(S.vx + p), REW ? 0.0 : ldc<C>(S.vy + p), ldc<C>(S.progress + p),
         (fl & RX_F_CRASHED) != 0};
-  double last_steering = REW ? 0.0 : S.last_steering[p];
+  double last_steering = REW ? 0.0 : ldc<C>(S.last_steering + p);
   const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
   const float2 act =
       (step_mode && !REW) ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
-  double last_progress = (KIN || REW) ? 0.0 : S.last_progress[p];
-  double ep_ret0 = (KIN || REW) ? 0.0 : S.ep_return[p];
-  int ep_len0 = (KIN || REW) ? 0 : S.ep_length[p];
+  double last_progress = (KIN || REW) ? 0.0 : ldc<C>(S.last_progress + p);
+  double ep_ret0 = (KIN || REW) ? 0.0 : ldc<C>(S.ep_return + p);
+  int ep_len0 = (KIN || REW) ? 0 : ldc<C>(S.ep_length + p);
   double speed_w = (KIN || REW) ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);  // caller's, env order
-  int steps = REW ? 0 : S.steps[p];  // REWARD: already advanced by KIN
+  int steps = REW ? 0 : ldc<C>(S.steps + p);  // REWARD: already advanced by KIN
   double cs[2] = {0.0, 0.0};
   if (REW) {
-    const double2 sc = reinterpret_cast<const double2*>(a.cs_scratch)[p];
-    cs[0] = sc.x;
-    cs[1] = sc.y;
+    cs[0] = ldc<C>(a.cs_scratch + 2 * p);
+    cs[1] = ldc<C>(a.cs_scratch + 2 * p + 1);
   }
   RX_STAMP(1);
   bool do_reset;
@@ -666,13 +686,13 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   if constexpr (REW) __asm__ volatile("" : "+v"(p));
   if (REW) {  // the REWARD half's late loads (see above)
     e = a.perm[p];
-    c.vx = S.vx[p];
-    c.vy = S.vy[p];
-    last_progress = S.last_progress[p];
-    ep_ret0 = S.ep_return[p];
-    ep_len0 = S.ep_length[p];
+    c.vx = ldc<C>(S.vx + p);
+    c.vy = ldc<C>(S.vy + p);
+    last_progress = ldc<C>(S.last_progress + p);
+    ep_ret0 = ldc<C>(S.ep_return + p);
+    ep_len0 = ldc<C>(S.ep_length + p);
     speed_w = S.speed_weight ? S.speed_weight[e] : a.speed_weight;
-    steps = S.steps[p];
+    steps = ldc<C>(S.steps + p);
   }
   bool ended = false;
   double epr = 0.0, epl_d = 0.0;
@@ -708,8 +728,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     epr = ep_ret0 + r;
     const int epl = ep_len0 + 1;
     epl_d = (double)epl;
-    S.ep_return[p] = epr;
-    S.ep_length[p] = epl;
+    stc<C>(S.ep_return + p, epr);
+    stc<C>(S.ep_length + p, epl);
     ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
@@ -739,8 +759,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     last_steering = 0.0;
     ef &= (uint8_t)~RX_EF_PENDING_RESET;
     if (KIN) ef |= RX_EF_RESET_NOW;
-    S.ep_return[p] = 0.0;
-    S.ep_length[p] = 0;
+    stc<C>(S.ep_return + p, 0.0);
+    stc<C>(S.ep_length + p, 0);
     if (a.io.info && (a.mode == RX_MODE_RESET || a.autoreset == RX_AUTORESET_NEXT_STEP)) {
       double* inf = a.io.info + (size_t)e * RX_INFO_W;
       inf[RX_INFO_SPEED] = 0.0;
@@ -751,41 +771,48 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
   if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
   if (FULL && (stepping || do_reset)) {
-    S.x[p] = c.x;
-    S.y[p] = c.y;
-    S.angle[p] = c.angle;
-    S.vx[p] = c.vx;
-    S.vy[p] = c.vy;
-    S.progress[p] = c.progress;
-    S.last_progress[p] = c.progress;  // racing_env.py:165 (0.0 after reset)
-    S.last_steering[p] = last_steering;
-    S.steps[p] = steps;
-    S.flags[p] = fl;
-    S.env_flags[p] = ef;
+    stc<C>(S.x + p, c.x);
+    stc<C>(S.y + p, c.y);
+    stc<C>(S.angle + p, c.angle);
+    stc<C>(S.vx + p, c.vx);
+    stc<C>(S.vy + p, c.vy);
+    stc<C>(S.progress + p, c.progress);
+    stc<C>(S.last_progress + p, c.progress);  // racing_env.py:165 (0.0 after reset)
+    stc<C>(S.last_steering + p, last_steering);
+    stc<C>(S.steps + p, steps);
+    stc<C>(S.flags + p, fl);
+    stc<C>(S.env_flags + p, ef);
   }
   if (KIN && (stepping || do_reset)) {
-    S.x[p] = c.x;
-    S.y[p] = c.y;
-    S.angle[p] = c.angle;
-    S.vx[p] = c.vx;
-    S.vy[p] = c.vy;
-    S.last_steering[p] = last_steering;
-    S.steps[p] = steps;
-    if (moving) reinterpret_cast<double2*>(a.cs_scratch)[p] = make_double2(cs[0], cs[1]);
+    stc<C>(S.x + p, c.x);
+    stc<C>(S.y + p, c.y);
+    stc<C>(S.angle + p, c.angle);
+    stc<C>(S.vx + p, c.vx);
+    stc<C>(S.vy + p, c.vy);
+    stc<C>(S.last_steering + p, last_steering);
+    stc<C>(S.steps + p, steps);
+    if (moving) {
+      if constexpr (C) {
+        stc<C>(a.cs_scratch + 2 * p, cs[0]);
+        stc<C>(a.cs_scratch + 2 * p + 1, cs[1]);
+      } else {
+        reinterpret_cast<double2*>(a.cs_scratch)[p] = make_double2(cs[0], cs[1]);
+      }
+    }
     if (do_reset) {
-      S.progress[p] = 0.0;
-      S.last_progress[p] = 0.0;
-      S.flags[p] = fl;
-      S.env_flags[p] = ef;
+      stc<C>(S.progress + p, 0.0);
+      stc<C>(S.last_progress + p, 0.0);
+      stc<C>(S.flags + p, fl);
+      stc<C>(S.env_flags + p, ef);
     }
   }
   if (REW && (stepping || do_reset)) {
     if (stepping) {
-      S.progress[p] = c.progress;
-      S.last_progress[p] = c.progress;  // racing_env.py:165
-      S.flags[p] = fl;
+      stc<C>(S.progress + p, c.progress);
+      stc<C>(S.last_progress + p, c.progress);  // racing_env.py:165
+      stc<C>(S.flags + p, fl);
     }
-    S.env_flags[p] = ef;
+    stc<C>(S.env_flags + p, ef);
   }
   RX_STAMP(7);
   // ---------------------------------------------------------------- outputs
@@ -1693,7 +1720,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 // of `tasks`: the ray-wave table's record and the global task buffer in k_step2 /
 // k_rays; in k_window a record built from the block and the block's sorted task row
 // in LDS).  `wave` only indexes the profiling stamps.
-template <int A, int LPR>
+template <int A, int LPR, bool C = false>
 __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
 #ifdef RX_RAY_STAMPS
   unsigned long long rstamp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1718,7 +1745,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   const int task = we.task_start + (own ? tl : count - 1);
   int env_local = 0, q, ray, pos;
   if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
-    const int t = tasks[task];
+    const int t = ldc<C>(tasks + task);
     const int iq = t / R;
     ray = t - iq * R;
     pos = iq / A;
@@ -1737,8 +1764,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   }
   if (a.ray_order != 2) pos = we.perm_start + env_local;
   const int i = A * pos + q;  // working state (position order); the obs row is A * perm[pos] + q
-  const double ox = a.st.x[i], oy = a.st.y[i];
-  const double theta = a.st.angle[i] + a.rel_angles[ray];  // racing_env.py:50
+  const double ox = ldc<C>(a.st.x + i), oy = ldc<C>(a.st.y + i);
+  const double theta = ldc<C>(a.st.angle + i) + a.rel_angles[ray];  // racing_env.py:50
   RAY_STAMP(1);
   double sn, cs;
   rx_sincos(theta, &sn, &cs);
@@ -1768,7 +1795,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     const float csf = (float)cs, snf = (float)sn;
     const rx_f2 id2 = {1.0f / csf, 1.0f / snf};
     // visit chunks outward from the wave's first car
-    int w0 = (int)(a.st.progress[i] * (double)W + 0.5);
+    int w0 = (int)(ldc<C>(a.st.progress + i) * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
     const int c0 = uniform(w0 / G);
     // direction quadrant (sign bits of the f32 direction, as id2's signs): a
@@ -2187,6 +2214,131 @@ __global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx
     __syncthreads();
   }
   if (wv == 0) prof_end(a0, b, prof_t0);
+}
+
+// ============================================================ k_flow
+// The same steps as k_window, scheduled as a task graph (rx_config.window = 2;
+// DESIGN.md §3 "Task-graph windows").  k_window keeps a block on one workgroup
+// for the whole window, so the window ends with the slowest block's 8-step chain
+// (its workgroups' durations spread 280-800 us at 65,536 envs).  Here every
+// (step, block) has the tasks of the split step -- KIN (dyn1_env<1, KIN> + the
+// block's ray-task sort), REWARD, and the block's ray classes -- and any wave of
+// the block's XCD runs any ready one: KIN(b, s) is ready when REWARD and every ray
+// class of (b, s - 1) have arrived (the last arrival pushes it), REWARD / rays of
+// (b, s) when KIN(b, s) is done (it pushes them).  One-wave workgroups pop task
+// codes from their XCD's queue (s_getreg XCC_ID; block b lives on queue b % 8,
+// so a block's tasks all run under one L2); the state rows a task hands to the
+// next go through sc1 stores and sc1 loads (ldc / stc, C = true) with the
+// storing wave's vmcnt(0) before the push or arrival -- MI355X_MICROARCH.md
+// "Valid forms", row 1.  Every wave of the window is a persistent worker; a
+// wave exits when its XCD's pops pass the window's task count.  Every spin is
+// bounded (the flag in ctl[256] records a timeout; rx_flow_errors reads it).
+// Bit-identical to K x rx_step by the same argument as k_window.
+#ifndef RX_FLOW_MINW
+#define RX_FLOW_MINW 6
+#endif
+#ifndef RX_FLOW_SLEEP
+#define RX_FLOW_SLEEP 2  // s_sleep between polls of an empty queue entry (x 64 cycles)
+#endif
+#ifndef RX_FLOW_SPIN_MAX
+#define RX_FLOW_SPIN_MAX (1 << 22)  // polls (~2 s with s_sleep 2) before a wave gives up
+#endif
+__device__ __forceinline__ int xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return (int)(x & 7);
+}
+
+// per window: KIN(b, 0) of every block queued on its XCD, the rest of each queue
+// emptied, counters zeroed, the window's task count per XCD.  Workgroup x = XCD x.
+__global__ __launch_bounds__(256) void k_flow_init(const rx_wave* __restrict__ dyn, int n_blocks, int R, rx_flow f) {
+  const int x = blockIdx.x;
+  int32_t* q = f.q + (size_t)x * f.cap;
+  int32_t* ctl = f.ctl + 32 * x;
+  int nb = 0, per_step = 0;
+  for (int b = x; b < n_blocks; b += 8) {
+    ++nb;
+    per_step += 2 + (dyn[b].count * R + 63) / 64;  // KIN, REWARD, ray classes
+  }
+  for (int i = threadIdx.x; i < f.cap; i += blockDim.x) {
+    const int b = x + 8 * i;
+    q[i] = i < nb ? ((b << 4) | 0) : -1;  // KIN(b, step 0)
+  }
+  for (int b = x + 8 * (int)threadIdx.x; b < n_blocks; b += 8 * (int)blockDim.x) f.cnt[b] = 0;
+  if (threadIdx.x == 0) {
+    ctl[0] = 0;        // head
+    ctl[1] = 64 * nb;  // tail
+    ctl[2] = per_step * f.n_steps;
+    if (x == 0) f.ctl[256] = 0;
+  }
+}
+
+__global__ __launch_bounds__(64, RX_FLOW_MINW) void k_flow(const rx_kargs* args, rx_flow f) {
+  const int lane = threadIdx.x & 63;
+  const rx_kargs& a0 = *(const rx_kargs*)(rx_ckargs)args;
+  const int x = xcc_id();
+  int32_t* q = f.q + (size_t)x * f.cap;
+  int32_t* ctl = f.ctl + 32 * x;
+  const int nb = a0.n_dyn_waves, R = a0.n_sensors;
+  const int total = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const unsigned long long prof_t0 = prof_start(a0);
+  __shared__ int32_t tcnt[kTaskSectors];
+  __shared__ int32_t tstage[64 * 16];
+  for (;;) {
+    // pop: one full-wave atomic (64 per entry), the old value read back into an SGPR
+    const int idx = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 0, 1)) >> 6;
+    if (idx >= total) break;
+    int code = -1;
+    for (int spin = 0; spin < RX_FLOW_SPIN_MAX; ++spin) {
+      code = __builtin_amdgcn_readfirstlane(__hip_atomic_load(q + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (code >= 0) break;
+      __builtin_amdgcn_s_sleep(RX_FLOW_SLEEP);
+    }
+    if (code < 0) {  // the producer never pushed: give up (recorded, the host raises)
+      if (lane == 0) atomicOr(f.ctl + 256, 1);
+      break;
+    }
+    const int kind = code & 15, sb = code >> 4, s = sb / nb, b = sb - s * nb;
+    const rx_kargs& as = *(const rx_kargs*)((rx_ckargs)args + s);
+    typedef const __attribute__((address_space(4))) int32_t* rx_cip;
+    const rx_cip dwp = (rx_cip)(const int32_t*)(as.dyn_waves + b);
+    const int n_tasks = dwp[3] * R, n_cls = (n_tasks + 63) >> 6, perm_start = dwp[1];
+    if (kind == 0) {
+      // ---- KIN(b, s): kinematics + the block's ray-task sort, then push REWARD + the classes
+      tcnt[lane] = 0;
+      double ang[1], ep[3] = {0.0, 0.0, 0.0};
+      int e = -1;
+      dyn1_env<1, RX_PART_KIN, true>(as, b, ang, e, ep);
+      sort_block_tasks<1, true>(as, perm_start, e, ang, tcnt, tstage);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int n = 1 + n_cls;
+      const int slot = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 1, n)) >> 6;
+      if (lane < n) {  // REWARD first, then the classes centre-first (longest chains first)
+        const int kd = lane == 0 ? 1 : 2 + win_class(lane, n_cls);
+        __hip_atomic_store(q + slot + lane, (sb << 4) | kd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      if (kind == 1) {
+        double ang[1], ep[3] = {0.0, 0.0, 0.0};
+        int e = -1;
+        dyn1_env<1, RX_PART_REWARD, true>(as, b, ang, e, ep);
+        add_episode_stats(as, ep);
+      } else {
+        const int j = kind - 2;
+        const rx_wave rw{dwp[0], perm_start, 64 * j, min(64, n_tasks - 64 * j)};
+        rays_wave<1, 1, true>(as, rw, as.tasks_out + (size_t)perm_start * R, b);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // arrival; the step's last one queues KIN(b, s + 1)
+      const int old = __builtin_amdgcn_readfirstlane(atomicAdd(f.cnt + b, 1)) >> 6;
+      if (old == (s + 1) * (1 + n_cls) - 1 && s + 1 < f.n_steps) {
+        const int slot = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 1, 1)) >> 6;
+        if (lane == 0)
+          __hip_atomic_store(q + slot, ((sb + nb) << 4) | 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  prof_end(a0, (int)blockIdx.x, prof_t0);
 }
 
 // ============================================================ k_rollout
@@ -2647,6 +2799,22 @@ extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int 
   hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
   hipLaunchKernelGGL(k_window, dim3(a->n_dyn_waves), dim3(64 * kWinWaves), RX_WIN_LDS_PAD, s, (const rx_kargs*)args,
                      n_steps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rx_flow_capacity(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_flow, 64, 0) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return per_cu * cus;
+}
+
+extern "C" int rx_launch_flow(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last, rx_kargs* args,
+                              const rx_flow* f, int grid, hipStream_t s) {
+  if (n_steps < 1 || n_steps > RX_WIN_MAX_STEPS || f->n_steps != n_steps) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
+  hipLaunchKernelGGL(k_flow_init, dim3(8), dim3(256), 0, s, a->dyn_waves, a->n_dyn_waves, a->n_sensors, *f);
+  hipLaunchKernelGGL(k_flow, dim3(grid), dim3(64), 0, s, (const rx_kargs*)args, *f);
   return (int)hipGetLastError();
 }
 

@@ -32,7 +32,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
            "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_set_start_draws",
-           "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps")
+           "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps", "rx_flow_errors")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward", "k_window")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
@@ -151,6 +151,7 @@ def load(build_if_missing=True):
     L.rx_step.argtypes = [_P, ctypes.POINTER(RxIO), _P]
     L.rx_step_phases.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, _P]
     L.rx_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, ctypes.POINTER(RxIOStrides), _P]
+    L.rx_flow_errors.argtypes = [_P, _P]
     gae_args = [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _P, _P]
     L.rx_gae.argtypes = gae_args
     L.rx_gae_scan.argtypes = gae_args

@@ -19,6 +19,7 @@ rx_step calls BIT FOR BIT:
   interval or spans several, windows longer than RX_WIN_MAX_STEPS, and the
   re-sort keys written on exactly the steps the per-step path writes them.
 """
+import ctypes
 import random
 
 import numpy as np
@@ -45,12 +46,23 @@ def _actions(g, K, N):
     return a
 
 
-def _pair(pool, widths, sched=None, sort_interval=None):
+MODES = [pytest.param(1, id="k_window"), pytest.param(2, id="k_flow")]
+
+
+def _flow_ok(v):
+    """k_flow records a bounded-spin timeout (an incomplete launch) in a device flag."""
+    n = ctypes.c_int32(-1)
+    from rx import _lib
+    _lib.check(v.L.rx_flow_errors(v._h, ctypes.byref(n)), "rx_flow_errors")
+    assert n.value == 0, "k_flow: a wave timed out waiting for a task"
+
+
+def _pair(pool, widths, sched=None, sort_interval=None, mode=1):
     from rx.vector_env import RacingVectorEnv
     kw = dict(device="cuda", autoreset="next_step", sort_interval=sort_interval)
-    on = RacingVectorEnv(pool, widths, sched={**(sched or {}), "window": 1}, **kw)
+    on = RacingVectorEnv(pool, widths, sched={**(sched or {}), "window": mode}, **kw)
     off = RacingVectorEnv(pool, widths, sched={**(sched or {}), "window": -1}, **kw)
-    assert on.schedule()["window"] == 1, on.schedule()
+    assert on.schedule()["window"] == mode, on.schedule()
     assert off.schedule()["window"] == 0
     return on, off
 
@@ -74,6 +86,7 @@ def _compare_calls(on, off, Ks, seed):
         for x, y in zip(*outs):
             assert torch.equal(x, y), K
         ended += int(outs[0][2].sum())
+    _flow_ok(on)
     sa, sb = on.get_state(), off.get_state()
     for k in sa:
         assert np.array_equal(sa[k], sb[k]), k
@@ -83,12 +96,13 @@ def _compare_calls(on, off, Ks, seed):
     return ended
 
 
-def test_window_equals_per_step_at_65536():
+@pytest.mark.parametrize("mode", MODES)
+def test_window_equals_per_step_at_65536(mode):
     """configs[2]: the bench's 65,536 envs (1,029 blocks, re-sort every 8 steps);
     calls of 20 (the driver's), 3, 8 and 37 steps -- windows starting anywhere in
     the re-sort interval -- bit-identical to the per-step launches."""
     pool, widths = _seed1_pool(65536)
-    on, off = _pair(pool, widths)
+    on, off = _pair(pool, widths, mode=mode)
     assert on.sort_interval == 8
     ended = _compare_calls(on, off, (20, 3, 8, 37), seed=5)
     assert ended > 5000
@@ -102,29 +116,33 @@ def test_window_equals_per_step_at_65536():
     off.close()
 
 
-def test_window_equals_per_step_at_4096():
+@pytest.mark.parametrize("mode", MODES)
+def test_window_equals_per_step_at_4096(mode):
     """configs[1]'s env count with the window schedule forced (one lane per ray and
     per env, the task sort every launch: what k_window runs) against the per-step
     launches of the same schedule, re-sort every 16 steps."""
     pool, widths = _seed1_pool(4096)
-    on, off = _pair(pool, widths, sched=dict(ray_lpr=1, reward_lpe=1, task_sort=1))
+    on, off = _pair(pool, widths, sched=dict(ray_lpr=1, reward_lpe=1, task_sort=1), mode=mode)
     _compare_calls(on, off, (128, 5, 16, 70), seed=9)
     on.close()
     off.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("N,interval", [(4100, 7), (3001, 0), (8256, 3)])
-def test_window_ragged_blocks_and_intervals(N, interval):
+def test_window_ragged_blocks_and_intervals(N, interval, mode):
     """Slot groups of every size (partial blocks), no re-sort at all (one window
     per call, split at RX_WIN_MAX_STEPS = 64 steps), and a re-sort every 3 steps."""
     pool, widths = _seed1_pool(N)
-    on, off = _pair(pool, widths, sched=dict(ray_lpr=1, reward_lpe=1, task_sort=1), sort_interval=interval)
+    on, off = _pair(pool, widths, sched=dict(ray_lpr=1, reward_lpe=1, task_sort=1), sort_interval=interval,
+                    mode=mode)
     _compare_calls(on, off, (1, 9, 100, 2), seed=N)
     on.close()
     off.close()
 
 
-def test_window_65536_subset_bit_exact_vs_oracle(oracle_dev):
+@pytest.mark.parametrize("mode", MODES)
+def test_window_65536_subset_bit_exact_vs_oracle(oracle_dev, mode):
     """The window path at the bench's launch geometry vs the device-libm oracle: a
     2,048-env subset of 65,536 compared after every one of 120 steps (six calls of
     20 steps, each call's per-step rows kept), whole f64 state after every call."""
@@ -132,8 +150,8 @@ def test_window_65536_subset_bit_exact_vs_oracle(oracle_dev):
     from tests.test_fullsize_gpu import REL1, _oracle_table
     N = 65536
     pool, widths = _seed1_pool(N)
-    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(window=1))
-    assert v.schedule()["window"] == 1
+    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(window=mode))
+    assert v.schedule()["window"] == mode
     idx = np.sort(np.random.default_rng(23).choice(N, 2048, replace=False))
     tab = _oracle_table(v)
     st = single_state(len(idx))
@@ -169,19 +187,21 @@ def test_window_65536_subset_bit_exact_vs_oracle(oracle_dev):
         for key in ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "steps", "flags"):
             assert np.array_equal(g[key][idx], st[key]), (call, key)
     assert ended > 100
+    _flow_ok(v)
     v.close()
 
 
-def test_window_graph_replay_equals_eager():
+@pytest.mark.parametrize("mode", MODES)
+def test_window_graph_replay_equals_eager(mode):
     """The bench captures its timed steps in a HIP graph: a captured rx_steps call
     (k_window_args + k_window + the re-sorts) replayed == the same call eager."""
     pool, widths = _seed1_pool(16384)
     from rx.vector_env import RacingVectorEnv
     va = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(ray_lpr=1, reward_lpe=1,
-                                                                                          task_sort=1, window=1))
+                                                                                          task_sort=1, window=mode))
     vb = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched=dict(ray_lpr=1, reward_lpe=1,
-                                                                                          task_sort=1, window=1))
-    assert va.schedule()["window"] == 1
+                                                                                          task_sort=1, window=mode))
+    assert va.schedule()["window"] == mode
     va.reset_device()
     vb.reset_device()
     a = _actions(torch.Generator(device="cuda").manual_seed(4), 24, 16384)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--burn", type=int, default=200)
     ap.add_argument("--sched", default="", help="extra schedule overrides key=value,...")
     ap.add_argument("--label", default="")
+    ap.add_argument("--mode", type=int, default=1, help="rx_config.window of the 'on' env: 1 k_window, 2 k_flow")
+    ap.add_argument("--sort-interval", type=int, default=None)
     args = ap.parse_args()
     from rx.track import gen_tracks
     from rx.vector_env import RacingVectorEnv
@@ -37,7 +39,8 @@ def main():
     pool = gen_tracks(num_tracks=N, seed=1)
     widths = [np.random.randint(6, 10) for _ in range(N)]
     extra = {k: int(v) for k, v in (kv.split("=") for kv in args.sched.split(",") if kv)}
-    envs = {w: RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sched={**extra, "window": w})
+    envs = {w: RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", sort_interval=args.sort_interval,
+                               sched={**extra, "window": args.mode if w == 1 else -1})
             for w in (1, -1)}
     torch.manual_seed(1234)
     K = args.steps
@@ -78,6 +81,7 @@ def main():
     out = {"label": args.label, "envs": N, "steps": K, "schedule_on": envs[1].schedule(),
            "window_on_Msteps": [round(x / 1e6, 1) for x in res[1]],
            "window_off_Msteps": [round(x / 1e6, 1) for x in res[-1]],
+           "sort_interval": envs[1].sort_interval,
            "kernel_us_on": prof[1], "kernel_us_off": prof[-1], "window_workgroups": wg,
            "lib": os.environ.get("RX_LIB_PATH", "default")}
     print(json.dumps(out), flush=True)
