@@ -419,7 +419,7 @@ def ppo_grad_roofline(t, dev, reps=160):
                     "so frac is a lower bound for k_ppo_grad alone"}
 
 
-def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dtype="fp32"):
+def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dtype="fp32", extra=None):
     """PPO training throughput (BASELINE.json configs[1] per GPU; configs[4]'s
     data-parallel update at N GPUs): rx.ppo.PPO on envs_per_gpu envs per rank,
     each update = T-step rollout with the fused policy in the loop + GAE + the
@@ -432,7 +432,8 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
     from rx.ppo import PPO
     from rx.track import gen_tracks
     n = envs_per_gpu * world
-    cfg = base_config(num_envs=n, num_steps=T, kl_target=1e9, shuffle="device", policy_dtype=policy_dtype)
+    cfg = base_config(num_envs=n, num_steps=T, kl_target=1e9, shuffle="device", policy_dtype=policy_dtype,
+                      **(extra or {}))
     cfg["total_timesteps"] = (updates + 1) * cfg["batch_size"]
     random.seed(1)
     np.random.seed(1)
@@ -472,11 +473,47 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
             "grad_roofline": grad_rf,
             "ms_per_update": round(el / updates * 1e3, 3), "envs_per_gpu": envs_per_gpu, "global_envs": n,
             "num_steps": T, "batch": B, "epochs_x_minibatches": f"{c['update_epochs']}x{n_mb}",
-            "update_path": "fused HIP (rx_ppo_minibatch_grad" + ("_shard + bucket all-reduce)" if world > 1 else ")"),
+            "update_path": "fused HIP (rx_ppo_minibatch_grad" + ("_shard + bucket all-reduce)"
+                                                                if world > 1 or c.get("shard_update") else ")"),
             "allreduce_per_update": ar["all_reduce"], "allreduce_bytes_per_update": ar["bytes"],
             "allreduce_per_update_expected": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
             "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
             "note": "KL early stop off, device shuffles; timed after one warm-up update"}
+
+
+def rccl_world1_leg(dev, envs, T, updates):
+    """the data-parallel update priced on ONE GPU before the driver's
+    8-GPU run -- a 1-rank RCCL process group, the shard path forced (config
+    shard_update: per epoch rx_ppo_adv_moments -> RCCL all-reduce -> finalize, per
+    optimizer step rx_ppo_minibatch_grad_shard -> RCCL all-reduce of the 42 KB
+    [gradient, KL] bucket -> rx_ppo_kl_check -> rx_adam_clip_step) with the
+    collectives really issued (rx.dist.FORCE_COLLECTIVES), as ONE captured HIP
+    graph per epoch (graph_dp) and as eager launches.  Beside ppo_train (the
+    single-rank fused update) it is the floor of the data-parallel overhead."""
+    import torch.distributed as td
+    from rx import dist as rdist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    td.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    rdist.FORCE_COLLECTIVES["on"] = True
+    out = {}
+    try:
+        for graph in (True, False):
+            rdist.GRAPH_DP.update(captured=None, error=None)
+            r = ppo_leg(1, 0, dev, None, "nccl", envs, T, updates, extra=dict(shard_update=True, graph_dp=graph))
+            out["graph" if graph else "eager"] = {k: r[k] for k in ("value", "ms_per_update", "allreduce_per_update",
+                                                                    "allreduce_bytes_per_update", "update_path")}
+            if graph:
+                out["graph_capture"] = dict(rdist.GRAPH_DP)
+        out.update(unit="train env-steps/s", backend="nccl (RCCL), world size 1",
+                   rccl=".".join(str(v) for v in torch.cuda.nccl.version()),
+                   note="collectives issued at world size 1 (no peer traffic): the launch / collective sequence "
+                        "of the data-parallel update on one GPU; allreduce_per_update counts Python-issued "
+                        "all-reduces (a graph replay issues its captured ones without Python)")
+    finally:
+        rdist.FORCE_COLLECTIVES["on"] = False
+        td.destroy_process_group()
+    return out
 
 
 def selfplay_leg(dev, envs, T, updates, pool_size=5):
@@ -699,6 +736,9 @@ def main():
                     help="on (default): the production steps are rx_steps calls over the HBM-resident action bank -- "
                          "with the window schedule the steps between two spatial re-sorts run as ONE k_window launch "
                          "(a workgroup per 64-env block for all of them); off: one rx_step (k_kin1 + k_step2) per step")
+    ap.add_argument("--rccl-world1", choices=("on", "off"), default="on",
+                    help="at N = 1: also time the data-parallel PPO update over a 1-rank RCCL group "
+                         "('ppo_train_rccl_world1': captured epoch graphs and eager)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, reports its device and "
                          "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
@@ -985,6 +1025,12 @@ def main():
     # (bf16 MFMA operands, f32 accumulation, f32 master weights / Adam), at N = 1 only
     ppo_bf16 = ppo_leg(world, rank, dev, dist, args.dist_backend, args.ppo_envs_per_gpu, args.ppo_steps,
                        args.ppo_updates, "bf16") if args.ppo_updates > 0 and world == 1 else None
+    rccl1 = None
+    if args.ppo_updates > 0 and world == 1 and args.rccl_world1 == "on":
+        try:
+            rccl1 = rccl_world1_leg(dev, args.ppo_envs_per_gpu, args.ppo_steps, args.ppo_updates)
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the headline is unaffected
+            rccl1 = {"error": f"{type(e).__name__}: {e}"[:400]}
     sp = None
     if args.selfplay_updates > 0 and world == 1:
         sp = selfplay_leg(dev, args.selfplay_envs, args.ppo_steps, args.selfplay_updates)
@@ -1084,6 +1130,7 @@ def main():
             "async_stream_groups": async_probe,
             "ppo_train": ppo,
             "ppo_train_bf16": ppo_bf16,
+            "ppo_train_rccl_world1": rccl1,
             "selfplay_train": sp,
             "time_to_90": tt90,
         }

@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 21
+#define RX_ABI_VERSION 22
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -127,6 +127,12 @@ typedef struct {
      as a task graph over per-XCD ready queues: any wave runs any ready (step, block) task), -1 off.
      Scheduling only. */
   int32_t window;
+  /* ABI v22: the ray-task ranking of the launches that sort the tasks (task_sort): 1 = a 4-wave workgroup
+     per 64-env block (k_kin1p: kinematics on one wave, the ranking on all four), 0 auto / -1 = the block's
+     one kinematics wave ranks its 704 tasks (k_kin1; auto is off: k_kin1p is 1.0 us faster but k_step2's
+     ray waves 1.6 us slower on its task order, profiles/r05/ab_kin_sort.jsonl).  The same counting sort
+     either way (rx_ray_tasks; tests/test_kin_sort_gpu.py).  Scheduling only. */
+  int32_t kin_sort;
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -201,9 +207,9 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
  * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
  * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval, rx_steps
  * multi-step windows (0/1, ABI v21), dynamics launches so far (the re-sort cadence counter: the
- * launch with count % sort_interval == 0 writes the re-sort keys; ABI v21).  Host only, no
- * device call. */
-#define RX_SCHEDULE_W 17
+ * launch with count % sort_interval == 0 writes the re-sort keys; ABI v21), workgroup-wide
+ * ray-task ranking (0/1, ABI v22).  Host only, no device call. */
+#define RX_SCHEDULE_W 18
 int rx_schedule(const rx_env* h, int32_t* out);
 
 /* Track table (host arrays, copied to the device).  Replaces the per-env
@@ -336,6 +342,11 @@ int rx_profile_waves(rx_env* h, int32_t launch, uint64_t* start, uint64_t* end, 
  * outside the tail).  Host only, no device call.  No counterpart in the
  * reference. */
 int rx_ray_waves(const rx_env* h, int32_t* out, int32_t cap, int32_t* n_waves);
+/* Diagnostics (ABI v22): the device ray-task list the last sorting launch wrote
+ * (ray_order 2: per 64-env block its A * n_sensors task ids (A p + q) R + r in
+ * direction-sector order), copied to host int32 out[cap] after the stream
+ * drains; *n = its length (N * A * n_sensors).  cap = 0 queries *n only. */
+int rx_ray_tasks(rx_env* h, int32_t* out, int64_t cap, int64_t* n, void* stream);
 
 /* GAE (agent/ppo.py:134-154), float32, bit-exact lane-per-env recurrence.
  * rewards/values/dones [T][N]; next_value/next_done [N]; adv/returns [T][N]. */
@@ -434,7 +445,14 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
  * *stop), then the clip + Adam update of params / exp_avg / exp_avg_sq
  * (rx_adam_clip_step's arithmetic; skipped when *stop is set).  params must be
  * b->params; cfg the rx_adam_clip_step layout of the same P parameters;
- * adam_ws holds rx_ppo_update_workspace_floats(obs_dim, cfg) floats. */
+ * adam_ws holds rx_ppo_update_workspace_floats(obs_dim, cfg) floats and must be
+ * ZERO-FILLED once when allocated (ABI v22): its last RX_PPO_TAIL_CTL words are
+ * the control block of the single-launch reduce + clip + Adam variant (a build
+ * option, RX_PPO_FUSED_TAIL=1, measured slower: DESIGN.md §5), whose word
+ * RX_PPO_TAIL_ERR counts workgroups that gave up waiting for the published clip
+ * coefficient (always 0 in the default build). */
+#define RX_PPO_TAIL_CTL 8
+#define RX_PPO_TAIL_ERR 6
 size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg);
 int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
                             float* ws_f32, double* ws_f64, float* grad, float* exp_avg, float* exp_avg_sq, float* step,

@@ -330,6 +330,8 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
+  if (cfg->kin_sort < -1 || cfg->kin_sort > 1)
+    return fail(RX_EINVAL, "kin_sort must be 0 (auto), 1 or -1 (got %d)", cfg->kin_sort);
   if (cfg->window < -1 || cfg->window > 2)
     return fail(RX_EINVAL, "window must be 0 (auto), 1 (k_window), 2 (k_flow) or -1 (got %d)", cfg->window);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
@@ -405,7 +407,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort, h->window, (int32_t)h->dyn_calls};
+                                    h->task_sort, h->window, (int32_t)h->dyn_calls, h->cfg.kin_sort > 0 ? 1 : 0};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -853,6 +855,7 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.ray_tail_lpr = h->ray_tail_lpr;
   a.reward_lpe = h->reward_lpe;
   a.argmin_window = h->argmin_window;
+  a.kin_sort = h->cfg.kin_sort > 0 ? 1 : 0;
   a.slot_nenv = h->slot_n.p;
   a.wide = h->dyn_lpe == 64;
   a.n_wide_tasks = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;
@@ -1065,6 +1068,21 @@ int rx_ray_waves(const rx_env* h, int32_t* out, int32_t cap, int32_t* n_waves) {
     out[4 * i + 3] = w.count;
   }
   *n_waves = (int32_t)n;
+  return RX_OK;
+}
+
+int rx_ray_tasks(rx_env* h, int32_t* out, int64_t cap, int64_t* n, void* stream) {
+  if (!h || !n || (cap > 0 && !out)) return fail(RX_EINVAL, "rx_ray_tasks: null argument");
+  if (!h->assigned) return fail(RX_ESTATE, "rx_ray_tasks before rx_assign");
+  const int64_t len = std::min<int64_t>((int64_t)h->tasks.n,
+                                        (int64_t)h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors);
+  *n = len;
+  if (cap <= 0) return RX_OK;
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(out, h->tasks.p, (size_t)std::min(cap, len) * sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(RX_EHIP, "rx_ray_tasks: copy failed");
   return RX_OK;
 }
 
@@ -1445,7 +1463,8 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
 
 size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg) {
   if ((obs_dim != 15 && obs_dim != 19) || adam_cfg_error(cfg) != RX_OK) return 0;
-  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors + 2;  // + Adam's two step scalars
+  // + Adam's two step scalars + the fused tail's RX_PPO_TAIL_CTL control words (zero-filled by the caller once)
+  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors + 2 + RX_PPO_TAIL_CTL;
 }
 
 int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
@@ -1464,11 +1483,19 @@ int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_conf
   if (!ws_f32 || !ws_f64 || !grad || !exp_avg || !exp_avg_sq || !step || !lr || !stop || !kl_at_stop || !adam_ws)
     return fail(RX_EINVAL, "rx_ppo_minibatch_update: null buffer");
   const hipStream_t s = (hipStream_t)stream;
+#if RX_PPO_FUSED_TAIL
+  // gradient, then ONE launch that reduces it, hands the clip coefficient over and steps Adam
+  const rx_adam_tail tail{params, exp_avg, exp_avg_sq};
+  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step, lr,
+                               &tail)))
+    return fail(RX_EHIP, "ppo update launch failed: %s", hipGetErrorString((hipError_t)rc));
+#else
   if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step, lr)))
     return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
   if ((rc = rx_launch_adam_apply(cfg, params, grad, exp_avg, exp_avg_sq, step, lr, stop, adam_ws,
                                  rx_ppo_reduce_blocks(b->obs_dim), s)))
     return fail(RX_EHIP, "adam launch failed: %s", hipGetErrorString((hipError_t)rc));
+#endif
   return RX_OK;
 }
 

@@ -168,6 +168,7 @@ struct rx_kargs {
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
   int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
   int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
+  int32_t kin_sort;       // sorting KIN launches: k_kin1p (the ranking over a 4-wave workgroup), else k_kin1
   int32_t ray_tail_from;  // ray waves >= this one (the dispatch tail) hold 64 / ray_tail_lpr tasks each, cast at
   int32_t ray_tail_lpr;   // ray_tail_lpr lanes per ray (2 or 4); -1 = no tail split (rx_config.ray_tail)
   // rx_set_start_draws (two-car envs): the start-slot order of the env that is the
@@ -234,6 +235,20 @@ __device__ __forceinline__ void rx_adam_scalars(const rx_adam_config& cfg, float
   out[0] = (float)(-(lr / (1.0 - pow(cfg.beta1, s))));
   out[1] = (float)sqrt(1.0 - pow(cfg.beta2, s));
 }
+// torch.optim.Adam's element update (foreach, non-capturable) after the clip
+// coefficient: g *= coef; m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g;
+// p += step_size * m / (sqrt(v)/bc2_sqrt + eps).  ONE definition for
+// k_adam_apply (rx_optim.hip) and the fused minibatch tail (rx_ppo.hip), so both
+// optimizer paths round every element identically.
+__device__ __forceinline__ void rx_adam_elem(float& g, float& m, float& v, float& p, float coef, float w1, float fb2,
+                                             float w2, float eps, float step_size, float bc2_sqrt) {
+  g = g * coef;
+  m = m + w1 * (g - m);  // torch.lerp, weight < 0.5 branch
+  v = v * fb2;
+  v = v + w2 * g * g;
+  const float den = sqrtf(v) / bc2_sqrt + eps;
+  p = p + step_size * (m / den);
+}
 // The re-sort's bin count for the wave's calling lanes (one per env, key =
 // its bin): lanes grouped by bin (ballot), then ONE vector atomic in which
 // every group leader adds its group size to hist[bin]; the returned old count
@@ -277,7 +292,20 @@ extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* sto
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
                                   const rx_adam_config* cfg = nullptr, float* norm_ws = nullptr,
-                                  float* step = nullptr, const double* lr = nullptr);
+                                  float* step = nullptr, const double* lr = nullptr,
+                                  const struct rx_adam_tail* fused = nullptr);
+// the Adam state the fused minibatch tail updates (k_ppo_reduce<true>): with it
+// the reduce launch also clips and applies Adam (norm_ws: + the control block).
+// A/B build only (RX_PPO_FUSED_TAIL=1): 16.3 us against 5.0 + 5.1 us for the
+// reduce and k_adam_apply launches it replaces
+#ifndef RX_PPO_FUSED_TAIL
+#define RX_PPO_FUSED_TAIL 0
+#endif
+struct rx_adam_tail {
+  float* p;
+  float* m;
+  float* v;
+};
 extern "C" int rx_ppo_reduce_blocks(int obs_dim);
 extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                                     const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s);

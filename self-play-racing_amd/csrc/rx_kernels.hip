@@ -934,6 +934,87 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
 #endif
 }
 
+// k_kin1 on the launches that sort the ray tasks (tasks_out set): a 4-wave
+// workgroup per 64-env block.  Wave 0 steps the block's kinematics
+// (dyn1_env<1, KIN>, as k_kin1); then every wave ranks the ray tasks of a
+// contiguous quarter of the sensors (rays [w*q, (w+1)*q), q = ceil(R/4)) in
+// per-wave sector counters with the LDS atomics of sort_block_tasks_lds -- 704
+// tasks on 256 lanes instead of 64, the phase that was 48 % of k_kin1's wave
+// (profiles/r04/kin_stamps.json) -- wave 0 turns the 4 x 64 counts into
+// offsets (sector-major, wave-minor), every wave scatters its tasks into the
+// LDS row and the whole workgroup stores the row.  A wave ranks its rays in
+// ray order and a wave instruction ranks its lanes in lane order, so the order
+// inside a sector is (ray, env position): the row k_kin1 writes, entry for entry.
+constexpr int kKinWaves = 4;
+__global__ __launch_bounds__(64 * kKinWaves) void k_kin1p(rx_kargs a) {
+  const int b = uniform((int)blockIdx.x);
+  const int wv = uniform((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  __shared__ int32_t tcnt[kKinWaves][kTaskSectors];
+  __shared__ int32_t tstage[64 * 16];
+  __shared__ double sAng[64];
+  __shared__ int32_t sPos[64];
+  __shared__ int32_t sTotal;
+  if (b >= a.n_dyn_waves) return;
+  const unsigned long long prof_t0 = prof_start(a);
+  tcnt[wv][lane] = 0;
+  if (wv == 0) {
+    double ang[1], ep[3] = {0.0, 0.0, 0.0};
+    int e = -1;
+    dyn1_env<1, RX_PART_KIN>(a, b, ang, e, ep);
+    sAng[lane] = ang[0];
+    sPos[lane] = e;
+  }
+  __syncthreads();
+  constexpr int kRW = 16 / kKinWaves;  // rays per wave at most (n_sensors <= 16 with ray_order 2)
+  const int R = a.n_sensors, q = (R + kKinWaves - 1) / kKinWaves;
+  const int p_l = sPos[lane];
+  const double ang_l = sAng[lane];
+  const float inv = (float)kTaskSectors * 0.15915494309189535f;  // sectors per radian
+  int pk[kRW];
+#pragma unroll
+  for (int i = 0; i < kRW; ++i) {
+    const int r = wv * q + i;
+    pk[i] = -1;
+    if (i < q && r < R && p_l >= 0) {
+      const float th = (float)(ang_l + a.rel_angles[r]);
+      const int sec = (int)__builtin_floorf(th * inv) & (kTaskSectors - 1);
+      pk[i] = (atomicAdd(&tcnt[wv][sec], 1) << 6) | sec;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {  // counts -> exclusive offsets, sector-major then wave
+    int cw[kKinWaves], c0 = 0;
+#pragma unroll
+    for (int w = 0; w < kKinWaves; ++w) {
+      cw[w] = tcnt[w][lane];
+      c0 += cw[w];
+    }
+    int c = c0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(c, o, 64);
+      if (lane >= o) c += v;
+    }
+    int base = c - c0;
+#pragma unroll
+    for (int w = 0; w < kKinWaves; ++w) {
+      tcnt[w][lane] = base;
+      base += cw[w];
+    }
+    if (lane == 63) sTotal = c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kRW; ++i)
+    if (pk[i] >= 0) tstage[tcnt[wv][pk[i] & 63] + (pk[i] >> 6)] = p_l * R + wv * q + i;  // task (A p + q) R + r
+  __syncthreads();
+  const int total = sTotal;
+  int32_t* out = a.tasks_out + (size_t)uniform(a.dyn_waves[b].perm_start) * R;
+  for (int i = (int)threadIdx.x; i < total; i += 64 * kKinWaves) out[i] = tstage[i];
+  if (wv == 0) prof_end(a, b, prof_t0);
+}
+
 // ============================================================ k_dyn, A == 2
 // MultiRacingEnv.step / reset (environment/multi_racing_env.py:118-269), one
 // env (both cars) per lane.
@@ -2732,7 +2813,11 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
-    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 1, 1), s, *a);
+    if (a->kin_sort && a->tasks_out && a->n_sensors <= 16)  // sorting launches: the 4-wave ranking
+      hipLaunchKernelGGL(k_kin1p, dim3(a->n_dyn_waves), dim3(64 * kKinWaves), 0, s, *a);
+    else
+      hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 1, 1), s,
+                         *a);
     return (int)hipGetLastError();
   }
   // RX_SPLIT_REWARD: the REWARD half alone; RX_SPLIT_REWARD_RAYS: both halves in one launch

@@ -147,15 +147,11 @@ __global__ __launch_bounds__(kT) void k_adam_apply(adam_args a) {
   const float w1 = (float)(1.0 - b1);
   const float fb2 = (float)b2, w2 = (float)(1.0 - b2);
   const float eps = (float)a.cfg.eps;
-  g = g * coef;
+  rx_adam_elem(g, m, v, p, coef, w1, fb2, w2, eps, step_size, bc2_sqrt);
   a.g[i] = g;
-  m = m + w1 * (g - m);  // torch.lerp, weight < 0.5 branch
-  v = v * fb2;
-  v = v + w2 * g * g;
   a.m[i] = m;
   a.v[i] = v;
-  const float den = sqrtf(v) / bc2_sqrt + eps;
-  a.p[i] = p + step_size * (m / den);
+  a.p[i] = p;
 }
 
 }  // namespace

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -31,7 +31,7 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_rollout_supported", "rx_rollout", "rx_ppo_adv_moments", "rx_ppo_adv_finalize", "rx_ppo_minibatch_grad_shard", "rx_ppo_kl_check", "rx_random_permutation",
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
-           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_set_start_draws",
+           "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_ray_tasks", "rx_set_start_draws",
            "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps", "rx_flow_errors")
 RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward", "k_window")
 ADAM_MAX_TENSORS = 32
@@ -48,17 +48,18 @@ class RxConfig(ctypes.Structure):
                 ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)] + \
                [(k, ctypes.c_int32) for k in ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window",
                                                "seg_filter", "box_quadrants", "ray_dispatch", "ray_tail",
-                                               "ray_tail_lpr", "task_sort", "window")]
+                                               "ray_tail_lpr", "task_sort", "window", "kin_sort")]
 
 
 # rx_config launch-schedule fields (ABI v17, v19, v20, v21): 0 = auto, -1 = off / none (include/rx.h).
 # Scheduling only: every value gives bit-identical results.
-SCHEDULE_W = 17  # rx_schedule: resolved schedule (include/rx.h)
+RX_PPO_TAIL_CTL, RX_PPO_TAIL_ERR = 8, 6  # rx_ppo_minibatch_update's control block at the end of adam_ws (rx.h)
+SCHEDULE_W = 18  # rx_schedule: resolved schedule (include/rx.h)
 SCHEDULE_KEYS = ("split", "wide", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
                  "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort",
-                 "window", "dyn_calls")
+                 "window", "dyn_calls", "kin_sort")
 SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "window")
+                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "window", "kin_sort")
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
@@ -192,6 +193,7 @@ def load(build_if_missing=True):
     L.rx_profile_read.argtypes = [_P, _P, _P]
     L.rx_profile_waves.argtypes = [_P, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, _P]
     L.rx_ray_waves.argtypes = [_P, _P, ctypes.c_int32, _P]
+    L.rx_ray_tasks.argtypes = [_P, _P, ctypes.c_int64, _P, _P]
     L.rx_set_start_draws.argtypes = [_P, _P, ctypes.c_int64, _P]
     for name in EXPORTS:
         if name not in ("rx_last_error", "rx_abi_version", "rx_ppo_workspace_floats", "rx_ppo_workspace_doubles",

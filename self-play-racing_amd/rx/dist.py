@@ -108,10 +108,26 @@ def average_flat(flat):
     flat.div_(td.get_world_size())
 
 
+# bench.py's world-size-1 RCCL leg: issue the collectives through a 1-rank process
+# group anyway, so the data-parallel update's launch / collective sequence is priced
+# on one GPU
+FORCE_COLLECTIVES = {"on": False}
+# the last data-parallel epoch graph capture (rx.ppo): captured or the refusal
+GRAPH_DP = {"captured": None, "error": None}
+
+
+def capturable():
+    """Collectives of this process group can be recorded in a HIP graph: RCCL
+    ("nccl") can, gloo (host-side) cannot; no group at all: nothing to record."""
+    if not (td.is_available() and td.is_initialized()):
+        return True
+    return td.get_backend() == "nccl"
+
+
 def all_reduce_sum(t):
     """In-place SUM over ranks (the fused data-parallel update pre-scales its
     shard gradient and KL by 1/world, so the sum is the global mean)."""
-    if active():
+    if active() or (FORCE_COLLECTIVES["on"] and td.is_available() and td.is_initialized()):
         _all_reduce(t)
     return t
 

@@ -409,9 +409,30 @@ class PPO:
         if fused:
             ent.fused = ppo_fused.FusedMinibatchGrad(self.agent, self._flat, b, mb, ent.perm, self.config)
             if rdist.world() > 1 or self.config.get("shard_update", False):
-                # collectives stay outside graphs; "shard_update" runs this path on one rank (tests)
+                # the data-parallel epoch ("shard_update" runs it on one rank: tests, the bench's
+                # world-1 RCCL leg): adv moments -> all-reduce -> finalize, then per optimizer step
+                # shard gradient -> bucket all-reduce -> KL check -> Adam.  config["graph_dp"]
+                # (default: auto = whenever the process group's collectives are capturable, RCCL)
+                # records the whole epoch, collectives included, as ONE HIP graph; a refused
+                # capture falls back to eager launches and is recorded in rdist.GRAPH_DP.
                 w = rdist.world()
-                ent.run = lambda: ent.fused.shard_epoch(ent.stop, ent.kl, w, rdist.all_reduce_sum)
+                eager = lambda: ent.fused.shard_epoch(ent.stop, ent.kl, w, rdist.all_reduce_sum)  # noqa: E731
+                ent.run = eager
+                want = self.config.get("graph_dp", "auto")
+                if want is True or (want == "auto" and rdist.capturable()):
+                    try:
+                        eager()  # warm-up with the stop flag up: workspaces, communicator; nothing moves
+                        torch.cuda.synchronize(dev)
+                        ent.graph = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(ent.graph):
+                            eager()
+                        torch.cuda.synchronize(dev)
+                        ent.run = ent.graph.replay
+                        rdist.GRAPH_DP.update(captured=True, error=None)
+                    except Exception as e:  # noqa: BLE001 -- recorded, eager launches instead
+                        ent.graph, ent.run = None, eager
+                        rdist.GRAPH_DP.update(captured=False, error=f"{type(e).__name__}: {e}"[:300])
+                        torch.cuda.synchronize(dev)
             elif capture:
                 ent.graph = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(dev)

@@ -105,11 +105,22 @@ class FusedMinibatchGrad:
             n = self.L.rx_ppo_update_workspace_floats(self.batch.obs_dim, f.cfg)
             if n == 0:
                 raise RuntimeError(self.L.rx_last_error().decode())
-            ws = self.adam_ws = torch.empty(n, dtype=torch.float32, device=self.stats.device)
+            # zero-filled: its last word is the fused launch's arrival counter (rx.h, ABI v22)
+            ws = self.adam_ws = torch.zeros(n, dtype=torch.float32, device=self.stats.device)
         _lib.check(self.L.rx_ppo_minibatch_update(
             self.batch, int(m), f.cfg, _lib.ptr(f.flat_param), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
             _lib.ptr(f.flat_grad), _lib.ptr(f.exp_avg), _lib.ptr(f.exp_avg_sq), _lib.ptr(f.step_t), _lib.ptr(f.lr_t),
             _lib.ptr(stop), _lib.ptr(kl_at_stop), _lib.ptr(ws), _lib.stream_ptr(stream)), "rx_ppo_minibatch_update")
+
+    def tail_errors(self):
+        """Workgroups of the fused update launch that gave up waiting for the
+        published clip coefficient (rx.h RX_PPO_TAIL_ERR; 0 unless two updates
+        shared the device at once).  Synchronises the device."""
+        ws = self.__dict__.get("adam_ws")
+        if ws is None:
+            return 0
+        ctl = ws[-_lib.RX_PPO_TAIL_CTL:].view(torch.int32)
+        return int(ctl[_lib.RX_PPO_TAIL_ERR])
 
     def epoch(self, stop, kl_at_stop, stats=True):
         """All minibatch steps of one epoch over the current perm (``stats``:

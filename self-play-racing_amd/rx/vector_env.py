@@ -292,6 +292,16 @@ class RacingVectorEnv:
         self._prof_cap = max(1, n.value)
         return self._prof_cap
 
+    def ray_tasks(self, stream=None):
+        """The device ray-task list (rx_ray_tasks): per 64-env block its A * R task
+        ids in direction-sector order, as the last sorting launch wrote it."""
+        n = ctypes.c_int64(0)
+        _lib.check(self.L.rx_ray_tasks(self._h, None, 0, ctypes.byref(n), None), "rx_ray_tasks")
+        t = np.zeros(max(n.value, 1), np.int32)
+        _lib.check(self.L.rx_ray_tasks(self._h, t.ctypes.data, n.value, ctypes.byref(n), _lib.stream_ptr(stream)),
+                   "rx_ray_tasks")
+        return t[:n.value]
+
     def ray_wave_table(self):
         """The ray-wave table in dispatch order (rx_ray_waves, host only): a dict of
         int arrays track, perm_start, task_start, count, plus per wave its class

@@ -167,8 +167,9 @@ def _rccl_worker(port, q):
             return t
 
         res = []
-        for shard in (False, True):
-            t = _trainer(graph_update=False, shard_update=shard, kl_target=1e9)
+        eager_calls = None
+        for shard, graph in ((False, False), (True, False), (True, True)):
+            t = _trainer(graph_update=False, shard_update=shard, graph_dp=graph, kl_target=1e9)
             data = _rollout(t)
             np.random.seed(4)
             saved = rd.all_reduce_sum
@@ -183,9 +184,12 @@ def _rccl_worker(port, q):
             torch.cuda.synchronize()
             res.append((t._flat.flat_param.cpu().numpy().copy(), t._flat.exp_avg.cpu().numpy().copy(),
                         float(t._flat.step_t)))
+            if shard and not graph:
+                eager_calls = dict(calls)
             c = t.config
+        graph_dp = dict(rd.GRAPH_DP)
         ver = ".".join(str(v) for v in torch.cuda.nccl.version())
-        q.put((res, calls, c["update_epochs"], c["num_minibatches"], ver))
+        q.put((res, eager_calls, c["update_epochs"], c["num_minibatches"], ver, graph_dp))
     finally:
         td.destroy_process_group()
 
@@ -202,11 +206,16 @@ def test_rccl_world1_shard_update_equals_fused():
     q = ctx.Queue()
     pr = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
     pr.start()
-    res, calls, E, n_mb, ver = q.get(timeout=600)
+    res, calls, E, n_mb, ver, graph_dp = q.get(timeout=600)
     pr.join(timeout=120)
     assert pr.exitcode == 0
-    (pa, ma, sa), (pb, mb_, sb) = res
+    (pa, ma, sa), (pb, mb_, sb), (pc, mc, sc) = res
     assert calls["dev"] and calls["n"] == 2 * E * (n_mb + 1)  # per update: E moment + E * n_mb bucket all-reduces
-    assert sa == sb == 2 * E * n_mb
+    assert sa == sb == sc == 2 * E * n_mb
     assert np.array_equal(pa, pb) and np.array_equal(ma, mb_)
-    print(f"\nRCCL {ver}: {calls['n']} all-reduces, {calls['bytes']} B, shard update == fused bit for bit")
+    # the data-parallel epoch captured as ONE HIP graph, RCCL all-reduces
+    # included (graph_dp), replayed == eager == the single-rank fused update
+    assert graph_dp["captured"] is True, graph_dp
+    assert np.array_equal(pa, pc) and np.array_equal(ma, mc)
+    print(f"\nRCCL {ver}: {calls['n']} all-reduces, {calls['bytes']} B, shard update (eager and one graph per "
+          "epoch) == fused bit for bit")

@@ -43,7 +43,7 @@ KERNELS = ("k_window_args", "k_window", "k_step2", "k_kin1", "k_kin2", "k_rays",
 
 
 def short(name):
-    if "k_dyn1<1, 1>" in name:  # dyn1_env<LPE = 1, PART = KIN>: the split step's k_kin1
+    if "k_dyn1<1, 1>" in name or "k_kin1p" in name:  # the split step's k_kin1 (k_kin1p: its sorting launches)
         return "k_kin1"
     if "k_dyn2<1>" in name:
         return "k_kin2"
