@@ -1536,6 +1536,11 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
 //   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
 // (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
 // range its rounding cannot cross the threshold).  Only hit segments divide.
+// The sign flips are one XOR of dotp's sign bit into the high words (not a
+// compare + two selects): they differ from `dotp < 0 ? -x : x` only for dotp =
+// -0.0 or NaN, where D > 1e-10 is false and no hit is reported either way.
+// bestf (the float32 bound of best the box tests read) is refreshed by the
+// callers once per scanned leaf, not per hit.
 // Smallest float32 >= x (x >= 0): the f32 box tests compare against it.
 __device__ __forceinline__ float f32_up(double x) {
   float f = (float)x;
@@ -1543,21 +1548,19 @@ __device__ __forceinline__ float f32_up(double x) {
   return f;
 }
 
-__device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, double v3x, double v3y, double& best,
-                                         float& bestf) {
+__device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, double v3x, double v3y, double& best) {
   const double v1x = ox - g.x, v1y = oy - g.y;
   const double dotp = g.z * v3x + g.w * v3y;
   const double cross = g.z * v1y - g.w * v1x;
   const double dot = v1x * v3x + v1y * v3y;
   const double D = __builtin_fabs(dotp);
-  const bool neg = dotp < 0.0;
-  const double C = neg ? -cross : cross;
-  const double N = neg ? -dot : dot;
+  const long long sgn = __double_as_longlong(dotp) & (long long)0x8000000000000000ull;
+  const double C = __longlong_as_double(__double_as_longlong(cross) ^ sgn);
+  const double N = __longlong_as_double(__double_as_longlong(dot) ^ sgn);
   const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
   if (hit) {
     const double t = C / D;
     best = t < best ? t : best;
-    bestf = f32_up(best);
   }
 }
 
@@ -1566,23 +1569,27 @@ typedef float rx_f2 __attribute__((ext_vector_type(2)));
 // Segment pre-filter (float32, one lane's ray).  With a = (o - start) . v3
 // (the reference's `dot`) and p = v2 . v3 (`dotp`), s = a / p lies in [0, 1]
 // iff a and a - p do not share a strict sign, i.e. iff
-// |2a - p| - |p| <= 0.  Computed in float32 from the float32 segment table,
-// the left side is within 2^-22 (3.5 M1 + 4.2 L) of its value on the f64
-// operands (M1 = |ox| + |oy| + |sx| + |sy|, L = the slot's longest segment),
-// and those differ from the exact one by ~2^-50 (M1 + L).  So a segment this
-// test rejects, with e2 = 2^-17 (M1 + L + 1) >= 8x that bound, has a and a - p
-// of one strict sign by a margin >= 2^-18 (M1 + L): the f64 test then sees
-// N < 0 or fl(N - D) > D 2^-53 and reports no hit.  Rejecting it changes
-// nothing; the wave runs the exact test on a segment iff some lane may hit it.
+// |2a - p| - |p| <= 0.  Computed in float32 from the float32 segment table as
+// a = c0 - sx v3x - sy v3y with the lane's c0 = o . v3 (two fmas on the
+// wave-uniform segment words, no packed operand copies) and p = sz v3x + sw v3y,
+// the left side is within 2^-22 (5.5 M1 + 3 L) of its value on the f64
+// operands (M1 = |ox| + |oy| + |sx| + |sy|, L = the slot's longest segment:
+// input roundings 3 * 2^-24 M1, c0 2 * 2^-24 M1, the two fmas 2 * 2^-24 M1, p
+// 4 * 2^-24 L, then 2a - p and the subtraction), and those differ from the
+// exact one by ~2^-50 (M1 + L).  So a segment this test rejects, with
+// e2 = 2^-17 (M1 + L + 1) >= 5.8x that bound, has a and a - p of one strict
+// sign by a margin >= 2^-18 (M1 + L): the f64 test then sees N < 0 or
+// fl(N - D) > D 2^-53 and reports no hit.  Rejecting it changes nothing; the
+// wave runs the exact test on a segment iff some lane may hit it.
 struct seg_pref {
   const float4* __restrict__ segf;  // the slot's float32 segments
-  rx_f2 of, v3f;                    // origin, (-sin, cos) in float32
+  rx_f2 v3f;                        // (-sin, cos) in float32
+  float c0;                         // of . v3f: the float32 origin projected on v3
   float e2;                         // 2^-17 (|ox| + |oy| + max(|sx| + |sy|) + L + 1)
 };
 __device__ __forceinline__ bool seg_may_hit(const float4 f, const seg_pref& pf) {
-  const rx_f2 pa = (pf.of - rx_f2{f.x, f.y}) * pf.v3f;
-  const rx_f2 pd = rx_f2{f.z, f.w} * pf.v3f;
-  const float aa = pa.x + pa.y, dp = pd.x + pd.y;
+  const float aa = __builtin_fmaf(-f.y, pf.v3f.y, __builtin_fmaf(-f.x, pf.v3f.x, pf.c0));
+  const float dp = __builtin_fmaf(f.w, pf.v3f.y, f.z * pf.v3f.x);
   return !(__builtin_fabsf(__builtin_fmaf(2.0f, aa, -dp)) - __builtin_fabsf(dp) > pf.e2);
 }
 
@@ -1600,23 +1607,25 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
                    f3 = ldu(pf.segf + j + 3);
       const bool h0 = __any(seg_may_hit(f0, pf)), h1 = __any(seg_may_hit(f1, pf)), h2 = __any(seg_may_hit(f2, pf)),
                  h3 = __any(seg_may_hit(f3, pf));
-      if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
-      if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best, bestf);
-      if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best, bestf);
-      if (h3) seg_test(ldu(seg + j + 3), ox, oy, v3x, v3y, best, bestf);
+      if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
+      if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best);
+      if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best);
+      if (h3) seg_test(ldu(seg + j + 3), ox, oy, v3x, v3y, best);
     }
     for (; j < j1; ++j)
-      if (__any(seg_may_hit(ldu(pf.segf + j), pf))) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
+      if (__any(seg_may_hit(ldu(pf.segf + j), pf))) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
+    bestf = f32_up(best);
     return;
   }
   for (; j + 4 <= j1; j += 4) {
     const double4 g0 = ldu(seg + j), g1 = ldu(seg + j + 1), g2 = ldu(seg + j + 2), g3 = ldu(seg + j + 3);  // uniform -> s_load
-    seg_test(g0, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g1, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g2, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g3, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g0, ox, oy, v3x, v3y, best);
+    seg_test(g1, ox, oy, v3x, v3y, best);
+    seg_test(g2, ox, oy, v3x, v3y, best);
+    seg_test(g3, ox, oy, v3x, v3y, best);
   }
-  for (; j < j1; ++j) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best, bestf);
+  for (; j < j1; ++j) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
+  bestf = f32_up(best);
 }
 
 // The four lanes of a quad (lanes 4i .. 4i+3) exchange a double: DPP
@@ -1649,7 +1658,7 @@ __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, i
       const double4 g = seg[j];
       bool may = jb + sub < j1;
       if constexpr (FILT) may = may && seg_may_hit(pf.segf[j], pf);
-      if (may) seg_test(g, ox, oy, v3x, v3y, best, bestf);
+      if (may) seg_test(g, ox, oy, v3x, v3y, best);
     }
     best = __builtin_fmin(best, quad_dpp<0xB1>(best));
     if constexpr (LPR == 4) best = __builtin_fmin(best, quad_dpp<0x4E>(best));
@@ -1885,7 +1894,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     const int quad0 = uniform(quad);
     int scanned = 0, tested = 0;
     // segment pre-filter operands (seg_may_hit): |sx| + |sy| <= |cx| + |cy| + 2 rad for every boundary point
-    const seg_pref pf{reinterpret_cast<const float4*>(a.tr.seg_f) + 2 * wp0, rx_f2{oxf, oyf}, rx_f2{-snf, csf},
+    const seg_pref pf{reinterpret_cast<const float4*>(a.tr.seg_f) + 2 * wp0, rx_f2{-snf, csf},
+                      __builtin_fmaf(oyf, csf, oxf * -snf),
                       (float)((__builtin_fabs(ox) + __builtin_fabs(oy) + __builtin_fabs(cx) + __builtin_fabs(cy) +
                                2.0 * rad + L + 1.0) * 0x1p-17)};
     RAY_STAMP(3);
@@ -2031,16 +2041,15 @@ __device__ __forceinline__ void ray_wide(const rx_kargs& a, int iq, int ray, con
   rx_sincos(a.st.angle[iq] + a.rel_angles[ray], &sn, &cs);  // racing_env.py:50
   const double v3x = -sn, v3y = cs;
   double best = __builtin_inf();
-  float bestf = __builtin_inff();
   int j = threadIdx.x & 63;
   for (; j + 192 < S_; j += 256) {  // four coalesced loads in flight before the (divergent) tests
     const double4 g0 = seg[j], g1 = seg[j + 64], g2 = seg[j + 128], g3 = seg[j + 192];
-    seg_test(g0, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g1, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g2, ox, oy, v3x, v3y, best, bestf);
-    seg_test(g3, ox, oy, v3x, v3y, best, bestf);
+    seg_test(g0, ox, oy, v3x, v3y, best);
+    seg_test(g1, ox, oy, v3x, v3y, best);
+    seg_test(g2, ox, oy, v3x, v3y, best);
+    seg_test(g3, ox, oy, v3x, v3y, best);
   }
-  for (; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best, bestf);
+  for (; j < S_; j += 64) seg_test(seg[j], ox, oy, v3x, v3y, best);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) best = __builtin_fmin(best, __shfl_xor(best, o, 64));
   if ((threadIdx.x & 63) == 0) ray_finish<A>(a, pos, q, ray, ox, oy, v3x, v3y, best);

@@ -14,30 +14,36 @@ F = np.float32
 
 
 def exact_hit(ox, oy, sx, sy, v2x, v2y, v3x, v3y):
-    """seg_test's hit predicate (division-free form of track.py:184-196)."""
+    """seg_test's hit predicate (division-free form of track.py:184-196); the
+    sign flips are the XOR of dotp's sign bit (np.signbit: -0.0 included)."""
     v1x, v1y = ox - sx, oy - sy
     dotp = v2x * v3x + v2y * v3y
     cross = v2x * v1y - v2y * v1x
     dot = v1x * v3x + v1y * v3y
     D = np.abs(dotp)
-    neg = dotp < 0.0
+    neg = np.signbit(dotp)
     C = np.where(neg, -cross, cross)
     N = np.where(neg, -dot, dot)
     return (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 2.0 ** -53)
 
 
+def fma32(a, b, c):
+    """float32 fma: the product of two float32 is exact in float64, the sum is
+    taken in extended precision and rounded once to float32."""
+    p = np.asarray(a, np.float64) * np.asarray(b, np.float64)
+    return (p.astype(np.longdouble) + np.asarray(c, np.longdouble)).astype(F)
+
+
 def prefilter(ox, oy, sx, sy, v2x, v2y, v3x, v3y, e2):
-    """seg_may_hit in float32: |2a - p| - |p| <= e2."""
+    """seg_may_hit in float32: a = c0 - sx v3x - sy v3y (c0 = o . v3 per lane),
+    p = sz v3x + sw v3y, keep iff |2a - p| - |p| <= e2."""
     of = (ox.astype(F), oy.astype(F))
     sf = (sx.astype(F), sy.astype(F), v2x.astype(F), v2y.astype(F))
     vf = (v3x.astype(F), v3y.astype(F))
-    pax = (of[0] - sf[0]) * vf[0]
-    pay = (of[1] - sf[1]) * vf[1]
-    pdx = sf[2] * vf[0]
-    pdy = sf[3] * vf[1]
-    aa = pax + pay
-    dp = pdx + pdy
-    q = F(2.0) * aa - dp  # fma(2, aa, -dp): 2*aa is exact, one rounding
+    c0 = fma32(of[1], vf[1], of[0] * vf[0])  # __builtin_fmaf(oyf, csf, oxf * -snf)
+    aa = fma32(-sf[1], vf[1], fma32(-sf[0], vf[0], c0))
+    dp = fma32(sf[3], vf[1], sf[2] * vf[0])
+    q = fma32(F(2.0), aa, -dp)  # fma(2, aa, -dp)
     return ~((np.abs(q) - np.abs(dp)) > e2)
 
 
