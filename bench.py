@@ -959,10 +959,12 @@ def main():
     waves = None
     if args.profile_steps > 0:
         events = {k: ("step" if k % 2 == 0 else "split") for k in range(args.profile_steps)}
+        mark("instrumented_begin")
         env0.profile(1)
         env0.profile(0)
         prof_el = timed(one_step, args.profile_steps, events)
         prof = env0.profile_read()
+        mark("instrumented_end")
         waves = wave_slots(env0, args.profile_steps * 3) if G == 1 else None
     # ---- instrumented windows (multi-step form): whole re-sort windows only -- the steps are
     # first aligned so the next one opens a window -- each k_window launch stamped per workgroup
@@ -972,10 +974,12 @@ def main():
         if iv > 0:
             run_steps((1 - env0.schedule()["dyn_calls"]) % iv)
         n_win_steps = max(iv, args.profile_steps // iv * iv) if iv > 0 else args.profile_steps
+        mark("windows_begin")
         env0.profile(1)
         run_steps(n_win_steps)
         env0.profile(0)
         wp = env0.profile_read().get("k_window")
+        mark("windows_end")
         if wp is not None:
             win = {"steps": n_win_steps, "launches": wp[1], "steps_per_launch": n_win_steps / wp[1],
                    "avg_launch_ms": wp[0], "ms_per_step": wp[0] * wp[1] / n_win_steps,
@@ -984,12 +988,14 @@ def main():
     # per REWARD wave its waypoint-box tests and leaf scans (rx_io.counters, one atomic per wave)
     work = None
     if args.counter_steps > 0 and G == 1:
+        mark("counters_begin")
         env0.enable_counters(True)
         for _ in range(args.counter_steps):
             one_step()
         torch.cuda.synchronize()
         cnt = env0.read_counters()
         env0.enable_counters(False)
+        mark("counters_end")
         sch = env0.schedule()
         steps_n = args.counter_steps * n
         work = {k: v for k, v in cnt.items()}

@@ -434,6 +434,15 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
 // env's position.  Runs every step with all 64 lanes of the wave (env lanes
 // have p >= 0).  The direction is the car's new angle
 // (the one k_rays casts from).  Scheduling only: no result depends on it.
+// Write-amplification A/B build only (profiles/r05/ab_write_amp.jsonl):
+// -DRX_WA_POSORDER=1 makes every io row of the single-agent split step (actions,
+// obs, reward, masks) the env's POSITION instead of its env id, so each wave's
+// rows are one contiguous, coalesced range -- an upper bound on what coalescing
+// the io traffic could buy.  Its outputs are permuted (not a product build).
+#ifndef RX_WA_POSORDER
+#define RX_WA_POSORDER 0
+#endif
+#define RX_IO_ROW(a, pos) (RX_WA_POSORDER ? (pos) : (a).perm[(pos)])
 constexpr int kTaskSectors = 64;
 template <int A>
 __device__ __forceinline__ int sort_block_tasks_lds(const rx_kargs& a, int p, const double* ang, int32_t* cnt,
@@ -587,7 +596,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   // p = the env's position in the wave order: the engine's working state is
   // stored in that order (coalesced); e = the env id, the row of every io buffer
   int p = we.perm_start + lane;
-  int e = REW ? -1 : a.perm[p];  // REWARD: loaded after the argmins
+  int e = REW ? -1 : RX_IO_ROW(a, p);  // REWARD: loaded after the argmins
 
   const rx_state& S = a.st;
   uint8_t ef = ldc<C>(S.env_flags + p);
@@ -685,7 +694,7 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   // live as 64-bit pointers across the argmins (they were spilled to scratch)
   if constexpr (REW) __asm__ volatile("" : "+v"(p));
   if (REW) {  // the REWARD half's late loads (see above)
-    e = a.perm[p];
+    e = RX_IO_ROW(a, p);
     c.vx = ldc<C>(S.vx + p);
     c.vy = ldc<C>(S.vy + p);
     last_progress = ldc<C>(S.last_progress + p);
@@ -1967,7 +1976,7 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
     }
     dist = (min_car < dist) ? min_car : dist;
   }
-  const int e = a.perm[pos];
+  const int e = RX_IO_ROW(a, pos);
   a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 

@@ -75,6 +75,22 @@ def main():
         "same_kernels_after_region": per(after),
         "sort_in_region": any(n.startswith("k_sort") for _, _, n in win),
     }
+    # the whole trace split by the bench's region marks: the timed region
+    # (the first t0 .. t1), the instrumented per-wave-stamped steps, the instrumented windows,
+    # the executed-work counter steps; "other" = burn-in, graph capture, legs after the env part
+    ci = 1 if res["clock"] == "boottime" else 2
+    spans = [("timed", t0, t1)]
+    for name in ("instrumented", "windows", "counters"):
+        b = [m[ci] for m in marks if m[0] == name + "_begin"]
+        e = [m[ci] for m in marks if m[0] == name + "_end"]
+        if b and e:
+            spans.append((name, b[0], e[0]))
+    regions = collections.defaultdict(list)
+    for r in rows:
+        tag = next((n for n, lo, hi in spans if lo <= r[0] <= hi), "other")
+        regions[tag].append(r)
+    summary["regions"] = {k: per(v) for k, v in regions.items()}
+    summary["region_spans_us"] = {n: round((hi - lo) / 1e3, 2) for n, lo, hi in spans}
     s = json.dumps(summary, indent=1)
     print(s)
     if out:
