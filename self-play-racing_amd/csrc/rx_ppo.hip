@@ -166,6 +166,51 @@ struct GradLds {
   static_assert(kGW * SMALL_PER <= 64 * kTS, "per-wave sums must fit in the dZ transpose");
 };
 
+// d loss / d head pre-activation g of the lane's row (every lane of the row) from
+// the head outputs y (lane (0, l15) holds output j in y[j]) and the row's inputs
+// s0..s3 (actor: actions 0 / 1, old log-prob, advantage; critic: return, old
+// value); the actor also adds old_logp - logp to kl on its q = 0 lanes.
+// agent/ppo.py:170-198 (clipped surrogate, clipped value loss); shared by both
+// precisions' trunks.
+template <int NET>
+__device__ __forceinline__ void head_grad(const rx_ppo_batch& b, float s0, float s1, float s2, float s3, bool live,
+                                          const f4& y, const float* b3, int l15, int q, const float (&var)[kNA],
+                                          const float (&lsc)[kNA], float mean, float sd, float invM, float clip,
+                                          float (&g)[NET ? 1 : kNA], double& kl) {
+  constexpr int NOUT = NET ? 1 : kNA;
+  const float lo = 1.0f - clip, hi = 1.0f + clip;
+  if constexpr (NET == 0) {
+    float mu[kNA], diff[kNA], logp = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kNA; ++j) {
+      mu[j] = rx_policy::tanh_fast(__shfl(y[j], l15, 64) + b3[j]);
+      diff[j] = (j ? s1 : s0) - mu[j];
+      logp += normal_logp(diff[j], var[j], lsc[j]);
+    }
+    const float oldlp = s2;
+    const float An = live ? (s3 - mean) / (sd + 1e-8f) : 0.0f;
+    const float ratio = expf(logp - oldlp);
+    const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
+    const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;  // torch.max splits ties
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+    const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) g[j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
+    if (live && q == 0) kl += (double)(oldlp - logp);
+  } else {
+    const float v = __shfl(y[0], l15, 64) + b3[0];
+    // 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
+    const float R = s0, ov = s1;
+    const float vd = v - ov;
+    const float vc = ov + fminf(fmaxf(vd, -clip), clip);
+    const float e1 = v - R, e2 = vc - R;
+    const float q1 = e1 * e1, q2 = e2 * e2;
+    const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
+    const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
+    g[0] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
+  }
+}
+
 // One trunk (NET: 0 = actor, 1 = critic) of one workgroup: rows_per_wg rows,
 // kRP = 64 per pass.  Per pass:
 //   A  each wave: forward, loss gradient g and dZ2 for its 16 rows (registers);
@@ -207,7 +252,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
   auto sload = [](const float* p) { return *(const __attribute__((address_space(4))) float*)p; };
   const float mean = sload(b.adv_stats + 2 * a.m), sd = sload(b.adv_stats + 2 * a.m + 1);
   const float invM = 1.0f / (float)b.mb;
-  const float clip = b.clip_coef, lo = 1.0f - clip, hi = 1.0f + clip;
+  const float clip = b.clip_coef;
   float var[kNA], lsc[kNA];
 #pragma unroll
   for (int j = 0; j < kNA; ++j) {
@@ -312,36 +357,7 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
     mlp_forward<D, NOUT, PREC>(w, x, H1, H2, y, l15, q, pass_ == 0 ? 16 : -1);
     if (pass_ == 0) PPO_STAMP(18);
     float g[NOUT];  // d loss / d head pre-activation, row rr (every lane of the row)
-    if (NET == 0) {
-      float mu[kNA], diff[kNA], logp = 0.0f;
-#pragma unroll
-      for (int j = 0; j < kNA; ++j) {
-        mu[j] = rx_policy::tanh_fast(__shfl(y[j], l15, 64) + w.b3[j]);
-        diff[j] = (j ? cur.s1 : cur.s0) - mu[j];
-        logp += normal_logp(diff[j], var[j], lsc[j]);
-      }
-      const float oldlp = cur.s2;
-      const float An = live ? (cur.s3 - mean) / (sd + 1e-8f) : 0.0f;
-      const float ratio = expf(logp - oldlp);
-      const float u1 = -An * ratio, u2 = -An * fminf(fmaxf(ratio, lo), hi);
-      const float g1 = u1 > u2 ? 1.0f : (u1 == u2 ? 0.5f : 0.0f), g2 = 1.0f - g1;  // torch.max splits ties
-      const float inr = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
-      const float dlogp = live ? invM * (g1 * -An + g2 * -An * inr) * ratio : 0.0f;
-#pragma unroll
-      for (int j = 0; j < NOUT; ++j) g[j] = dlogp * diff[j] / var[j] * (1.0f - mu[j] * mu[j]);
-      if (live && q == 0) kl += (double)(oldlp - logp);
-    } else {
-      const float v = __shfl(y[0], l15, 64) + w.b3[0];
-      // 0.5 * max((v-R)^2, (v_clip-R)^2), agent/ppo.py:194-198
-      const float R = cur.s0, ov = cur.s1;
-      const float vd = v - ov;
-      const float vc = ov + fminf(fmaxf(vd, -clip), clip);
-      const float e1 = v - R, e2 = vc - R;
-      const float q1 = e1 * e1, q2 = e2 * e2;
-      const float gq1 = q1 > q2 ? 1.0f : (q1 == q2 ? 0.5f : 0.0f), gq2 = 1.0f - gq1;
-      const float vin = (vd >= -clip && vd <= clip) ? 1.0f : 0.0f;
-      g[0] = live ? b.vf_coef * 0.5f * invM * (gq1 * 2.0f * e1 + gq2 * 2.0f * e2 * vin) : 0.0f;
-    }
+    head_grad<NET>(b, cur.s0, cur.s1, cur.s2, cur.s3, live, y, w.b3, l15, q, var, lsc, mean, sd, invM, clip, g, kl);
     if (pass_ == 0) PPO_STAMP(19);
     f4 dZ[4];  // dZ2 = (W3^T g) * (1 - H2^2)
 #pragma unroll
@@ -548,6 +564,354 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
       a.kl_partial[blockIdx.x] = ((kd[0] + kd[4 * st]) + (kd[2 * st] + kd[6 * st])) +
                                  ((kd[st] + kd[5 * st]) + (kd[3 * st] + kd[7 * st]));
   }
+}
+
+// ================================================================ bf16 k_ppo_grad
+// The bf16 gradient (rx_ppo_batch.precision = RX_PREC_BF16) with
+// every matrix operand in the form the 16x16x32 bf16 MFMA reads, so the pass is
+// MFMAs, their LDS reads and the activation math -- no per-use conversions:
+//  * weights: built ONCE per workgroup as bf16 MFMA fragments in LDS, one
+//    ds_read_b128 each -- F1 (layer 1), F2 (layer 2), F3 (head) in the exact
+//    operand order of mlp_forward's bf16 path (the forward is bit-identical to
+//    k_policy_act / k_rollout's), FT2 = W2^T for dH1 = W2^T dZ2;
+//  * the batch-row reductions dW = sum_rows dZ^T [H | X | 1]: the accumulator
+//    tiles hold the row on the lane, so each lane stores its 4 registers of a
+//    tile packed (v_cvt_pk_bf16_f32, one ds_write_b64) into a [row][unit] image
+//    and the operand is read back transposed with ds_read_b64_tr_b16
+//    (MI355X / cdna_hip_programming.md T10), rows 32s + 8g + 4h + (0..3) per
+//    read: the batch row is the MFMA K dimension;
+//  * bias gradients ride on ones columns: db2 as a fifth dW2 column tile (H
+//    image column 64 = 1), db1 on the X image's column D (as the fp32 kernel),
+//    dW3 | db3 as an MFMA over the g image (operand rows j < NOUT) against the
+//    H2 image and its ones tile.
+// Gradients are rounded to bf16 only where they are matrix operands, as the
+// fp32-vs-bf16 contract of rx.h says; accumulation and everything else is f32.
+// Same pass structure as the fp32 kernel (A forward + loss + images | B dW2, dH1
+// | C images | D dW1, dW3), 52 KB of LDS: three 4-wave workgroups per CU.
+template <int D>
+struct GradLdsB {
+  static constexpr int ZS = 72, HS = 80, XS = 48, GS = 24;  // image row strides (bf16): conflict-free T10 reads
+  static constexpr int F1 = 0, F2 = F1 + 4 * 64 * 16, FT2 = F2 + 8 * 64 * 16, F3 = FT2 + 8 * 64 * 16,
+                       B1 = F3 + 2 * 64 * 16, B2 = B1 + 64 * 4, W3 = B2 + 64 * 4, B3 = W3 + kNA * 64 * 4,
+                       IZ = B3 + 16, IH = IZ + kRP * ZS * 2, IX = IH + kRP * HS * 2, IG = IX + kRP * XS * 2,
+                       KL = IG + kRP * GS * 2, TOTAL = KL + 8 * kGW;
+  static_assert(IZ % 16 == 0 && IH % 16 == 0 && IX % 16 == 0 && IG % 16 == 0, "16-byte aligned images");
+};
+
+using bf4 = __bf16 __attribute__((ext_vector_type(4)));
+using s4 = short __attribute__((ext_vector_type(4)));
+// 4 bf16 of one image row: the lane's 4 accumulator registers of a tile
+__device__ __forceinline__ void st_bf4(char* img, int off_elems, const f4& v) {
+  bf4 b;
+  b[0] = (__bf16)v[0], b[1] = (__bf16)v[1], b[2] = (__bf16)v[2], b[3] = (__bf16)v[3];
+  *reinterpret_cast<bf4*>(img + 2 * off_elems) = b;
+}
+// The 16x16x32 operand of k-step s over an image [row][col] (stride S bf16):
+// A[m = col c0 + lane & 15][k = row 32 s + 8 (lane >> 4) + j], two transposed reads
+// of 4 rows each (T10: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3).
+template <int S>
+__device__ __forceinline__ bf8 tr_frag(const char* img, int s, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int e0 = (32 * s + 8 * g + (i >> 2)) * S + c0 + 4 * (i & 3);
+  typedef short __attribute__((ext_vector_type(4))) v4s;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(img + 2 * e0));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(img + 2 * (e0 + 4 * S)));
+  bf8 r;
+  const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
+  const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = pl[j], r[4 + j] = ph[j];
+  return r;
+}
+
+template <int D, int NET>
+__device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float* __restrict__ W, char* lds,
+                                                  float* __restrict__ out) {
+  using L = Lay<D>;
+  using G = Geo<D>;
+  using S = GradLdsB<D>;
+  constexpr int NOUT = NET ? 1 : kNA, NT1 = G::NT1;
+  constexpr int oW1 = NET ? L::cW1 : L::aW1, ob1 = NET ? L::cb1 : L::ab1, oW2 = NET ? L::cW2 : L::aW2,
+                ob2 = NET ? L::cb2 : L::ab2, oW3 = NET ? L::cW3 : L::aW3, ob3 = NET ? L::cb3 : L::ab3;
+  static_assert(kGW == 4, "the bf16 trunk partitions its tiles over 4 waves");
+  const rx_ppo_batch& b = a.b;
+  const int t0 = threadIdx.x, lane = t0 & 63, l15 = lane & 15, q = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(t0 >> 6);
+  const int rr = 16 * wv + l15;  // this lane's row within the pass
+  const int64_t row0 = (int64_t)blockIdx.x * a.rows_per_wg;
+  const int64_t row_end = min(row0 + (int64_t)a.rows_per_wg, (int64_t)b.mb);
+  auto sgpr = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+  auto sload = [](const float* p) { return *(const __attribute__((address_space(4))) float*)p; };
+  const float mean = sload(b.adv_stats + 2 * a.m), sd = sload(b.adv_stats + 2 * a.m + 1);
+  const float invM = 1.0f / (float)b.mb;
+  const float clip = b.clip_coef;
+  float var[kNA], lsc[kNA];
+#pragma unroll
+  for (int j = 0; j < kNA; ++j) {
+    const float scale = expf(sload(b.log_std + j));
+    var[j] = sgpr(scale * scale);
+    lsc[j] = sgpr(logf(scale));
+  }
+  struct RowIn {
+    float x[8], s0, s1, s2, s3;
+  };
+  auto src_of = [&](int64_t base) -> int64_t {
+    const int64_t r_mb = base + rr;
+    if (r_mb >= row_end) return -1;
+    const int64_t v = b.perm[(int64_t)a.m * b.mb + r_mb];
+    return (v >= 0 && v < b.n_rows) ? v : -1;
+  };
+  auto load_row = [&](int64_t src) -> RowIn {
+    RowIn in;
+    const bool ok = src >= 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * q + j;
+      in.x[j] = (ok && d < D) ? b.obs[src * D + d] : 0.0f;
+    }
+    if (NET == 0) {
+      in.s0 = ok ? b.actions[src * kNA] : 0.0f;
+      in.s1 = ok ? b.actions[src * kNA + 1] : 0.0f;
+      in.s2 = ok ? b.logprobs[src] : 0.0f;
+      in.s3 = ok ? b.advantages[src] : 0.0f;
+    } else {
+      in.s0 = ok ? b.returns[src] : 0.0f;
+      in.s1 = ok ? b.values[src] : 0.0f;
+      in.s2 = in.s3 = 0.0f;
+    }
+    return in;
+  };
+  // ---- the trunk's weight fragments: every staging load into registers first (the
+  // perm indices before them, the first rows' gathers after), then the LDS stores
+  int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
+  // F1: slot t = (mt = t >> 6, lane): W1[16 mt + l15'][8 q' + j] (zero beyond D)
+  float f1[8];
+  {
+    const int ln = t0 & 63, o = 16 * (t0 >> 6) + (ln & 15), q1 = ln >> 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * q1 + j;
+      f1[j] = d < D ? W[oW1 + o * D + d] : 0.0f;
+    }
+  }
+  // F2 / FT2: slots t + 256 k = (mt, s, lane): F2 = W2[16 mt + l15'][h(s, q', j)],
+  // FT2 = W2[h(s, q', j)][16 mt + l15'], h(s, q, j) = 32 s + 16 (j >> 2) + 4 q + (j & 3)
+  float4 f2[2][2];
+  float ft[2][8];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int sl = t0 + 256 * k, mt = sl >> 7, s = (sl >> 6) & 1, ln = sl & 63, u = 16 * mt + (ln & 15),
+              q1 = ln >> 4;
+    f2[k][0] = *reinterpret_cast<const float4*>(W + oW2 + u * kH + 32 * s + 4 * q1);
+    f2[k][1] = *reinterpret_cast<const float4*>(W + oW2 + u * kH + 32 * s + 16 + 4 * q1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ft[k][j] = W[oW2 + (32 * s + 16 * (j >> 2) + 4 * q1 + (j & 3)) * kH + u];
+  }
+  // F3: slot t < 128 = (s, lane): W3[l15'][h(s, q', j)] for l15' < NOUT, else 0
+  float4 f3[2] = {make_float4(0.0f, 0.0f, 0.0f, 0.0f), make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
+  if (t0 < 128 && (t0 & 15) < NOUT) {
+    const int s = t0 >> 6, ln = t0 & 63, q1 = ln >> 4;
+    f3[0] = *reinterpret_cast<const float4*>(W + oW3 + (ln & 15) * kH + 32 * s + 4 * q1);
+    f3[1] = *reinterpret_cast<const float4*>(W + oW3 + (ln & 15) * kH + 32 * s + 16 + 4 * q1);
+  }
+  const float bv0 = t0 < 64 ? W[ob1 + t0] : (t0 < 128 ? W[ob2 + t0 - 64] : 0.0f);
+  const float bv1 = t0 < NOUT * 64 ? W[oW3 + t0] : 0.0f;
+  const float b3v = t0 < NOUT ? W[ob3 + t0] : 0.0f;
+  RowIn cur = load_row(src);
+  bf8* F1 = reinterpret_cast<bf8*>(lds + S::F1);
+  bf8* F2 = reinterpret_cast<bf8*>(lds + S::F2);
+  bf8* FT2 = reinterpret_cast<bf8*>(lds + S::FT2);
+  bf8* F3 = reinterpret_cast<bf8*>(lds + S::F3);
+  float* fB1 = reinterpret_cast<float*>(lds + S::B1);
+  float* fB2 = reinterpret_cast<float*>(lds + S::B2);
+  float* fW3 = reinterpret_cast<float*>(lds + S::W3);
+  float* fB3 = reinterpret_cast<float*>(lds + S::B3);
+  char* iZ = lds + S::IZ;
+  char* iH = lds + S::IH;
+  char* iX = lds + S::IX;
+  char* iG = lds + S::IG;
+  F1[t0] = to_bf8(make_float4(f1[0], f1[1], f1[2], f1[3]), make_float4(f1[4], f1[5], f1[6], f1[7]));
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    F2[t0 + 256 * k] = to_bf8(f2[k][0], f2[k][1]);
+    FT2[t0 + 256 * k] = to_bf8(make_float4(ft[k][0], ft[k][1], ft[k][2], ft[k][3]),
+                               make_float4(ft[k][4], ft[k][5], ft[k][6], ft[k][7]));
+  }
+  if (t0 < 128) F3[t0] = to_bf8(f3[0], f3[1]);
+  if (t0 < 64)
+    fB1[t0] = bv0;
+  else if (t0 < 128)
+    fB2[t0 - 64] = bv0;
+  if (t0 < NOUT * 64) fW3[t0] = bv1;
+  if (t0 < NOUT) fB3[t0] = b3v;
+  // constant image columns: H's ones tile (column 64 = 1, 65..79 = 0), G's zero columns 4..15
+  {
+    const int r = t0 >> 2, c = 64 + 4 * (t0 & 3);  // 64 rows x 4 chunks of 4 columns
+    st_bf4(iH, r * S::HS + c, c == 64 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
+    if ((t0 & 3) != 0) st_bf4(iG, r * S::GS + 4 * (t0 & 3), f4{0.0f, 0.0f, 0.0f, 0.0f});
+  }
+  __syncthreads();
+  f4 acc2[5], acc1[NT1], acc3 = {0.0f, 0.0f, 0.0f, 0.0f}, acc3b = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) acc2[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < NT1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  double kl = 0.0;
+  const float* b3 = fB3;
+  for (int64_t base = row0; base < row_end; base += kRP) {
+    // ================================================================ A
+    const int64_t src_nn = src_of(base + 2 * kRP);
+    const RowIn nxt = load_row(src_n);
+    const bool live = src >= 0;
+    // [X | 1] row: d = 8q + j, the ones column d = D carries db1
+    {
+      float xv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[j] = 8 * q + j == D ? 1.0f : cur.x[j];
+      *reinterpret_cast<bf8*>(iX + 2 * (rr * S::XS + 8 * q)) =
+          to_bf8(make_float4(xv[0], xv[1], xv[2], xv[3]), make_float4(xv[4], xv[5], xv[6], xv[7]));
+    }
+    // forward: mlp_forward's bf16 arithmetic on the prebuilt fragments
+    f4 H1[4], H2[4], y;
+    {
+      const bf8 bx = to_bf8(make_float4(cur.x[0], cur.x[1], cur.x[2], cur.x[3]),
+                            make_float4(cur.x[4], cur.x[5], cur.x[6], cur.x[7]));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f4 z = mma16(F1[mt * 64 + lane], bx, f4{0.0f, 0.0f, 0.0f, 0.0f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + fB1[16 * mt + 4 * q + r]);
+      }
+      const bf8 bh[2] = {to_bf8(H1[0], H1[1]), to_bf8(H1[2], H1[3])};
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) z = mma16(F2[(2 * mt + s) * 64 + lane], bh[s], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + fB2[16 * mt + 4 * q + r]);
+      }
+      y = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) y = mma16(F3[s * 64 + lane], to_bf8(H2[2 * s], H2[2 * s + 1]), y);
+    }
+    float g[NOUT];
+    head_grad<NET>(b, cur.s0, cur.s1, cur.s2, cur.s3, live, y, b3, l15, q, var, lsc, mean, sd, invM, clip, g, kl);
+    f4 dZ[4];  // dZ2 = (W3^T g) * (1 - H2^2)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * t + 4 * q + r;
+        float dh = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NOUT; ++j) dh = fmaf(fW3[j * kH + h], g[j], dh);
+        dZ[t][r] = dh * (1.0f - H2[t][r] * H2[t][r]);
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st_bf4(iZ, rr * S::ZS + 16 * t + 4 * q, dZ[t]);
+      st_bf4(iH, rr * S::HS + 16 * t + 4 * q, H1[t]);
+    }
+    if (q == 0) st_bf4(iG, rr * S::GS, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
+    __syncthreads();
+    // ================================================================ B
+    // dW2 rows [16 wv, +16) x column tiles 0..3, db2 on tile 4 (the ones column)
+#pragma unroll
+    for (int s = 0; s < kRP / 32; ++s) {
+      const bf8 av = tr_frag<S::ZS>(iZ, s, 16 * wv, lane);
+#pragma unroll
+      for (int c = 0; c < 5; ++c) acc2[c] = mma16(av, tr_frag<S::HS>(iH, s, 16 * c, lane), acc2[c]);
+    }
+    // dH1 = W2^T dZ2 (B = dZ2 in registers, k = output unit), dZ1 = dH1 * (1 - H1^2)
+    f4 dZ1[4];
+    {
+      const bf8 bz[2] = {to_bf8(dZ[0], dZ[1]), to_bf8(dZ[2], dZ[3])};
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) z = mma16(FT2[(2 * mt + s) * 64 + lane], bz[s], z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
+      }
+    }
+    __syncthreads();
+    // ================================================================ C
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st_bf4(iZ, rr * S::ZS + 16 * t + 4 * q, dZ1[t]);
+      st_bf4(iH, rr * S::HS + 16 * t + 4 * q, H2[t]);
+    }
+    __syncthreads();
+    // ================================================================ D
+    // dW1 (+ db1 at d = D) rows [16 wv, +16); dW3 column tile wv, db3 (wave 0) on the ones tile
+#pragma unroll
+    for (int s = 0; s < kRP / 32; ++s) {
+      const bf8 av = tr_frag<S::ZS>(iZ, s, 16 * wv, lane);
+#pragma unroll
+      for (int c = 0; c < NT1; ++c) acc1[c] = mma16(av, tr_frag<S::XS>(iX, s, 16 * c, lane), acc1[c]);
+      const bf8 gv = tr_frag<S::GS>(iG, s, 0, lane);
+      acc3 = mma16(gv, tr_frag<S::HS>(iH, s, 16 * wv, lane), acc3);
+      if (wv == 0) acc3b = mma16(gv, tr_frag<S::HS>(iH, s, 64, lane), acc3b);
+    }
+    __syncthreads();  // the next pass overwrites the images
+    src = src_n;
+    src_n = src_nn;
+    cur = nxt;
+  }
+  // ---- tile accumulators -> the partial row (each wave owns its tiles)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = 16 * wv + 4 * q + r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) out[oW2 + o * kH + 16 * c + l15] = acc2[c][r];
+    if (l15 == 0) out[ob2 + o] = acc2[4][r];
+#pragma unroll
+    for (int c = 0; c < NT1; ++c) {
+      const int d = 16 * c + l15;
+      if (d < D)
+        out[oW1 + o * D + d] = acc1[c][r];
+      else if (d == D)
+        out[ob1 + o] = acc1[c][r];
+    }
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) out[oW3 + j * kH + 16 * wv + l15] = acc3[j];
+    if (wv == 0 && l15 == 0) {
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) out[ob3 + j] = acc3b[j];
+    }
+  }
+  if constexpr (NET == 0) {  // approx_kl partial: per wave, folded over the waves in a fixed order
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) kl += __shfl_xor(kl, o, 64);
+    double* kd = reinterpret_cast<double*>(lds + S::KL);
+    if (lane == 0) kd[wv] = kl;
+    __syncthreads();
+    if (t0 == 0) a.kl_partial[blockIdx.x] = (kd[0] + kd[2]) + (kd[1] + kd[3]);
+  }
+}
+
+// bf16 (RX_PPO_BF_FRAG = 1, the default): the fragment / transposed-image trunk
+// above, three workgroups per CU (52 KB of LDS, <= 168 VGPRs); 0 = the bf16 path
+// of ppo_grad_trunk (per-use conversions from the f32 LDS copy), kept for A/B.
+#ifndef RX_PPO_BF_FRAG
+#define RX_PPO_BF_FRAG 1
+#endif
+template <int D>
+__global__ __launch_bounds__(kGT, 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
+                                                        float* __restrict__ partial) {
+  if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
+  __shared__ __attribute__((aligned(16))) char lds[GradLdsB<D>::TOTAL];
+  float* out = partial + (size_t)blockIdx.x * Lay<D>::Pp;
+  if (blockIdx.y == 0)
+    ppo_grad_trunk_bf<D, 0>(a, W, lds, out);
+  else
+    ppo_grad_trunk_bf<D, 1>(a, W, lds, out);
 }
 
 // blockIdx.y = trunk (0 actor, 1 critic: their losses share no parameter, so
@@ -1097,13 +1461,17 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
   int P, Pp;
   const bool bf = b->precision == kBF16;
   if (b->obs_dim == 15) {
-    if (bf)
+    if (bf && RX_PPO_BF_FRAG)
+      hipLaunchKernelGGL((k_ppo_grad_bf<15>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
+    else if (bf)
       hipLaunchKernelGGL((k_ppo_grad<15, kBF16>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     else
       hipLaunchKernelGGL((k_ppo_grad<15, kF32>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     P = Lay<15>::P, Pp = Lay<15>::Pp;
   } else {
-    if (bf)
+    if (bf && RX_PPO_BF_FRAG)
+      hipLaunchKernelGGL((k_ppo_grad_bf<19>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
+    else if (bf)
       hipLaunchKernelGGL((k_ppo_grad<19, kBF16>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
     else
       hipLaunchKernelGGL((k_ppo_grad<19, kF32>), dim3(n_wg, 2), dim3(kGT), 0, s, a, b->params, partial);
