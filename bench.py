@@ -732,6 +732,10 @@ def main():
                          "--steps production steps (each one rx_step: k_kin1 + k_step2, the re-sorts where they "
                          "fall), captured untimed before the refill steps -- the launch path of the captured PPO "
                          "rollout; off: one rx_step call per step from Python")
+    ap.add_argument("--graph-head", type=int, default=0,
+                    help="with --graph on: the first H steps form a graph of their own, replayed just before the "
+                         "graph of the other K - H (the GPU starts on the head while the host submits the rest); "
+                         "0 = one graph (default: H = 1 / 2 measured no better, profiles/r05/ab_graph_head.jsonl)")
     ap.add_argument("--multi-step", choices=("on", "off"), default="on",
                     help="on (default): the production steps are rx_steps calls over the HBM-resident action bank -- "
                          "with the window schedule the steps between two spatial re-sorts run as ONE k_window launch "
@@ -922,16 +926,28 @@ def main():
     # library's host-side schedule -- re-sort and task-order launches -- is recorded
     # as it falls for these steps), the timed region replays it exactly once
     step_graph = None
+    graph_parts = []
     if args.graph == "on" and G == 1:
         torch.cuda.synchronize(dev)
-        step_graph = torch.cuda.CUDAGraph()
-        # thread_local: a process group's watchdog thread may query its events meanwhile
-        with torch.cuda.graph(step_graph, stream=torch.cuda.Stream(device=dev), capture_error_mode="thread_local"):
-            steps(args.steps)
+        # --graph-head H: the first H steps as a graph of their own, the rest as a second
+        # graph.  A graph launch submits all of its nodes before the first one runs
+        # (t0 -> first kernel ~70 us for the 20-step graph, profiles/r05/window20_*),
+        # so the small head graph starts the GPU while the host still submits the rest.
+        head = max(0, min(args.graph_head, args.steps - 1))
+        graph_parts = [head, args.steps - head] if head > 0 else [args.steps]
+        cap = torch.cuda.Stream(device=dev)
+        step_graph = []
+        for k in graph_parts:
+            g = torch.cuda.CUDAGraph()
+            # thread_local: a process group's watchdog thread may query its events meanwhile
+            with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
+                steps(k)
+            step_graph.append(g)
         torch.cuda.synchronize(dev)
         # one untimed replay (K more burn-in steps of the same work): a graph's first
         # launch also uploads it, which would otherwise sit at the timed region's edge
-        step_graph.replay()
+        for g in step_graph:
+            g.replay()
         torch.cuda.synchronize(dev)
     ep_untimed = [0.0, 0.0, 0]
     if refill:
@@ -946,7 +962,7 @@ def main():
         ep_untimed = [sum(x) for x in zip(*(e.episode_stats() for e in envs))]
     # ---- timed region: production steps only (one rx_step per step, no instrumentation)
     if step_graph is not None:
-        elapsed = timed(lambda ev=None: step_graph.replay(), 1, collect=refill == 0)
+        elapsed = timed(lambda ev=None: [g.replay() for g in step_graph], 1, collect=refill == 0)
     elif multi:
         elapsed = timed(lambda ev=None: run_steps(args.steps), 1, collect=refill == 0)
     else:
@@ -1102,14 +1118,20 @@ def main():
             "steady_state": {"untimed_steps_before_timing": untimed + (args.steps if step_graph is not None else 0),
                              "episodes_ended_before_timing": ep_untimed[2],
                              "episodes_ended_in_timed_region": ep[2],
-                             "timed_region": ("production steps only: ONE rx_steps call of all the steps over the "
-                                              "HBM-resident action bank -- k_window launches, each the steps up to "
-                                              "the next spatial re-sort, then the re-sort -- no instrumentation"
+                             "timed_region": ("production steps only: rx_steps over the HBM-resident action bank "
+                                              f"(rx_config.window {schedule.get('window', 0)}: "
+                                              + ("k_window / k_flow launches between re-sorts"
+                                                 if schedule.get("window", 0) else "the per-step launches k_kin1 + "
+                                                 "k_step2, the re-sort every sort_interval steps") +
+                                              "), no instrumentation"
                                               if multi else
                                               "production steps only: one rx_step (k_kin1 + k_step2) per step, "
                                               "no instrumentation"),
-                             "launch": (f"one HIP graph replay of the {args.steps} steps (captured and replayed "
-                                        "once untimed)"
+                             "launch": ((f"HIP graph replays of {' + '.join(map(str, graph_parts))} steps (captured "
+                                         "and replayed once untimed; the second graph's host submission overlaps "
+                                         "the first's execution)" if len(graph_parts) > 1 else
+                                         f"one HIP graph replay of the {args.steps} steps (captured and replayed "
+                                         "once untimed)")
                                         if step_graph is not None else
                                         ("one rx_steps call" if multi else "one rx_step call per step from Python"))},
             # dominant kernel of the production step: k_window (multi-step form) or k_step2 (REWARD half
