@@ -588,14 +588,27 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
 // fp32-vs-bf16 contract of rx.h says; accumulation and everything else is f32.
 // Same pass structure as the fp32 kernel (A forward + loss + images | B dW2, dH1
 // | C images | D dW1, dW3), 52 KB of LDS: three 4-wave workgroups per CU.
+// RX_PPO_BF_DB = 1 (A/B build): two barriers per pass instead of four -- the
+// dZ1 / H2 images separate from the dZ2 / H1 ones and [X | 1] / g double-buffered
+// by pass parity, so phase C's stores need no barrier before them and the next
+// pass's phase A none after phase D (79 KB of LDS: two workgroups per CU, all
+// that a minibatch's 512 workgroups fill).  Measured no faster (17.63 vs 17.56
+// us, profiles/r05/ab_bf16_barriers.json): the barriers are not what the
+// kernel waits on, so the default keeps the 52 KB layout.
+#ifndef RX_PPO_BF_DB
+#define RX_PPO_BF_DB 0
+#endif
 template <int D>
 struct GradLdsB {
-  static constexpr int ZS = 72, HS = 80, XS = 48, GS = 24;  // image row strides (bf16): conflict-free T10 reads
+  static constexpr int DB = RX_PPO_BF_DB ? 2 : 1;  // image sets
+  static constexpr int ZS = 72, HS = 80, XS = 48, GS = RX_PPO_BF_DB ? 16 : 24;  // row strides (bf16)
   static constexpr int F1 = 0, F2 = F1 + 4 * 64 * 16, FT2 = F2 + 8 * 64 * 16, F3 = FT2 + 8 * 64 * 16,
                        B1 = F3 + 2 * 64 * 16, B2 = B1 + 64 * 4, W3 = B2 + 64 * 4, B3 = W3 + kNA * 64 * 4,
-                       IZ = B3 + 16, IH = IZ + kRP * ZS * 2, IX = IH + kRP * HS * 2, IG = IX + kRP * XS * 2,
-                       KL = IG + kRP * GS * 2, TOTAL = KL + 8 * kGW;
+                       IZ = B3 + 16, IH = IZ + DB * kRP * ZS * 2, IX = IH + DB * kRP * HS * 2,
+                       IG = IX + DB * kRP * XS * 2, KL = IG + DB * kRP * GS * 2, TOTAL = KL + 8 * kGW;
+  // image set k (k < DB) of each kind at its base + k * kRP * stride * 2 bytes
   static_assert(IZ % 16 == 0 && IH % 16 == 0 && IX % 16 == 0 && IG % 16 == 0, "16-byte aligned images");
+  static_assert(TOTAL <= 80 * 1024, "two workgroups per CU");
 };
 
 using bf4 = __bf16 __attribute__((ext_vector_type(4)));
@@ -747,10 +760,12 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   if (t0 < NOUT * 64) fW3[t0] = bv1;
   if (t0 < NOUT) fB3[t0] = b3v;
   // constant image columns: H's ones tile (column 64 = 1, 65..79 = 0), G's zero columns 4..15
-  {
+#pragma unroll
+  for (int k = 0; k < S::DB; ++k) {
     const int r = t0 >> 2, c = 64 + 4 * (t0 & 3);  // 64 rows x 4 chunks of 4 columns
-    st_bf4(iH, r * S::HS + c, c == 64 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
-    if ((t0 & 3) != 0) st_bf4(iG, r * S::GS + 4 * (t0 & 3), f4{0.0f, 0.0f, 0.0f, 0.0f});
+    st_bf4(iH + k * kRP * S::HS * 2, r * S::HS + c,
+           c == 64 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
+    if ((t0 & 3) != 0) st_bf4(iG + k * kRP * S::GS * 2, r * S::GS + 4 * (t0 & 3), f4{0.0f, 0.0f, 0.0f, 0.0f});
   }
   __syncthreads();
   f4 acc2[5], acc1[NT1], acc3 = {0.0f, 0.0f, 0.0f, 0.0f}, acc3b = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -760,8 +775,13 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   for (int k = 0; k < NT1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
   double kl = 0.0;
   const float* b3 = fB3;
+  int par = 0;  // pass parity: the [X | 1] / g image set of this pass (DB)
+  char* const iZ2 = iZ + (S::DB > 1 ? kRP * S::ZS * 2 : 0);  // dZ1 (DB) or dZ2 then dZ1
+  char* const iH2 = iH + (S::DB > 1 ? kRP * S::HS * 2 : 0);  // H2 (DB) or H1 then H2
   for (int64_t base = row0; base < row_end; base += kRP) {
     // ================================================================ A
+    char* const pX = iX + (S::DB > 1 ? par * kRP * S::XS * 2 : 0);
+    char* const pG = iG + (S::DB > 1 ? par * kRP * S::GS * 2 : 0);
     const int64_t src_nn = src_of(base + 2 * kRP);
     const RowIn nxt = load_row(src_n);
     const bool live = src >= 0;
@@ -770,7 +790,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       float xv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] = 8 * q + j == D ? 1.0f : cur.x[j];
-      *reinterpret_cast<bf8*>(iX + 2 * (rr * S::XS + 8 * q)) =
+      *reinterpret_cast<bf8*>(pX + 2 * (rr * S::XS + 8 * q)) =
           to_bf8(make_float4(xv[0], xv[1], xv[2], xv[3]), make_float4(xv[4], xv[5], xv[6], xv[7]));
     }
     // forward: mlp_forward's bf16 arithmetic on the prebuilt fragments
@@ -815,7 +835,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       st_bf4(iZ, rr * S::ZS + 16 * t + 4 * q, dZ[t]);
       st_bf4(iH, rr * S::HS + 16 * t + 4 * q, H1[t]);
     }
-    if (q == 0) st_bf4(iG, rr * S::GS, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
+    if (q == 0) st_bf4(pG, rr * S::GS, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
     __syncthreads();
     // ================================================================ B
     // dW2 rows [16 wv, +16) x column tiles 0..3, db2 on tile 4 (the ones column)
@@ -838,26 +858,27 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
         for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
       }
     }
-    __syncthreads();
+    if constexpr (S::DB == 1) __syncthreads();  // (DB: C writes the second image set)
     // ================================================================ C
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      st_bf4(iZ, rr * S::ZS + 16 * t + 4 * q, dZ1[t]);
-      st_bf4(iH, rr * S::HS + 16 * t + 4 * q, H2[t]);
+      st_bf4(iZ2, rr * S::ZS + 16 * t + 4 * q, dZ1[t]);
+      st_bf4(iH2, rr * S::HS + 16 * t + 4 * q, H2[t]);
     }
     __syncthreads();
     // ================================================================ D
     // dW1 (+ db1 at d = D) rows [16 wv, +16); dW3 column tile wv, db3 (wave 0) on the ones tile
 #pragma unroll
     for (int s = 0; s < kRP / 32; ++s) {
-      const bf8 av = tr_frag<S::ZS>(iZ, s, 16 * wv, lane);
+      const bf8 av = tr_frag<S::ZS>(iZ2, s, 16 * wv, lane);
 #pragma unroll
-      for (int c = 0; c < NT1; ++c) acc1[c] = mma16(av, tr_frag<S::XS>(iX, s, 16 * c, lane), acc1[c]);
-      const bf8 gv = tr_frag<S::GS>(iG, s, 0, lane);
-      acc3 = mma16(gv, tr_frag<S::HS>(iH, s, 16 * wv, lane), acc3);
-      if (wv == 0) acc3b = mma16(gv, tr_frag<S::HS>(iH, s, 64, lane), acc3b);
+      for (int c = 0; c < NT1; ++c) acc1[c] = mma16(av, tr_frag<S::XS>(pX, s, 16 * c, lane), acc1[c]);
+      const bf8 gv = tr_frag<S::GS>(pG, s, 0, lane);
+      acc3 = mma16(gv, tr_frag<S::HS>(iH2, s, 16 * wv, lane), acc3);
+      if (wv == 0) acc3b = mma16(gv, tr_frag<S::HS>(iH2, s, 64, lane), acc3b);
     }
-    __syncthreads();  // the next pass overwrites the images
+    if constexpr (S::DB == 1) __syncthreads();  // the next pass overwrites the images (DB: the other set)
+    par ^= 1;
     src = src_n;
     src_n = src_nn;
     cur = nxt;
@@ -903,7 +924,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
 #define RX_PPO_BF_FRAG 1
 #endif
 template <int D>
-__global__ __launch_bounds__(kGT, 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
+__global__ __launch_bounds__(kGT, RX_PPO_BF_DB ? 2 : 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
                                                         float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
   __shared__ __attribute__((aligned(16))) char lds[GradLdsB<D>::TOTAL];
