@@ -696,39 +696,21 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     }
     return in;
   };
-  // ---- the trunk's weight fragments: every staging load into registers first (the
-  // perm indices before them, the first rows' gathers after), then the LDS stores
+  // ---- the trunk's weight fragments.  Coalesced f32 loads of W1 / W2 (the perm
+  // indices before them, the first rows' gathers after) into an LDS scratch in
+  // the image region, then every fragment is assembled from LDS: per-element
+  // gathers from L2 (W1's 60-byte rows, W2's columns for FT2) cost ~400 cache-line
+  // accesses per wave and made staging 35 % of the wave (profiles/r05/
+  // ppo_stamps_bf16.json); coalesced, ~85.
   int64_t src = src_of(row0), src_n = src_of(row0 + kRP);
-  // F1: slot t = (mt = t >> 6, lane): W1[16 mt + l15'][8 q' + j] (zero beyond D)
-  float f1[8];
-  {
-    const int ln = t0 & 63, o = 16 * (t0 >> 6) + (ln & 15), q1 = ln >> 4;
+  constexpr int kW1N = (64 * D + kGT - 1) / kGT;  // W1 elements per thread
+  constexpr int kS2 = 68;                         // W2 scratch row stride (f32, float4-aligned)
+  float w1v[kW1N];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = 8 * q1 + j;
-      f1[j] = d < D ? W[oW1 + o * D + d] : 0.0f;
-    }
-  }
-  // F2 / FT2: slots t + 256 k = (mt, s, lane): F2 = W2[16 mt + l15'][h(s, q', j)],
-  // FT2 = W2[h(s, q', j)][16 mt + l15'], h(s, q, j) = 32 s + 16 (j >> 2) + 4 q + (j & 3)
-  float4 f2[2][2];
-  float ft[2][8];
+  for (int j = 0; j < kW1N; ++j) w1v[j] = t0 + kGT * j < 64 * D ? W[oW1 + t0 + kGT * j] : 0.0f;
+  float4 w2v[4];  // W2 as 1,024 float4: thread t holds float4s t, t + 256, ...
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int sl = t0 + 256 * k, mt = sl >> 7, s = (sl >> 6) & 1, ln = sl & 63, u = 16 * mt + (ln & 15),
-              q1 = ln >> 4;
-    f2[k][0] = *reinterpret_cast<const float4*>(W + oW2 + u * kH + 32 * s + 4 * q1);
-    f2[k][1] = *reinterpret_cast<const float4*>(W + oW2 + u * kH + 32 * s + 16 + 4 * q1);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ft[k][j] = W[oW2 + (32 * s + 16 * (j >> 2) + 4 * q1 + (j & 3)) * kH + u];
-  }
-  // F3: slot t < 128 = (s, lane): W3[l15'][h(s, q', j)] for l15' < NOUT, else 0
-  float4 f3[2] = {make_float4(0.0f, 0.0f, 0.0f, 0.0f), make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
-  if (t0 < 128 && (t0 & 15) < NOUT) {
-    const int s = t0 >> 6, ln = t0 & 63, q1 = ln >> 4;
-    f3[0] = *reinterpret_cast<const float4*>(W + oW3 + (ln & 15) * kH + 32 * s + 4 * q1);
-    f3[1] = *reinterpret_cast<const float4*>(W + oW3 + (ln & 15) * kH + 32 * s + 16 + 4 * q1);
-  }
+  for (int j = 0; j < 4; ++j) w2v[j] = reinterpret_cast<const float4*>(W + oW2)[t0 + kGT * j];
   const float bv0 = t0 < 64 ? W[ob1 + t0] : (t0 < 128 ? W[ob2 + t0 - 64] : 0.0f);
   const float bv1 = t0 < NOUT * 64 ? W[oW3 + t0] : 0.0f;
   const float b3v = t0 < NOUT ? W[ob3 + t0] : 0.0f;
@@ -745,21 +727,57 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   char* iH = lds + S::IH;
   char* iX = lds + S::IX;
   char* iG = lds + S::IG;
-  F1[t0] = to_bf8(make_float4(f1[0], f1[1], f1[2], f1[3]), make_float4(f1[4], f1[5], f1[6], f1[7]));
+  float* sW2 = reinterpret_cast<float*>(lds + S::IZ);  // scratch: W2 [64][kS2], then W1 [64][D]
+  float* sW1 = sW2 + 64 * kS2;
+  static_assert(S::KL - S::IZ >= (64 * kS2 + 64 * D) * 4, "the staging scratch fits in the image region");
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    F2[t0 + 256 * k] = to_bf8(f2[k][0], f2[k][1]);
-    FT2[t0 + 256 * k] = to_bf8(make_float4(ft[k][0], ft[k][1], ft[k][2], ft[k][3]),
-                               make_float4(ft[k][4], ft[k][5], ft[k][6], ft[k][7]));
+  for (int j = 0; j < kW1N; ++j)
+    if (t0 + kGT * j < 64 * D) sW1[t0 + kGT * j] = w1v[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e4 = t0 + kGT * j, o = e4 >> 4, i = 4 * (e4 & 15);
+    *reinterpret_cast<float4*>(sW2 + o * kS2 + i) = w2v[j];
   }
-  if (t0 < 128) F3[t0] = to_bf8(f3[0], f3[1]);
   if (t0 < 64)
     fB1[t0] = bv0;
   else if (t0 < 128)
     fB2[t0 - 64] = bv0;
   if (t0 < NOUT * 64) fW3[t0] = bv1;
   if (t0 < NOUT) fB3[t0] = b3v;
+  __syncthreads();
+  {  // F1: slot t = (mt = t >> 6, lane): W1[16 mt + l15'][8 q' + j] (zero beyond D)
+    const int ln = t0 & 63, o = 16 * (t0 >> 6) + (ln & 15), q1 = ln >> 4;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 8 * q1 + j < D ? sW1[o * D + 8 * q1 + j] : 0.0f;
+    F1[t0] = to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  }
+  // F2 / FT2: slots t + 256 k = (mt, s, lane): F2 = W2[16 mt + l15'][h(s, q', j)],
+  // FT2 = W2[h(s, q', j)][16 mt + l15'], h(s, q, j) = 32 s + 16 (j >> 2) + 4 q + (j & 3)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int sl = t0 + 256 * k, mt = sl >> 7, s = (sl >> 6) & 1, ln = sl & 63, u = 16 * mt + (ln & 15),
+              q1 = ln >> 4;
+    F2[sl] = to_bf8(*reinterpret_cast<const float4*>(sW2 + u * kS2 + 32 * s + 4 * q1),
+                    *reinterpret_cast<const float4*>(sW2 + u * kS2 + 32 * s + 16 + 4 * q1));
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = sW2[(32 * s + 16 * (j >> 2) + 4 * q1 + (j & 3)) * kS2 + u];
+    FT2[sl] = to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  }
+  // F3: slot t < 128 = (s, lane): W3[l15'][h(s, q', j)] for l15' < NOUT, else 0
+  if (t0 < 128) {
+    const int s = t0 >> 6, ln = t0 & 63, q1 = ln >> 4;
+    float4 lo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), hi = lo;
+    if ((ln & 15) < NOUT) {
+      lo = *reinterpret_cast<const float4*>(fW3 + (ln & 15) * kH + 32 * s + 4 * q1);
+      hi = *reinterpret_cast<const float4*>(fW3 + (ln & 15) * kH + 32 * s + 16 + 4 * q1);
+    }
+    F3[t0] = to_bf8(lo, hi);
+  }
+  __syncthreads();  // the scratch is dead: the images may be written
   // constant image columns: H's ones tile (column 64 = 1, 65..79 = 0), G's zero columns 4..15
+  // (read only after the next pass's first barrier)
 #pragma unroll
   for (int k = 0; k < S::DB; ++k) {
     const int r = t0 >> 2, c = 64 + 4 * (t0 & 3);  // 64 rows x 4 chunks of 4 columns
@@ -767,7 +785,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
            c == 64 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
     if ((t0 & 3) != 0) st_bf4(iG + k * kRP * S::GS * 2, r * S::GS + 4 * (t0 & 3), f4{0.0f, 0.0f, 0.0f, 0.0f});
   }
-  __syncthreads();
+  PPO_STAMP(1);
   f4 acc2[5], acc1[NT1], acc3 = {0.0f, 0.0f, 0.0f, 0.0f}, acc3b = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int k = 0; k < 5; ++k) acc2[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -776,6 +794,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   double kl = 0.0;
   const float* b3 = fB3;
   int par = 0;  // pass parity: the [X | 1] / g image set of this pass (DB)
+  int pass_ = 0;
   char* const iZ2 = iZ + (S::DB > 1 ? kRP * S::ZS * 2 : 0);  // dZ1 (DB) or dZ2 then dZ1
   char* const iH2 = iH + (S::DB > 1 ? kRP * S::HS * 2 : 0);  // H2 (DB) or H1 then H2
   for (int64_t base = row0; base < row_end; base += kRP) {
@@ -837,6 +856,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     }
     if (q == 0) st_bf4(pG, rr * S::GS, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
     __syncthreads();
+    PPO_STAMP(2 + 4 * pass_);
     // ================================================================ B
     // dW2 rows [16 wv, +16) x column tiles 0..3, db2 on tile 4 (the ones column)
 #pragma unroll
@@ -859,6 +879,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       }
     }
     if constexpr (S::DB == 1) __syncthreads();  // (DB: C writes the second image set)
+    PPO_STAMP(3 + 4 * pass_);
     // ================================================================ C
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -866,6 +887,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       st_bf4(iH2, rr * S::HS + 16 * t + 4 * q, H2[t]);
     }
     __syncthreads();
+    PPO_STAMP(4 + 4 * pass_);
     // ================================================================ D
     // dW1 (+ db1 at d = D) rows [16 wv, +16); dW3 column tile wv, db3 (wave 0) on the ones tile
 #pragma unroll
@@ -878,12 +900,16 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       if (wv == 0) acc3b = mma16(gv, tr_frag<S::HS>(iH2, s, 64, lane), acc3b);
     }
     if constexpr (S::DB == 1) __syncthreads();  // the next pass overwrites the images (DB: the other set)
+    PPO_STAMP(5 + 4 * pass_);
+    ++pass_;
     par ^= 1;
     src = src_n;
     src_n = src_nn;
     cur = nxt;
   }
+  (void)pass_;  // (indexes the profiling build's stamps only)
   // ---- tile accumulators -> the partial row (each wave owns its tiles)
+  PPO_STAMP(14);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int o = 16 * wv + 4 * q + r;
@@ -915,6 +941,10 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     __syncthreads();
     if (t0 == 0) a.kl_partial[blockIdx.x] = (kd[0] + kd[2]) + (kd[1] + kd[3]);
   }
+#ifdef RX_PPO_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);  // the partial-row stores landed (profiling build)
+#endif
+  PPO_STAMP(15);
 }
 
 // bf16 (RX_PPO_BF_FRAG = 1, the default): the fragment / transposed-image trunk
@@ -927,6 +957,7 @@ template <int D>
 __global__ __launch_bounds__(kGT, RX_PPO_BF_DB ? 2 : 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
                                                         float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
+  PPO_STAMP(0);
   __shared__ __attribute__((aligned(16))) char lds[GradLdsB<D>::TOTAL];
   float* out = partial + (size_t)blockIdx.x * Lay<D>::Pp;
   if (blockIdx.y == 0)

@@ -82,8 +82,9 @@ for m in range(4, 12):
                 "end_spread_cycles": float(s[ok, -1].max() - np.percentile(s[ok, -1], 1))})
     a = st[:, [1, 16, 17, 18, 19, 2]]  # pass 0, phase A: layer 1, layer 2, head, loss, dZ2 + transposes
     ok = (a > 0).all(axis=1)
-    res[-1]["p0A_sub_cycles_median"] = dict(zip(["layer1", "layer2", "head", "loss", "dz2_lds"],
-                                                np.median(np.diff(a[ok], axis=1), axis=0).round(0).tolist()))
+    if ok.any():  # (the fp32 trunk's forward sub-stamps; the bf16 trunk has none)
+        res[-1]["p0A_sub_cycles_median"] = dict(zip(["layer1", "layer2", "head", "loss", "dz2_lds"],
+                                                    np.median(np.diff(a[ok], axis=1), axis=0).round(0).tolist()))
 labels = ["stage"] + [f"p{p}{ph}" for p in range(res[-1]["passes"]) for ph in "ABCD"] + ["accum", "small"]
 out = {"mb": mb, "precision": prec, "n_wg_per_trunk": n_wg, "labels": labels, "runs": res[-3:]}
 print(json.dumps(out))
