@@ -112,6 +112,7 @@ struct rx_env {
   DevBuf<rx_kargs> win_args;               // k_window / k_flow per-step argument blocks [RX_WIN_MAX_STEPS]
   int32_t flow_grid = 0;                   // k_flow one-wave workgroups (resident capacity)
   DevBuf<int32_t> flow_q, flow_ctl, flow_cnt;  // k_flow queues [8][cap], control words, block arrival counters
+  DevBuf<uint8_t> policy_frag;  // the bf16 rollout's operand fragments of both trunks (k_policy_frag, rx_rollout_steps)
   int32_t flow_cap = 0;
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
@@ -733,6 +734,12 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
       }
     }
   }
+  if (!h->policy_frag.p) {  // allocated here, not in rx_rollout_steps: it may run inside a graph capture
+    RX_HIP(hipSetDevice(h->cfg.device));
+    if (hipMalloc(&h->policy_frag.p, rx_policy_frag_bytes()) != hipSuccess)
+      return fail(RX_ENOMEM, "rx_assign: policy fragment image");
+    h->policy_frag.n = rx_policy_frag_bytes();
+  }
   h->assigned = true;
   h->tasks_stale = true;
   h->sort_pending = false;
@@ -1264,13 +1271,22 @@ int rx_rollout_steps(rx_env* h, const rx_io* io, const rx_rollout_io* r, int32_t
   if (precision != RX_PREC_FP32 && precision != RX_PREC_BF16)
     return fail(RX_EINVAL, "rx_rollout_steps: precision=%d (RX_PREC_FP32 or RX_PREC_BF16)", precision);
   const int64_t N = h->cfg.n_envs, D = h->D;
+  // bf16: the parameters are fixed for the whole rollout, so their bf16 operand
+  // fragments are built once (k_policy_frag) and every step's policy launch
+  // reads them -- the same bf16 values rx_policy_act converts per use
+  const void* frag = nullptr;
+  if (precision == RX_PREC_BF16) {
+    if (rx_launch_policy_frag(r->obs_dim, r->params, h->policy_frag.p, (hipStream_t)stream))
+      return fail(RX_EHIP, "rx_rollout_steps: fragment launch failed");
+    frag = h->policy_frag.p;
+  }
   for (int32_t t = 0; t < r->T; ++t) {
     const bool last = t + 1 == r->T;
     const rx_policy_io pio{r->obs_dim, N, r->obs + t * N * D, r->eps + t * N * 2, r->params, r->log_std,
                            r->actions + t * N * 2, r->logprobs + t * N, r->values + t * N, 0, 0, precision,
                            nullptr, 0};
-    int rc = rx_policy_act(&pio, stream);
-    if (rc) return rc;
+    int rc = rx_launch_policy_act(&pio, (hipStream_t)stream, frag);
+    if (rc) return fail(RX_EHIP, "rx_rollout_steps: policy launch failed: %s", hipGetErrorString((hipError_t)rc));
     rx_io s = *io;
     s.actions = r->actions + t * N * 2;
     s.obs = last ? r->next_obs : r->obs + (t + 1) * N * D;

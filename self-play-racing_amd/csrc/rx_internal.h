@@ -279,7 +279,10 @@ extern "C" int rx_launch_adam(const rx_adam_config* cfg, float* p, float* g, flo
                               const double* lr, const uint8_t* stop, float* ws, hipStream_t s);
 extern "C" size_t rx_ppo_partial_floats(int obs_dim, int mb);
 extern "C" int rx_ppo_n_wg(int mb);
-extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s);
+// frag: NULL, or (bf16) the rollout's fragment image from rx_launch_policy_frag
+extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s, const void* frag = nullptr);
+extern "C" size_t rx_policy_frag_bytes();
+extern "C" int rx_launch_policy_frag(int obs_dim, const float* params, void* img, hipStream_t s);
 // both self-play policies of a rollout step in one launch (obs_dim 19; k_selfplay_act)
 extern "C" int rx_launch_selfplay_act(const rx_policy_io* ag, const rx_policy_io* op, float* obs_out,
                                       const float* rew_src, float* rew_out, int agent, hipStream_t s);

@@ -166,15 +166,48 @@ __device__ __forceinline__ void mlp_forward(const Wt& w, const float (&x)[Geo<D>
   }
 }
 
+// The bf16 forward of mlp_forward on PREBUILT operand fragments (16 bytes per
+// lane per MFMA operand, in exactly the element order mlp_forward's bf16 path
+// converts): F1[mt][lane] layer 1, F2[2 mt + s][lane] layer 2, F3[s][lane] the head
+// (rows >= NOUT zero).  Same bf16 values, same MFMAs in the same order as
+// mlp_forward<.., kBF16>: bit-identical.  The pointers may be LDS (k_ppo_grad_bf)
+// or global (the rollout's per-rollout image, k_policy_frag).
+template <int NOUT>
+__device__ __forceinline__ void mlp_forward_frag(const bf8* F1, const bf8* F2, const bf8* F3, const float* b1,
+                                                 const float* b2, const float (&x)[8], f4 (&H1)[4], f4 (&H2)[4],
+                                                 f4& y, int lane, int q) {
+  const bf8 bx = to_bf8(make_float4(x[0], x[1], x[2], x[3]), make_float4(x[4], x[5], x[6], x[7]));
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const f4 z = mma16(F1[mt * 64 + lane], bx, f4{0.0f, 0.0f, 0.0f, 0.0f});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + b1[16 * mt + 4 * q + r]);
+  }
+  const bf8 bh[2] = {to_bf8(H1[0], H1[1]), to_bf8(H1[2], H1[3])};
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) z = mma16(F2[(2 * mt + s) * 64 + lane], bh[s], z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + b2[16 * mt + 4 * q + r]);
+  }
+  y = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) y = mma16(F3[s * 64 + lane], to_bf8(H2[2 * s], H2[2 * s + 1]), y);
+}
+// one trunk's fragment image in global memory (k_policy_frag): F1 | F2 | F3
+constexpr int kFragF1 = 0, kFragF2 = 4 * 64, kFragF3 = kFragF2 + 8 * 64, kFragTrunk = kFragF3 + 2 * 64;  // bf8 units
+
 // Rollout policy step (agent/ppo.py:105-110, get_action_and_value on obs[t]):
 // per row  action = clamp(eps * std + mu, -1, 1)   (Normal.sample() = normal_() * std + mu)
 //          logp   = sum_j Normal(mu, std).log_prob(action_j),  value = critic(obs).
 // eps [N][2] is drawn by the caller with torch's normal_() so the sampling
 // stream is torch's.  Wave = 16 rows of one trunk, weights straight from the
 // (L2-resident) parameter buffer.
-template <int D, int PREC>
+template <int D, int PREC, bool FRAG = false>
 __device__ __forceinline__ void policy_rows(const rx_policy_io& io, const float* __restrict__ P, bool critic,
-                                            int64_t rb) {
+                                            int64_t rb, const bf8* __restrict__ frag = nullptr) {
   using L = Lay<D>;
   constexpr int XN = Geo<D>::template XN<PREC>;
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
@@ -191,7 +224,10 @@ __device__ __forceinline__ void policy_rows(const rx_policy_io& io, const float*
   f4 H1[4], H2[4], y;
   if (!critic) {
     const WGlobal w{P + L::aW1, P + L::ab1, P + L::aW2, P + L::ab2, P + L::aW3, P + L::ab3, D};
-    mlp_forward<D, kNA, PREC>(w, x, H1, H2, y, l15, q);
+    if constexpr (FRAG && PREC == kBF16)
+      mlp_forward_frag<kNA>(frag + kFragF1, frag + kFragF2, frag + kFragF3, w.b1, w.b2, x, H1, H2, y, lane, q);
+    else
+      mlp_forward<D, kNA, PREC>(w, x, H1, H2, y, l15, q);
     if (q != 0 || !live) return;
     float logp = 0.0f;
 #pragma unroll
@@ -208,7 +244,12 @@ __device__ __forceinline__ void policy_rows(const rx_policy_io& io, const float*
     if (io.logprobs) io.logprobs[row] = logp;
   } else {
     const WGlobal w{P + L::cW1, P + L::cb1, P + L::cW2, P + L::cb2, P + L::cW3, P + L::cb3, D};
-    mlp_forward<D, 1, PREC>(w, x, H1, H2, y, l15, q);
+    if constexpr (FRAG && PREC == kBF16) {
+      const bf8* fc = frag + kFragTrunk;
+      mlp_forward_frag<1>(fc + kFragF1, fc + kFragF2, fc + kFragF3, w.b1, w.b2, x, H1, H2, y, lane, q);
+    } else {
+      mlp_forward<D, 1, PREC>(w, x, H1, H2, y, l15, q);
+    }
     if (q != 0 || !live) return;
     io.values[row] = y[0] + P[L::cb3];
   }

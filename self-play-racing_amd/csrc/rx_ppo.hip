@@ -112,13 +112,48 @@ struct WLds {
   __device__ float w3(int j, int h) const { return W3[j * kH + h]; }
 };
 
-template <int D, int PREC>
-__global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P) {
+template <int D, int PREC, bool FRAG = false>
+__global__ __launch_bounds__(kT) void k_policy_act(rx_policy_io io, const float* __restrict__ P,
+                                                   const bf8* __restrict__ frag) {
   // a workgroup's 4 waves run ONE trunk (even workgroups actor, odd critic) on
   // 4 consecutive 16-row blocks, so a CU's L1 holds one trunk's 21 KB of weights
   const bool critic = blockIdx.x & 1;
   const int64_t rb = (int64_t)(blockIdx.x >> 1) * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  policy_rows<D, PREC>(io, P, critic, rb);
+  policy_rows<D, PREC, FRAG>(io, P, critic, rb, frag);
+}
+
+// The bf16 rollout's fragment image (rx_rollout_steps, once per rollout: the
+// parameters do not change inside it): per trunk (workgroup y) F1 | F2 | F3 in
+// mlp_forward_frag's layout, the same bf16 conversions mlp_forward's bf16 path
+// does per use -- so every rollout policy launch reads one 16-byte fragment per
+// MFMA operand from L2 instead of 8 scalar loads and 4 conversions.
+template <int D>
+__global__ __launch_bounds__(256) void k_policy_frag(const float* __restrict__ P, bf8* __restrict__ img) {
+  using L = Lay<D>;
+  const bool critic = blockIdx.x == 1;
+  const float* W1 = P + (critic ? L::cW1 : L::aW1);
+  const float* W2 = P + (critic ? L::cW2 : L::aW2);
+  const float* W3 = P + (critic ? L::cW3 : L::aW3);
+  const int nout = critic ? 1 : kNA;
+  bf8* out = img + (critic ? kFragTrunk : 0);
+  for (int sl = threadIdx.x; sl < kFragTrunk; sl += 256) {
+    const int ln = sl & 63, l15 = ln & 15, q = ln >> 4;
+    float v[8];
+    if (sl < kFragF2) {  // F1[mt][lane] = W1[16 mt + l15][8 q + j] (zero beyond D)
+      const int o = 16 * (sl >> 6) + l15;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 8 * q + j < D ? W1[o * D + 8 * q + j] : 0.0f;
+    } else if (sl < kFragF3) {  // F2[2 mt + s][lane] = W2[16 mt + l15][h(s, q, j)]
+      const int k = (sl - kFragF2) >> 6, mt = k >> 1, s = k & 1, o = 16 * mt + l15;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = W2[o * kH + 32 * s + 16 * (j >> 2) + 4 * q + (j & 3)];
+    } else {  // F3[s][lane] = W3[l15][h(s, q, j)] for l15 < n_out, else 0
+      const int s = (sl - kFragF3) >> 6;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = l15 < nout ? W3[l15 * kH + 32 * s + 16 * (j >> 2) + 4 * q + (j & 3)] : 0.0f;
+    }
+    out[sl] = to_bf8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  }
 }
 
 // One self-play rollout step's policies in ONE launch (rx_selfplay_rollout_steps):
@@ -814,28 +849,7 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     }
     // forward: mlp_forward's bf16 arithmetic on the prebuilt fragments
     f4 H1[4], H2[4], y;
-    {
-      const bf8 bx = to_bf8(make_float4(cur.x[0], cur.x[1], cur.x[2], cur.x[3]),
-                            make_float4(cur.x[4], cur.x[5], cur.x[6], cur.x[7]));
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f4 z = mma16(F1[mt * 64 + lane], bx, f4{0.0f, 0.0f, 0.0f, 0.0f});
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H1[mt][r] = rx_policy::tanh_fast(z[r] + fB1[16 * mt + 4 * q + r]);
-      }
-      const bf8 bh[2] = {to_bf8(H1[0], H1[1]), to_bf8(H1[2], H1[3])};
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) z = mma16(F2[(2 * mt + s) * 64 + lane], bh[s], z);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H2[mt][r] = rx_policy::tanh_fast(z[r] + fB2[16 * mt + 4 * q + r]);
-      }
-      y = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) y = mma16(F3[s * 64 + lane], to_bf8(H2[2 * s], H2[2 * s + 1]), y);
-    }
+    mlp_forward_frag<NOUT>(F1, F2, F3, fB1, fB2, cur.x, H1, H2, y, lane, q);
     float g[NOUT];
     head_grad<NET>(b, cur.s0, cur.s1, cur.s2, cur.s3, live, y, b3, l15, q, var, lsc, mean, sd, invM, clip, g, kl);
     f4 dZ[4];  // dZ2 = (W3^T g) * (1 - H2^2)
@@ -1565,21 +1579,36 @@ extern "C" int rx_launch_selfplay_act(const rx_policy_io* ag, const rx_policy_io
   return (int)hipGetLastError();
 }
 
-extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s) {
+extern "C" int rx_launch_policy_act(const rx_policy_io* io, hipStream_t s, const void* frag) {
   // one wave per 16 rows and trunk, 4 waves (one trunk) per workgroup
   const int64_t blocks16 = (io->n + 15) / 16;
   const int n_wg = (int)(2 * ((blocks16 + 3) / 4));
   const bool bf = io->precision == kBF16;
+  const bf8* fr = static_cast<const bf8*>(frag);
   if (io->obs_dim == 15) {
-    if (bf)
-      hipLaunchKernelGGL((k_policy_act<15, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    if (bf && fr)
+      hipLaunchKernelGGL((k_policy_act<15, kBF16, true>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
+    else if (bf)
+      hipLaunchKernelGGL((k_policy_act<15, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
     else
-      hipLaunchKernelGGL((k_policy_act<15, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+      hipLaunchKernelGGL((k_policy_act<15, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
   } else {
-    if (bf)
-      hipLaunchKernelGGL((k_policy_act<19, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+    if (bf && fr)
+      hipLaunchKernelGGL((k_policy_act<19, kBF16, true>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
+    else if (bf)
+      hipLaunchKernelGGL((k_policy_act<19, kBF16>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
     else
-      hipLaunchKernelGGL((k_policy_act<19, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params);
+      hipLaunchKernelGGL((k_policy_act<19, kF32>), dim3(n_wg), dim3(kT), 0, s, *io, io->params, fr);
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" size_t rx_policy_frag_bytes() { return 2 * (size_t)kFragTrunk * sizeof(bf8); }
+
+extern "C" int rx_launch_policy_frag(int obs_dim, const float* params, void* img, hipStream_t s) {
+  if (obs_dim == 15)
+    hipLaunchKernelGGL(k_policy_frag<15>, dim3(2), dim3(256), 0, s, params, static_cast<bf8*>(img));
+  else
+    hipLaunchKernelGGL(k_policy_frag<19>, dim3(2), dim3(256), 0, s, params, static_cast<bf8*>(img));
   return (int)hipGetLastError();
 }

@@ -173,7 +173,7 @@ def test_configs0_one_env_ppo_iteration():
                                    err_msg=k)
 
 
-@pytest.mark.parametrize("n,T,prec", [(4096, 64, "fp32"), (3000, 40, "bf16"), (64, 30, "fp32")])
+@pytest.mark.parametrize("n,T,prec", [(4096, 64, "fp32"), (4096, 32, "bf16"), (3000, 40, "bf16"), (64, 30, "fp32")])
 def test_rollout_steps_equals_per_step_path(n, T, prec):
     """rx_rollout_steps (ABI v19: T x (rx_policy_act + rx_step) enqueued by ONE
     call, the default eager rollout of every single-agent handle the persistent
