@@ -1601,6 +1601,25 @@ __device__ __forceinline__ bool seg_may_hit(const float4 f, const seg_pref& pf) 
   const float dp = __builtin_fmaf(f.w, pf.v3f.y, f.z * pf.v3f.x);
   return !(__builtin_fabsf(__builtin_fmaf(2.0f, aa, -dp)) - __builtin_fabsf(dp) > pf.e2);
 }
+// |x| - |y| as ONE v_sub_f32 with abs modifiers (the packed VALU has none)
+__device__ __forceinline__ float abs_sub(float x, float y) {
+  float d;
+  asm("v_sub_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
+  return d;
+}
+// seg_may_hit for two segments at once, the same float32 operations: a, p and
+// 2a - p of both in packed fmas (v_pk_fma_f32: 2.5 VALU per segment), then
+// one abs-subtract each (left to itself the compiler pairs the abs-subtracts too,
+// as 4 v_and + 1 v_pk_add, or packs nothing).  Same roundings: same decisions.
+__device__ __forceinline__ void seg_may_hit2(const float4 f0, const float4 f1, const seg_pref& pf, bool& h0,
+                                             bool& h1) {
+  const rx_f2 vx = {pf.v3f.x, pf.v3f.x}, vy = {pf.v3f.y, pf.v3f.y}, c0 = {pf.c0, pf.c0};
+  const rx_f2 aa = __builtin_elementwise_fma(-rx_f2{f0.y, f1.y}, vy, __builtin_elementwise_fma(-rx_f2{f0.x, f1.x}, vx, c0));
+  const rx_f2 dp = __builtin_elementwise_fma(rx_f2{f0.w, f1.w}, vy, rx_f2{f0.z, f1.z} * vx);
+  const rx_f2 u = __builtin_elementwise_fma(rx_f2{2.0f, 2.0f}, aa, -dp);
+  h0 = !(abs_sub(u.x, dp.x) > pf.e2);
+  h1 = !(abs_sub(u.y, dp.y) > pf.e2);
+}
 
 // Segments [j0, j1) of a wave-uniform slot, four scalar loads in flight at a
 // time (each test ends in a divergent branch, so a plain loop would wait for
@@ -1614,8 +1633,10 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
     for (; j + 4 <= j1; j += 4) {
       const float4 f0 = ldu(pf.segf + j), f1 = ldu(pf.segf + j + 1), f2 = ldu(pf.segf + j + 2),
                    f3 = ldu(pf.segf + j + 3);
-      const bool h0 = __any(seg_may_hit(f0, pf)), h1 = __any(seg_may_hit(f1, pf)), h2 = __any(seg_may_hit(f2, pf)),
-                 h3 = __any(seg_may_hit(f3, pf));
+      bool m0, m1, m2, m3;
+      seg_may_hit2(f0, f1, pf, m0, m1);
+      seg_may_hit2(f2, f3, pf, m2, m3);
+      const bool h0 = __any(m0), h1 = __any(m1), h2 = __any(m2), h3 = __any(m3);
       if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
       if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best);
       if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best);
