@@ -1595,6 +1595,9 @@ struct seg_pref {
   rx_f2 v3f;                        // (-sin, cos) in float32
   float c0;                         // of . v3f: the float32 origin projected on v3
   float e2;                         // 2^-17 (|ox| + |oy| + max(|sx| + |sy|) + L + 1)
+#ifdef RX_RAY_STAMPS
+  int* cnt;  // profiling build: [0] segments pre-filtered, [1] exact tests run, [2] of them with a lane's hit
+#endif
 };
 __device__ __forceinline__ bool seg_may_hit(const float4 f, const seg_pref& pf) {
   const float aa = __builtin_fmaf(-f.y, pf.v3f.y, __builtin_fmaf(-f.x, pf.v3f.x, pf.c0));
@@ -1637,6 +1640,18 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
       seg_may_hit2(f0, f1, pf, m0, m1);
       seg_may_hit2(f2, f3, pf, m2, m3);
       const bool h0 = __any(m0), h1 = __any(m1), h2 = __any(m2), h3 = __any(m3);
+#ifdef RX_RAY_STAMPS
+      pf.cnt[0] += 4;
+      const bool hh[4] = {h0, h1, h2, h3};
+      for (int u = 0; u < 4; ++u) {
+        if (!hh[u]) continue;
+        const double b0 = best;
+        seg_test(ldu(seg + j + u), ox, oy, v3x, v3y, best);
+        pf.cnt[1] += 1;
+        pf.cnt[2] += __any(best != b0) ? 1 : 0;
+      }
+      continue;
+#endif
       if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
       if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best);
       if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best);
@@ -1843,7 +1858,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 template <int A, int LPR, bool C = false>
 __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
 #ifdef RX_RAY_STAMPS
-  unsigned long long rstamp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long rstamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   rstamp[6] = wall_clock64();
   RAY_STAMP(0);
 #endif
@@ -1924,10 +1939,17 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     const int quad0 = uniform(quad);
     int scanned = 0, tested = 0;
     // segment pre-filter operands (seg_may_hit): |sx| + |sy| <= |cx| + |cy| + 2 rad for every boundary point
+#ifdef RX_RAY_STAMPS
+    int cnt[3] = {0, 0, 0};
+#endif
     const seg_pref pf{reinterpret_cast<const float4*>(a.tr.seg_f) + 2 * wp0, rx_f2{-snf, csf},
                       __builtin_fmaf(oyf, csf, oxf * -snf),
                       (float)((__builtin_fabs(ox) + __builtin_fabs(oy) + __builtin_fabs(cx) + __builtin_fabs(cy) +
-                               2.0 * rad + L + 1.0) * 0x1p-17)};
+                               2.0 * rad + L + 1.0) * 0x1p-17)
+#ifdef RX_RAY_STAMPS
+                      , cnt
+#endif
+    };
     RAY_STAMP(3);
     auto scan = [&](auto filt) {
       constexpr bool F = decltype(filt)::value;
@@ -1949,6 +1971,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
 #ifdef RX_RAY_STAMPS
     rstamp[8] = (unsigned long long)tested;
     rstamp[9] = (unsigned long long)scanned;
+    rstamp[10] = (unsigned long long)cnt[1] | ((unsigned long long)cnt[2] << 32);  // exact tests | that lowered a best
+    rstamp[11] = (unsigned long long)cnt[0];                                       // segments pre-filtered
 #else
     if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
       atomicAdd(&a.io.counters[0], (unsigned long long)tested);
@@ -1961,7 +1985,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   RAY_STAMP(5);
   rstamp[7] = wall_clock64();
   if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))
-    for (int j = 0; j < 10; ++j) a.io.counters[16 + 12 * wave + j] = rstamp[j];
+    for (int j = 0; j < 12; ++j) a.io.counters[16 + 12 * wave + j] = rstamp[j];
 #endif
 }
 

@@ -6,8 +6,10 @@ in-kernel s_memtime stamps.
 
 Phases per ray wave (stamps after a full s_waitcnt): 0->1 task id, state
 loads; 1->2 sincos; 2->3 culling setup; 3->4 box traversal + leaf scans;
-4->5 obs store.  Also per wave: wall-clock start / end (100 MHz), box tests and
-leaf scans.  Reported for all waves, by dispatch rank (ray-wave class run,
+4->5 obs store.  Also per wave: wall-clock start / end (100 MHz), box tests,
+leaf scans, segments through the float32 pre-filter (4-segment groups), exact
+segment tests run (some lane passed the pre-filter) and those that lowered
+some lane's best.  Reported for all waves, by dispatch rank (ray-wave class run,
 RX_RAY_DISPATCH 3) and for the waves that end in the last 25 % of the launch
 (the tail).  Profiling variant only; the product library has no stamps.
 Reference: environment/track.py:173-199 (the raycast these waves compute).
@@ -41,7 +43,9 @@ def stats(d, sel):
     return {"waves": int(sel.sum()), "phase_cycles_median": np.median(x[:, :5], axis=0).round(0).tolist(),
             "phase_cycles_mean": x[:, :5].mean(axis=0).round(0).tolist(),
             "wall_us_mean": round(float(x[:, 5].mean()), 2), "box_tests_mean": round(float(x[:, 6].mean()), 1),
-            "leaf_scans_mean": round(float(x[:, 7].mean()), 2)}
+            "leaf_scans_mean": round(float(x[:, 7].mean()), 2),
+            "segments_prefiltered_mean": round(float(x[:, 10].mean()), 1),
+            "exact_tests_mean": round(float(x[:, 8].mean()), 1), "exact_tests_lowering_best_mean": round(float(x[:, 9].mean()), 1)}
 
 
 def main():
@@ -67,9 +71,13 @@ def main():
         env.counters.zero_()
         env.step_device(act())
         torch.cuda.synchronize()
-        st = env.counters[16:].view(nrw, 12)[:, :10].cpu().numpy().astype(np.float64)
+        raw = env.counters[16:].view(nrw, 12).cpu().numpy()
+        st = raw[:, :10].astype(np.float64)
         ok = st[:, 0] > 0
-        d = np.zeros((nrw, 8))
+        d = np.zeros((nrw, 11))
+        d[:, 8] = (raw[:, 10] & 0xFFFFFFFF).astype(np.float64)  # exact segment tests (some lane passed the pre-filter)
+        d[:, 9] = (raw[:, 10] >> 32).astype(np.float64)  # of them: a lane's best lowered
+        d[:, 10] = raw[:, 11].astype(np.float64)  # segments through the pre-filter (4-segment groups)
         d[:, :5] = np.diff(st[:, :6], axis=1)
         d[:, 5] = (st[:, 7] - st[:, 6]) / 100.0  # 100 MHz ticks -> us
         d[:, 6:8] = st[:, 8:10]
