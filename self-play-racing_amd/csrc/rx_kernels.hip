@@ -1725,19 +1725,26 @@ __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, i
 // Chunks are visited outward from the wave's first car, so best tightens
 // early; envs are kept spatially sorted (write_sort_key) so a wave's cars
 // are neighbours.
-// The slab test runs in packed float32 on outward-rounded f32 boxes (x and y
-// slabs in one v_pk_add / v_pk_mul each).  Conservative by construction
-// (DESIGN.md §3): the per-lane box margin mbf adds 3(|ox|+|oy|+1)2^-24 for the
-// f32 rounding of the origin, every remaining rounding scales a slab endpoint
-// by at most 1 +- 6*2^-24, and the slack k = 2^-20 > 2 * 6*2^-24 on both the
-// empty-interval test and the entry distance absorbs it; bestf >= best.  An
-// f32 direction component of 0 gives +-inf slab bounds (NaN when the origin
-// sits on the slab plane, which fmin/fmax drop: the axis is then unconstrained).
-__device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 nlo, rx_f2 nhi, rx_f2 id2,
+// The slab test runs in packed float32 on outward-rounded f32 boxes: a slab
+// plane's t = (b + n) / d is ONE v_pk_fma_f32 per box corner, b * id + c with
+// the lane's c = n * id (n = the margin-grown origin offset, id = 1 / d)
+// computed once per ray.  Conservative by construction: the
+// per-lane box margin mbf adds 3(|ox|+|oy|+1)2^-24 for the f32 rounding of the
+// origin and 2^-22(|ox|+|oy|+mbf) for the rounding of c (an absolute error of
+// at most 2^-24 |n| in position units, covered 4x); the remaining roundings
+// scale a slab endpoint by at most 1 +- 6*2^-24, and the slack k = 2^-20 >
+// 2 * 6*2^-24 on both the empty-interval test and the entry distance absorbs
+// them; bestf >= best.  |b * id| stays far below f32 overflow: no double lies
+// within 2^-64 of an odd multiple of pi/2 at the angles a car reaches, so a
+// nonzero cos / sin rounds to |d| > 2^-65 and |id| < 2^65.  An f32
+// direction component of 0 makes id and c infinite: b * inf + c is +-inf or
+// NaN, and fmin / fmax drop a NaN, leaving the axis unconstrained -- more
+// boxes kept, never fewer.
+__device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 clo, rx_f2 chi, rx_f2 id2,
                                                float mtf, float bestf) {
   const float4 b = ldu(reinterpret_cast<const float4*>(box));
-  const rx_f2 t1 = (rx_f2{b.x, b.y} + nlo) * id2;
-  const rx_f2 t2 = (rx_f2{b.z, b.w} + nhi) * id2;
+  const rx_f2 t1 = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, clo);
+  const rx_f2 t2 = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, chi);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1.x, t2.x), __builtin_fminf(t1.y, t2.y)), -mtf);
   const float hi = __builtin_fminf(__builtin_fmaxf(t1.x, t2.x), __builtin_fmaxf(t1.y, t2.y));
   const float k = 0x1p-20f;
@@ -1751,17 +1758,17 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
 
 // chunk_needed_f for a wave whose lanes all cast into one direction quadrant:
 // the box comes quadrant-ordered as (near.x, near.y, far.x, far.y) and nn / nf
-// are the matching origin offsets, so each axis' entry / exit distance needs no
+// are the matching origin offsets (times id), so each axis' entry / exit distance needs no
 // min / max (4 fewer VALU).  Same decision as chunk_needed_f: with the axis'
 // direction sign fixed, rounding is monotone, so min(t1, t2) IS the near
 // plane's t and max(t1, t2) the far one's; only where chunk_needed_f meets a
 // NaN (0 * inf: origin on a slab plane, f32 direction component 0) does this
 // test drop the NaN and keep the box -- more conservative, never less.
-__device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx_f2 nn, rx_f2 nf, rx_f2 id2,
+__device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx_f2 cn, rx_f2 cf, rx_f2 id2,
                                                float mtf, float bestf) {
   const float4 b = ldu(reinterpret_cast<const float4*>(box));
-  const rx_f2 tn = (rx_f2{b.x, b.y} + nn) * id2;
-  const rx_f2 tf = (rx_f2{b.z, b.w} + nf) * id2;
+  const rx_f2 tn = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, cn);
+  const rx_f2 tf = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, cf);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), -mtf);
   const float hi = __builtin_fminf(tf.x, tf.y);
   const float k = 0x1p-20f;
@@ -1771,8 +1778,8 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
 
 // The culled scan of one lane's ray over slot k's chunks (cull_chunk G > 0),
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
-// `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far);
-// otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi).
+// `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far) * id;
+// otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi) * id.
 template <bool FAST, bool FILT, int LPR>
 __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
                                           int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
@@ -1923,8 +1930,9 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     const double mb = u2 * (3.0 * Rr + 2.0 * L) * L * 1e10 + 1e-9;
     // float32 box-test operands (chunk_needed_f): origin, margins, inverse direction d = (cos, sin)
     const float oxf = (float)ox, oyf = (float)oy;
-    const float mbf = (float)mb * (1.0f + 0x1p-20f) +
-                      3.0f * (__builtin_fabsf(oxf) + __builtin_fabsf(oyf) + 1.0f) * 0x1p-24f;
+    const float mbf0 = (float)mb * (1.0f + 0x1p-20f) +
+                       3.0f * (__builtin_fabsf(oxf) + __builtin_fabsf(oyf) + 1.0f) * 0x1p-24f;
+    const float mbf = mbf0 + (__builtin_fabsf(oxf) + __builtin_fabsf(oyf) + mbf0) * 0x1p-22f;  // + c's rounding
     const float mtf = (float)mt * (1.0f + 0x1p-20f) + 1e-6f;
     const rx_f2 nlo = {-(oxf + mbf), -(oyf + mbf)}, nhi = {mbf - oxf, mbf - oyf};
     const float csf = (float)cs, snf = (float)sn;
@@ -1956,11 +1964,11 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
       if (a.box_quadrants && __all(quad == quad0)) {
         const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
         const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
-        cull_scan<true, F, LPR>(a, k, W, nch, seg, c0, quad0 + 1, nn, nf, id2, mtf, ox, oy, v3x, v3y, best, bestf,
-                                tested, scanned, pf);
+        cull_scan<true, F, LPR>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x, v3y,
+                                best, bestf, tested, scanned, pf);
       } else {
-        cull_scan<false, F, LPR>(a, k, W, nch, seg, c0, 0, nlo, nhi, id2, mtf, ox, oy, v3x, v3y, best, bestf,
-                                 tested, scanned, pf);
+        cull_scan<false, F, LPR>(a, k, W, nch, seg, c0, 0, nlo * id2, nhi * id2, id2, mtf, ox, oy, v3x, v3y, best,
+                                 bestf, tested, scanned, pf);
       }
     };
     if (a.seg_filter && a.tr.seg_f)
