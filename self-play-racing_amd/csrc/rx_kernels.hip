@@ -1740,16 +1740,32 @@ __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, i
 // direction component of 0 makes id and c infinite: b * inf + c is +-inf or
 // NaN, and fmin / fmax drop a NaN, leaving the axis unconstrained -- more
 // boxes kept, never fewer.
+// The box decision from the slab interval [lo, hi] (entry clamped at -mtf):
+// x = lo - |lo| k and y = hi + |hi| k bound the exact entry from below and
+// the exit from above (k = 2^-20 covers the <= 6 * 2^-24 relative roundings
+// of lo and hi, and the 2 * 2^-24 of x and y themselves); the ray misses the
+// box if x - y > 1e-6, and no segment in it can lower the lane's minimum if
+// x >= bm = bestf + mtf (the caller's per-leaf sum: its rounding, 2^-24 of a
+// value that x exceeds, is inside x's 2^-20 slack).  9 VALU per box test with
+// the two packed fmas, max3 and min.
+// (x and y as single v_fma_f32 with abs modifiers: left to itself the SLP
+// vectorizer pairs them into a v_pk_fma_f32 plus a v_or and a v_and for the
+// abs the packed form lacks.)
+__device__ __forceinline__ bool slab_keep(float lo, float hi, float bm) {
+  const float k = 0x1p-20f;
+  float x, y;
+  asm("v_fma_f32 %0, -|%1|, %2, %1" : "=v"(x) : "v"(lo), "s"(k));
+  asm("v_fma_f32 %0, |%1|, %2, %1" : "=v"(y) : "v"(hi), "s"(k));
+  return !(x - y > 1e-6f) && x < bm;
+}
 __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 clo, rx_f2 chi, rx_f2 id2,
-                                               float mtf, float bestf) {
+                                               float mtf, float bm) {
   const float4 b = ldu(reinterpret_cast<const float4*>(box));
   const rx_f2 t1 = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, clo);
   const rx_f2 t2 = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, chi);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1.x, t2.x), __builtin_fminf(t1.y, t2.y)), -mtf);
   const float hi = __builtin_fminf(__builtin_fmaxf(t1.x, t2.x), __builtin_fmaxf(t1.y, t2.y));
-  const float k = 0x1p-20f;
-  const bool miss = (lo - hi) > __builtin_fmaf(__builtin_fabsf(lo) + __builtin_fabsf(hi), k, 1e-6f);
-  return !miss && (__builtin_fmaf(-__builtin_fabsf(lo), k, lo) - mtf < bestf);
+  return slab_keep(lo, hi, bm);
 }
 
 template <int A>
@@ -1765,15 +1781,13 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
 // NaN (0 * inf: origin on a slab plane, f32 direction component 0) does this
 // test drop the NaN and keep the box -- more conservative, never less.
 __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx_f2 cn, rx_f2 cf, rx_f2 id2,
-                                               float mtf, float bestf) {
+                                               float mtf, float bm) {
   const float4 b = ldu(reinterpret_cast<const float4*>(box));
   const rx_f2 tn = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, cn);
   const rx_f2 tf = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, cf);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), -mtf);
   const float hi = __builtin_fminf(tf.x, tf.y);
-  const float k = 0x1p-20f;
-  const bool miss = (lo - hi) > __builtin_fmaf(__builtin_fabsf(lo) + __builtin_fabsf(hi), k, 1e-6f);
-  return !miss && (__builtin_fmaf(-__builtin_fabsf(lo), k, lo) - mtf < bestf);
+  return slab_keep(lo, hi, bm);
 }
 
 // The culled scan of one lane's ray over slot k's chunks (cull_chunk G > 0),
@@ -1788,8 +1802,9 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
   const int G = a.cull_chunk;
   const float* __restrict__ fboxes =
       a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uniform(a.tr.chunk_off[k]));
+  float bm = bestf + mtf;  // refreshed with bestf after every leaf scan
   auto needed = [&](const float* box) {
-    return FAST ? chunk_needed_q(box, n1, n2, id2, mtf, bestf) : chunk_needed_f(box, n1, n2, id2, mtf, bestf);
+    return FAST ? chunk_needed_q(box, n1, n2, id2, mtf, bm) : chunk_needed_f(box, n1, n2, id2, mtf, bm);
   };
   const int SG = a.cull_super;
   if (SG <= 0) {
@@ -1804,6 +1819,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
           ++scanned;
           leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
                                    bestf, pf);
+          bm = bestf + mtf;
         }
       }
     }
@@ -1835,6 +1851,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
           ++scanned;
           leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
                                    bestf, pf);
+          bm = bestf + mtf;
         }
       }
     }
