@@ -160,6 +160,25 @@ class PPO:
             pa = self._policy_act = ppo_fused.PolicyAct(self.agent, self._flat, obs.shape[1], obs.shape[2], prec)
         return pa
 
+    def _next_value(self, next_obs):
+        """agent.get_value(next_obs).flatten() -- GAE's bootstrap value
+        (agent/ppo.py:224-226) -- on the fused policy path from the same
+        rx_policy_act kernel that computed the rollout's values (one launch
+        instead of the critic's torch GEMMs and activations), with a zero noise
+        block (no RNG draw) and scratch action / log-prob rows; torch's forward
+        otherwise or with config["fused_next_value"] = False."""
+        fp = self._fused_policy(next_obs.unsqueeze(0)) if self.config.get("fused_next_value", True) else None
+        if fp is None:
+            return self.agent.get_value(next_obs).flatten()
+        n = next_obs.shape[0]
+        buf = self.__dict__.get("_nv_buf")
+        if buf is None or buf[0].shape[0] != n or buf[0].device != next_obs.device:
+            z = lambda *s: torch.zeros(s, dtype=torch.float32, device=next_obs.device)  # noqa: E731
+            buf = self._nv_buf = (z(n, 2), z(n, 2), z(n))  # noise (zeros), action sink, values
+        eps, act, val = buf
+        fp(next_obs, act, None, val, eps=eps)
+        return val
+
     def _step_rollout(self, obs):
         """rx_rollout_steps driver (config["rollout_steps"], default "auto" = on)
         for a single-agent handle on the fused policy path, else None."""
@@ -599,7 +618,7 @@ class PPO:
             obs, actions, logprobs, dones, rewards, values, next_obs, next_done, ep = self.collect_rollout(
                 obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
             with torch.no_grad():
-                next_value = self.agent.get_value(next_obs).flatten()
+                next_value = self._next_value(next_obs)
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
             global_step += c["batch_size"]

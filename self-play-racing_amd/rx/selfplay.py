@@ -249,7 +249,7 @@ class SelfPlayPPO(PPO):
                 obs, actions, logprobs, dones, rewards, values, next_obs, next_done)
             mark("rollout_ms")
             with torch.no_grad():
-                next_value = self.agent.get_value(next_obs).flatten()
+                next_value = self._next_value(next_obs)
             advantages, returns = self.compute_advantages(rewards, dones, values, next_value, next_done)
             mark("gae_ms")
             self.ppo_update(advantages, returns, values, logprobs, actions, obs)
