@@ -256,3 +256,32 @@ def test_multi_evaluator_protocol_runs():
     assert len(res["all_episodes"]) == 200 and "placement" in res["all_episodes"][0]
     assert all(1 <= e["steps"] <= 200 for e in res["all_episodes"])
     ev.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_next_value_matches_critic_and_draws_no_rng(dtype):
+    """GAE's bootstrap value on the fused policy path (PPO._next_value, round 5):
+    the rx_policy_act critic -- the kernel that computed the rollout's values --
+    within float rounding of agent.get_value (bf16: its matrix-core tolerance),
+    with no draw from torch's CUDA generator (the rollout noise stream is the
+    reference's), and torch's forward when config fused_next_value is off."""
+    t, _ = _train_single_style(num_envs=64, num_steps=8, policy_dtype=dtype)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    obs = torch.rand((64, 15), device="cuda", generator=g) * 2 - 1
+    with torch.no_grad():
+        want = t.agent.get_value(obs).flatten()
+    state = torch.cuda.get_rng_state()
+    with torch.no_grad():
+        got = t._next_value(obs).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(state, torch.cuda.get_rng_state())
+    tol = 2e-5 if dtype == "fp32" else 3e-2
+    torch.testing.assert_close(got, want, rtol=tol, atol=tol * float(want.abs().max()))
+    # the same kernel, the same floats, as the rollout's value rows
+    pa = t._fused_policy(obs.unsqueeze(0))
+    act, val = torch.empty((64, 2), device="cuda"), torch.empty(64, device="cuda")
+    pa(obs, act, None, val, eps=torch.zeros((64, 2), device="cuda"))
+    assert torch.equal(val, got)
+    t.config["fused_next_value"] = False
+    with torch.no_grad():
+        assert torch.equal(t._next_value(obs), want)
