@@ -521,9 +521,11 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     at ``envs`` envs with an opponent pool of ``pool_size``: rx.selfplay.SelfPlayPPO's
     own train_iter (pool advance, opponent draw + env rebuild, rollout with the
     frozen opponent's rx_policy_act in the loop, GAE, the 10 x 16 fused update).
-    The snapshot cadence is shortened to every update (the reference's 15) so the
-    pool is full (pool_size snapshots, FIFO) before timing; KL early stop off and
-    device shuffles so every update does the same work; no checkpoint files.
+    The snapshot cadence is shortened to every update while the pool fills
+    (pool_size snapshots, FIFO), then set back to the reference's 15 for the timed
+    updates (a snapshot -- one device deepcopy of the policy, ~1 ms -- every 15th
+    update, as configs[3] runs); KL early stop off and device shuffles so every
+    update does the same work; no checkpoint files.
     Then one more update with a sync between phases gives the split."""
     from rx.configs import self_play_config
     from rx.envs import MultiRacingEnv
@@ -544,6 +546,7 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
         next(it)
     torch.cuda.synchronize()
     pool_before = len(t.opponent_pool)
+    t.snapshot_freq = 15  # self_play_config's cadence (agent/self_play_ppo.py:115-122) from here on
     gc.collect()
     gc.disable()
     t0 = time.perf_counter()
@@ -552,6 +555,13 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
+    # the reference cadence's snapshot, amortised: the timed updates fall between two
+    # snapshot updates, so one snapshot_agent() (timed here, synced) counts 1/15 per update
+    ts = time.perf_counter()
+    t.snapshot_agent()
+    torch.cuda.synchronize()
+    snap_s = time.perf_counter() - ts
+    el += updates * snap_s / t.snapshot_freq
     # phase split of one more update of the same loop (same buffers and graphs), a device
     # sync at every phase boundary (SelfPlayPPO.phase_ms)
     t.phase_ms = {}
@@ -565,8 +575,10 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
            "batch": B, "pool_size": pool_size, "pool_filled_before_timing": pool_before,
            "opponent": "frozen pool snapshot, one rx_policy_act launch per step over all envs",
            "phase_split_one_update": ph,
-           "note": "BASELINE configs[3]; snapshot every update (reference: 15) so the pool is full before timing; "
-                   "KL early stop off, device shuffles, no checkpoint files; timed after the pool-filling updates"}
+           "snapshot_freq_timed": t.snapshot_freq, "snapshot_ms_amortised": round(snap_s * 1e3, 3),
+           "note": "BASELINE configs[3]; snapshot every update until the pool is full, then the reference's every 15 "
+                   "updates; KL early stop off, device shuffles, no checkpoint files; timed after the pool-filling "
+                   "updates"}
     t.envs.close()
     return res
 
