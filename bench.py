@@ -259,6 +259,99 @@ def seed1_pool(n_total):
     return pool, widths
 
 
+def stress_pool(n, seed=2):
+    """SURVEY.md §8(d) stress variant: all-distinct tracks.  environment/track.py:47-56
+    with seed=None draws every track's parameters (P in [10, 14]) and points from the
+    global RNG without the per-track reseed (track.py:5-6) that collapses a seeded pool
+    to 7 slots; widths randint(6, 10) as train.py:79."""
+    from rx.track import gen_tracks
+    np.random.seed(seed)
+    pool = gen_tracks(num_tracks=n, seed=None)
+    widths = [np.random.randint(6, 10) for _ in range(n)]
+    return pool, widths
+
+
+def stress_leg(dev, n, steps, untimed, sched, profile_steps=32, seed=2):
+    """The headline workload (configs[2]: n single-agent envs, uniform random actions
+    resident in HBM, next-step autoreset, one HIP graph of `steps` production steps)
+    on the all-distinct-track pool of stress_pool: every env its own track slot."""
+    from rx.track import TrackSet
+    from rx.vector_env import RacingVectorEnv
+    t0 = time.perf_counter()
+    pool, widths = stress_pool(n, seed)
+    ts = TrackSet.build(pool, widths)
+    build_s = time.perf_counter() - t0
+    env = RacingVectorEnv(pool, widths, n_agents=1, n_sensors=11, device=dev, autoreset="next_step", track_set=ts,
+                          sched=sched)
+    n_slots = len(env.tracks)
+    P = np.bincount([len(c) for c in pool], minlength=15)[10:15]
+    g = torch.Generator(device=dev).manual_seed(4321)
+    bank = max(1, min(steps + untimed + profile_steps, (256 << 20) // (8 * n)))
+    acts = torch.rand((bank, n, 2), device=dev, generator=g) * torch.tensor([2.0, 1.0], device=dev) + \
+        torch.tensor([-1.0, 0.0], device=dev)
+    it = [0]
+
+    def run(K):
+        while K > 0:
+            k = it[0] % bank
+            m = min(K, bank - k)
+            env.steps_device(acts[k:k + m])
+            it[0] += m
+            K -= m
+    env.reset_device()
+    run(untimed)
+    torch.cuda.synchronize(dev)
+    cap = torch.cuda.Stream(device=dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
+        run(steps)
+    graph.replay()  # untimed: upload + K more burn-in steps
+    torch.cuda.synchronize(dev)
+    env.episode_stats()
+    gc.collect()
+    gc.disable()
+    t1 = time.perf_counter()
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t1
+    gc.enable()
+    ep = env.episode_stats()
+    env.profile(1)
+    run(profile_steps)
+    env.profile(0)
+    torch.cuda.synchronize(dev)
+    prof = env.profile_read()
+    waves = wave_slots(env, profile_steps * 2)
+    env.enable_counters(True)
+    run(8)
+    torch.cuda.synchronize(dev)
+    cnt = env.read_counters()
+    env.enable_counters(False)
+    sch = env.schedule()
+    env.close()
+    del graph
+    step2 = prof.get("k_step2", (float("nan"), 0))[0]
+    kin = prof.get("k_kin1", (float("nan"), 0))[0]
+    gbs = STEP2_BYTES_PER_ENV * n / (step2 * 1e-3) / 1e9
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "track_slots": n_slots,
+            "control_points_hist_P10_to_P14": P.tolist(), "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
+            "episodes_ended_in_timed_region": ep[2], "table_build_s": round(build_s, 2),
+            "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
+            "roofline": {"bound": "hbm", "kernel": "k_step2", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "bytes_per_env": STEP2_BYTES_PER_ENV,
+                         "avg_launch_ms": round(step2, 5), "step_kernels_ms": round(step2 + kin, 5)},
+            "wave_slot_utilisation": waves.get("wave_slot_utilisation") if waves else None,
+            "wave_slots": waves,
+            "executed_work": {"ray_box_tests_per_ray_wave": round(cnt["ray_chunk_tests"] / (8 * sch["ray_waves"]), 2),
+                              "ray_leaf_scans_per_env_step": round(cnt["ray_chunks_scanned"] / (8 * n), 3),
+                              "wp_leaf_scans_per_env_step": round(cnt["wp_chunks_scanned"] / (8 * n), 3)},
+            "schedule": sch,
+            "workload": f"configs[2] on the stress pool: np.random.seed({seed}); gen_tracks({n}, seed=None) "
+                        "(track.py:47-56, no per-track reseed), widths randint(6, 10): every env its own track; "
+                        "uniform random actions resident in HBM, next-step autoreset, one HIP graph replay of "
+                        f"{steps} steps after {untimed} + {steps} untimed"}
+
+
 def gae_roofline(n_envs, dev, T=512, reps=20):
     """k_gae (agent/ppo.py:134-154) on a [T, N] rollout: HBM-bound, 20 B per
     (t, env) element (read r, v, d; write A, R; f32) -- SURVEY.md §8(d).  At the
@@ -467,6 +560,12 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
     B = T * n
     c = t.config
     n_mb = c["num_minibatches"]
+    dp_ranks = None
+    if dist:  # what every rank ran: the epoch's launch form (rdist.capture_all_or_none) and its all-reduces
+        me = {"rank": rank, "graph_dp": dict(rdist.GRAPH_DP), "allreduce_per_update": ar["all_reduce"],
+              "allreduce_bytes_per_update": ar["bytes"]}
+        dp_ranks = [None] * world
+        dist.all_gather_object(dp_ranks, me)
     grad_rf = ppo_grad_roofline(t, dev) if world == 1 else None
     t.envs.close()
     return {"value": round(B * updates / el, 1), "unit": "train env-steps/s", "updates": updates,
@@ -478,6 +577,7 @@ def ppo_leg(world, rank, dev, dist, backend, envs_per_gpu, T, updates, policy_dt
             "allreduce_per_update": ar["all_reduce"], "allreduce_bytes_per_update": ar["bytes"],
             "allreduce_per_update_expected": (c["update_epochs"] * (n_mb + 1) + 1) if world > 1 else 0,
             "allreduce_bucket_bytes": 4 * (t._flat.numel + 1) if world > 1 else 0,
+            "dp_ranks": dp_ranks,
             "note": "KL early stop off, device shuffles; timed after one warm-up update"}
 
 
@@ -499,6 +599,7 @@ def rccl_world1_leg(dev, envs, T, updates):
     out = {}
     try:
         for graph in (True, False):
+            rdist.GRAPH_DP.clear()
             rdist.GRAPH_DP.update(captured=None, error=None)
             r = ppo_leg(1, 0, dev, None, "nccl", envs, T, updates, extra=dict(shard_update=True, graph_dp=graph))
             out["graph" if graph else "eager"] = {k: r[k] for k in ("value", "ms_per_update", "allreduce_per_update",
@@ -547,6 +648,13 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     torch.cuda.synchronize()
     pool_before = len(t.opponent_pool)
     t.snapshot_freq = 15  # self_play_config's cadence (agent/self_play_ppo.py:115-122) from here on
+    taken = [0]  # snapshots the timed updates really take (an update index that is a multiple of 15)
+    snap0 = t.snapshot_agent
+
+    def counted():
+        taken[0] += 1
+        return snap0()
+    t.snapshot_agent = counted
     gc.collect()
     gc.disable()
     t0 = time.perf_counter()
@@ -555,13 +663,15 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
-    # the reference cadence's snapshot, amortised: the timed updates fall between two
-    # snapshot updates, so one snapshot_agent() (timed here, synced) counts 1/15 per update
+    t.snapshot_agent = snap0
+    # the reference cadence's snapshot, amortised: updates / 15 snapshots belong to the timed
+    # updates; the ones they took are inside `el` already, the rest (one snapshot_agent(),
+    # timed here, synced) are added -- never counted twice
     ts = time.perf_counter()
     t.snapshot_agent()
     torch.cuda.synchronize()
     snap_s = time.perf_counter() - ts
-    el += updates * snap_s / t.snapshot_freq
+    el += max(0.0, updates / t.snapshot_freq - taken[0]) * snap_s
     # phase split of one more update of the same loop (same buffers and graphs), a device
     # sync at every phase boundary (SelfPlayPPO.phase_ms)
     t.phase_ms = {}
@@ -576,6 +686,7 @@ def selfplay_leg(dev, envs, T, updates, pool_size=5):
            "opponent": "frozen pool snapshot, one rx_policy_act launch per step over all envs",
            "phase_split_one_update": ph,
            "snapshot_freq_timed": t.snapshot_freq, "snapshot_ms_amortised": round(snap_s * 1e3, 3),
+           "snapshots_taken_in_timed_updates": taken[0],
            "note": "BASELINE configs[3]; snapshot every update until the pool is full, then the reference's every 15 "
                    "updates; KL early stop off, device shuffles, no checkpoint files; timed after the pool-filling "
                    "updates"}
@@ -755,6 +866,10 @@ def main():
     ap.add_argument("--rccl-world1", choices=("on", "off"), default="on",
                     help="at N = 1: also time the data-parallel PPO update over a 1-rank RCCL group "
                          "('ppo_train_rccl_world1': captured epoch graphs and eager)")
+    ap.add_argument("--stress", choices=("on", "off"), default="on",
+                    help="also time the headline workload on SURVEY.md §8(d)'s stress pool (all-distinct tracks, "
+                         "gen_tracks(N, seed=None)), reported as 'stress'")
+    ap.add_argument("--stress-envs", type=int, default=None, help="envs of the stress leg (default --envs-per-gpu)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher / process-group check only: every rank joins the group, reports its device and "
                          "runs one all-reduce; no GPU work, no measurement (tests/test_bench_launch_cpu.py)")
@@ -1037,6 +1152,9 @@ def main():
                          "counters, after the timed region")
     for e in envs:
         e.close()
+    stress = None
+    if args.stress == "on" and rank == 0:
+        stress = stress_leg(dev, args.stress_envs or E, args.steps, untimed, sched)
     async_probe = None
     Ga = args.async_probe_groups
     if Ga > 1 and E % Ga == 0 and Ga != G:
@@ -1167,6 +1285,7 @@ def main():
                               "achieved_GBs": round(STEP_BYTES_PER_ENV * n / ((kin_ms + step2_ms) * 1e-3) / 1e9, 3)},
             "dist": dist_info,
             "gae": gae,
+            "stress": stress,
             "async_stream_groups": async_probe,
             "ppo_train": ppo,
             "ppo_train_bf16": ppo_bf16,

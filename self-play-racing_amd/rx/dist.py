@@ -112,8 +112,54 @@ def average_flat(flat):
 # group anyway, so the data-parallel update's launch / collective sequence is priced
 # on one GPU
 FORCE_COLLECTIVES = {"on": False}
-# the last data-parallel epoch graph capture (rx.ppo): captured or the refusal
+# the last data-parallel epoch graph decision (rx.ppo, capture_all_or_none): this rank's
+# capture, the cross-rank agreement, the replay-vs-eager validation, the refusal
 GRAPH_DP = {"captured": None, "error": None}
+
+
+def agree(ok, device=None):
+    """True iff ``ok`` holds on EVERY rank (one MIN all-reduce of a flag; on the
+    device for RCCL, on the host for gloo).  Not counted in COUNTS: it runs once
+    per captured epoch form, outside the update's steady state."""
+    if not active():
+        return bool(ok)
+    dev = device if (td.get_backend() == "nccl" and device is not None) else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    td.all_reduce(t, op=td.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def capture_all_or_none(capture, validate=None, device=None):
+    """The data-parallel epoch's launch form, decided for ALL ranks at once.
+
+    ``capture()`` records the epoch (collectives included) as a HIP graph and
+    returns it, or raises; ``validate(graph)`` (optional) replays it against the
+    eager epoch on the same state and returns whether they agree bit for bit.
+    Every rank then learns, by one MIN all-reduce per stage, whether every rank
+    captured (and validated): if any did not, EVERY rank runs the eager epoch, so
+    no two ranks ever issue the same collectives from different launch forms.
+    -> (graph or None, record); the record also lands in GRAPH_DP."""
+    graph, err = None, None
+    try:
+        graph = capture()
+        ok = graph is not None
+    except Exception as e:  # noqa: BLE001 -- recorded; the ranks agree on eager below
+        ok, err = False, f"{type(e).__name__}: {e}"[:300]
+    rec = {"captured": ok, "error": err, "rank": rank(), "world": world()}
+    ok = agree(ok, device)
+    rec["all_captured"] = ok
+    if ok and validate is not None:
+        try:
+            v = bool(validate(graph))
+        except Exception as e:  # noqa: BLE001
+            v, rec["error"] = False, f"validate: {type(e).__name__}: {e}"[:300]
+        rec["validated"] = v
+        ok = agree(v, device)
+        rec["all_validated"] = ok
+    rec["form"] = "graph" if ok else "eager"
+    GRAPH_DP.clear()
+    GRAPH_DP.update(rec)
+    return (graph if ok else None), rec
 
 
 def capturable():

@@ -268,7 +268,7 @@ class PPO:
         torch.cuda.synchronize(self.device)
         torch.cuda.set_rng_state(rng, self.device)  # the warm-up must not shift the sampling stream
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):  # records only: no env step executes during capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):  # records only: no env step executes during capture
             self._rollout_body(*bufs)
         self._graphs[key] = g
         return g
@@ -432,30 +432,55 @@ class PPO:
                 # world-1 RCCL leg): adv moments -> all-reduce -> finalize, then per optimizer step
                 # shard gradient -> bucket all-reduce -> KL check -> Adam.  config["graph_dp"]
                 # (default: auto = whenever the process group's collectives are capturable, RCCL)
-                # records the whole epoch, collectives included, as ONE HIP graph; a refused
-                # capture falls back to eager launches and is recorded in rdist.GRAPH_DP.
+                # records the whole epoch, collectives included, as ONE HIP graph -- on every
+                # rank or on none (rdist.capture_all_or_none): the capture must succeed on all
+                # ranks, and its first replay must equal the eager epoch bit for bit on all
+                # ranks (parameters, Adam moments, step count, stop flag, KL), else every rank
+                # runs the eager launches.  The decision is recorded in rdist.GRAPH_DP.
                 w = rdist.world()
                 eager = lambda: ent.fused.shard_epoch(ent.stop, ent.kl, w, rdist.all_reduce_sum)  # noqa: E731
                 ent.run = eager
                 want = self.config.get("graph_dp", "auto")
                 if want is True or (want == "auto" and rdist.capturable()):
-                    try:
+                    fl = self._flat
+                    state = [fl.flat_param, fl.exp_avg, fl.exp_avg_sq, fl.step_t, ent.stop, ent.kl]
+
+                    def capture():
                         eager()  # warm-up with the stop flag up: workspaces, communicator; nothing moves
                         torch.cuda.synchronize(dev)
-                        ent.graph = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(ent.graph):
-                            eager()
-                        torch.cuda.synchronize(dev)
-                        ent.run = ent.graph.replay
-                        rdist.GRAPH_DP.update(captured=True, error=None)
-                    except Exception as e:  # noqa: BLE001 -- recorded, eager launches instead
-                        ent.graph, ent.run = None, eager
-                        rdist.GRAPH_DP.update(captured=False, error=f"{type(e).__name__}: {e}"[:300])
-                        torch.cuda.synchronize(dev)
+                        g = torch.cuda.CUDAGraph()
+                        try:
+                            # thread_local: the process group's watchdog thread may query its
+                            # events meanwhile (global mode would invalidate the capture)
+                            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                                eager()
+                        finally:
+                            torch.cuda.synchronize(dev)
+                        return g
+
+                    def validate(g):
+                        keep = [t.clone() for t in state]
+
+                        def run(fn):
+                            ent.stop.zero_()
+                            ent.kl.zero_()
+                            fn()
+                            torch.cuda.synchronize(dev)
+                            out = [t.clone() for t in state]
+                            for t, k in zip(state, keep):
+                                t.copy_(k)
+                            return out
+                        try:
+                            return all(torch.equal(a, b) for a, b in zip(run(eager), run(g.replay)))
+                        finally:
+                            torch.cuda.synchronize(dev)
+
+                    ent.graph, _ = rdist.capture_all_or_none(capture, validate, device=dev)
+                    ent.run = ent.graph.replay if ent.graph is not None else eager
             elif capture:
                 ent.graph = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(dev)
-                with torch.cuda.graph(ent.graph):
+                with torch.cuda.graph(ent.graph, capture_error_mode="thread_local"):
                     ent.fused.epoch(ent.stop, ent.kl)
                 ent.run = ent.graph.replay
             else:
@@ -470,7 +495,7 @@ class PPO:
                     self._graph_minibatch(b, ent.perm[:mb])
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
-            with torch.cuda.graph(ent.graph):
+            with torch.cuda.graph(ent.graph, capture_error_mode="thread_local"):
                 for start in range(0, B, mb):
                     self._graph_minibatch(b, ent.perm[start:start + mb])
             ent.run = ent.graph.replay
@@ -536,7 +561,7 @@ class PPO:
             if ent.graph is not None:
                 g = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(ent.perm.device)
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     ent.fused.epoch(ent.stop, ent.kl, stats=False)
                 run = g.replay
                 ent.graph_nostats = g

@@ -165,6 +165,15 @@ class TrackGeometry:
         return (wp[0, 0], wp[0, 1], np.arctan2(wp[1, 1] - wp[0, 1], wp[1, 0] - wp[0, 0]))
 
 
+def _geoms_worker(args):
+    """Worker of TrackSet.build (a spawned process: numpy / scipy only): the
+    packed table rows of its tracks (TrackSet.arrays layout), not the objects --
+    pickling every TrackGeometry back cost more than the splines."""
+    items, factor = args
+    g = [TrackGeometry(cp, w, factor) for cp, w in items]
+    return TrackSet._pack(g)
+
+
 class TrackSet:
     """Deduplicated (control points, width) slots packed as the device table.
 
@@ -176,6 +185,46 @@ class TrackSet:
         self.geoms = []
         self._index = {}
         self._packed = None
+
+    @classmethod
+    def build(cls, control_points, widths, workers=None, factor=30):
+        """The slots of (control_points[i], widths[i]) for every i, in first-sight
+        order (as ``slot`` adds them), with the splines of many distinct slots
+        computed in ``workers`` spawned processes (each runs TrackGeometry, so the
+        geometry is bit-identical to the serial build).  For pools of thousands of
+        distinct tracks -- ``gen_tracks(n, seed=None)``, SURVEY.md §8(d)'s stress
+        variant -- where the serial spline (~1 ms per track) dominates."""
+        ts = cls(factor)
+        todo = []
+        for cp, w in zip(control_points, widths):
+            cp = DEFAULT_CONTROL_POINTS if cp is None else cp
+            w = DEFAULT_WIDTH if w is None else w
+            key = cls._key(cp, w)
+            if key not in ts._index:
+                ts._index[key] = len(todo)
+                todo.append((cp, w))
+        if workers is None:
+            import os
+            workers = min(16, len(os.sched_getaffinity(0)))
+        if workers <= 1 or len(todo) < 256:
+            ts.geoms = [TrackGeometry(cp, w, factor) for cp, w in todo]
+            return ts
+        import multiprocessing as mp
+        per = (len(todo) + 4 * workers - 1) // (4 * workers)
+        parts = [(todo[i:i + per], factor) for i in range(0, len(todo), per)]
+        with mp.get_context("spawn").Pool(workers) as pool:
+            packed = list(pool.imap(_geoms_worker, parts))
+        W = np.concatenate([np.diff(p["wp_off"]) for p in packed])
+        a = dict(wp_off=np.concatenate([[0], np.cumsum(W)]).astype(np.int32),
+                 **{k: np.ascontiguousarray(np.concatenate([p[k] for p in packed]))
+                    for k in ("wp", "nrm", "seg", "meta")})
+        off = a["wp_off"]
+        for k, (cp, w) in enumerate(todo):  # views into the packed table (TrackGeometry.from_arrays)
+            s, e = off[k], off[k + 1]
+            ts.geoms.append(TrackGeometry.from_arrays(cp, w, a["wp"][s:e], a["nrm"][s:e], a["seg"][2 * s:2 * e],
+                                                      a["meta"][k, 4]))
+        ts._packed = a
+        return ts
 
     @staticmethod
     def _key(cp, width):
@@ -197,22 +246,25 @@ class TrackSet:
     def __len__(self):
         return len(self.geoms)
 
+    @staticmethod
+    def _pack(g):
+        W = [len(t.waypoints) for t in g]
+        wp_off = np.concatenate([[0], np.cumsum(W)]).astype(np.int32)
+        wp = np.ascontiguousarray(np.concatenate([t.waypoints for t in g]), dtype=np.float64)
+        nrm = np.ascontiguousarray(np.concatenate([t.normals for t in g]), dtype=np.float64)
+        seg = np.ascontiguousarray(np.concatenate(
+            [np.concatenate([t.segment_cache["starts"], t.segment_cache["v2"]], axis=1) for t in g]),
+            dtype=np.float64)
+        meta = np.zeros((len(g), 8), dtype=np.float64)
+        for k, t in enumerate(g):
+            sx, sy, sa = t.get_start_pos()
+            meta[k] = (sx, sy, sa, float(t.track_width), float(t.max_track_distance),
+                       t.normals[0, 0], t.normals[0, 1], 0.0)
+        return dict(wp_off=wp_off, wp=wp, nrm=nrm, seg=seg, meta=meta)
+
     def arrays(self):
         if self._packed is None:
-            g = self.geoms
-            W = [len(t.waypoints) for t in g]
-            wp_off = np.concatenate([[0], np.cumsum(W)]).astype(np.int32)
-            wp = np.ascontiguousarray(np.concatenate([t.waypoints for t in g]), dtype=np.float64)
-            nrm = np.ascontiguousarray(np.concatenate([t.normals for t in g]), dtype=np.float64)
-            seg = np.ascontiguousarray(np.concatenate(
-                [np.concatenate([t.segment_cache["starts"], t.segment_cache["v2"]], axis=1) for t in g]),
-                dtype=np.float64)
-            meta = np.zeros((len(g), 8), dtype=np.float64)
-            for k, t in enumerate(g):
-                sx, sy, sa = t.get_start_pos()
-                meta[k] = (sx, sy, sa, float(t.track_width), float(t.max_track_distance),
-                           t.normals[0, 0], t.normals[0, 1], 0.0)
-            self._packed = dict(wp_off=wp_off, wp=wp, nrm=nrm, seg=seg, meta=meta)
+            self._packed = self._pack(self.geoms)
         return self._packed
 
     # ------------------------------------------------------------ on-disk table

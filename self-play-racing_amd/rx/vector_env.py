@@ -60,26 +60,24 @@ class _NumpyStartDraws:
 
     def __init__(self, env):
         self.env = env
-        self.cursor = torch.zeros(2, dtype=torch.int64, device=env.device)
+        # [used, over, stray]: rx_set_start_draws counts into the first two; a reset launched
+        # between sessions (a direct rx_step / rx_reset) takes no draw and lands in [1], which
+        # the next begin() stashes in [2] without a host sync -- end() reports it
+        self.cursor = torch.zeros(3, dtype=torch.int64, device=env.device)
         self.buf = None
         self.active = False
         self.state0 = None
 
     def begin(self, cap):
         cap = max(int(cap), 1)
-        if self.buf is not None:  # between sessions the handle holds 0 draws: a reset there overruns
-            torch.cuda.synchronize(self.env.device)
-            stray = int(self.cursor[1].item())
-            if stray:
-                raise _lib.RxError(f"start draws: {stray} resets ran outside a start-draw session (their start "
-                                   "slots did not come from np.random)")
         self.state0 = np.random.get_state()
         u = np.random.randint(0, 2**32, size=cap, dtype=np.uint32)
         np.random.set_state(self.state0)
         if self.buf is None or self.buf.numel() < cap:
             self.buf = torch.empty(cap, dtype=torch.int32, device=self.env.device)
         self.buf[:cap].copy_(torch.from_numpy(u.view(np.int32)))
-        self.cursor.zero_()
+        self.cursor[2:].copy_(self.cursor[1:2])  # resets since the last session (enqueued, no sync)
+        self.cursor[:2].zero_()
         _lib.check(self.env.L.rx_set_start_draws(self.env._h, _lib.ptr(self.buf), cap, _lib.ptr(self.cursor)),
                    "rx_set_start_draws")
         self.active = True
@@ -87,19 +85,22 @@ class _NumpyStartDraws:
     def end(self):
         self.active = False
         torch.cuda.synchronize(self.env.device)
-        used, over = (int(x) for x in self.cursor.cpu().numpy())
+        used, over, stray = (int(x) for x in self.cursor.cpu().numpy())
         np.random.set_state(self.state0)
         if used:
             np.random.randint(0, 2**32, size=used, dtype=np.uint32)  # the reference's draws, consumed
         # until the next session the handle holds NO draws with a zeroed cursor: a reset
-        # launched outside a session (a direct rx_step / rx_reset) takes nothing from the
-        # buffer, is counted in cursor[1], and the next begin() raises instead of handing
-        # out already-consumed outputs again
+        # launched outside a session takes nothing from the buffer and is counted in
+        # cursor[1]; the next session reports it.  Every count is
+        # cleared here, so one report does not poison later sessions.
         self.cursor.zero_()
         _lib.check(self.env.L.rx_set_start_draws(self.env._h, _lib.ptr(self.buf), 0, _lib.ptr(self.cursor)),
                    "rx_set_start_draws")
         if over:
             raise _lib.RxError(f"start draws: {over} resets beyond the session's {self.buf.numel()} draws")
+        if stray:
+            raise _lib.RxError(f"start draws: {stray} resets ran outside a start-draw session (their start "
+                               "slots did not come from np.random)")
 
 
 def default_sort_interval(n_envs, n_agents):

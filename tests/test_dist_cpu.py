@@ -162,3 +162,66 @@ def test_two_rank_sampling_seeds_differ():
         assert pr.exitcode == 0
     assert res[0][0] == 1 and res[1][0] == 2
     assert res[0][1] == (0, 4) and res[1][1] == (4, 4)
+
+
+def _capture_worker(rank, world, port, q, fail_rank, bad_replay_rank):
+    """rdist.capture_all_or_none with a capture that fails (or a replay that
+    disagrees with eager) on ONE rank: every rank must end on the eager form, and
+    the eager epochs -- which all-reduce -- must leave the ranks bit-identical."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as td
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rx.dist as rd
+        w = torch.full((8,), float(rank + 1), dtype=torch.float64)
+
+        def eager_epoch():  # stands in for the shard epoch: local work + a bucket all-reduce
+            g = torch.sin(w * 1.7) / world
+            td.all_reduce(g)
+            w.sub_(0.1 * g)
+
+        def capture():
+            if rank == fail_rank:
+                raise RuntimeError("capture refused on this rank (test)")
+            return "graph"
+
+        def validate(graph):
+            return rank != bad_replay_rank
+
+        graph, rec = rd.capture_all_or_none(capture, validate)
+        run = eager_epoch if graph is None else (lambda: None)
+        w.fill_(1.0)  # the shared state every rank starts the update from
+        for _ in range(3):
+            run()
+        q.put((rank, rec, w.numpy().copy()))
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,bad_replay_rank", [(1, -1), (-1, 0), (-1, -1)])
+def test_two_rank_graph_capture_is_all_or_none(fail_rank, bad_replay_rank):
+    """the data-parallel epoch graph is used on every rank or on none.
+    A capture refused on rank 1, or a replay that disagrees with eager on rank 0,
+    puts BOTH ranks on the eager launches (and the ranks stay bit-identical); with
+    every rank capturing and validating, both take the graph."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_capture_worker, args=(r, 2, port, q, fail_rank, bad_replay_rank))
+             for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = {r: (rec, w) for r, rec, w in (q.get(timeout=120) for _ in procs)}
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    forms = {res[r][0]["form"] for r in (0, 1)}
+    assert len(forms) == 1, res
+    want = "graph" if fail_rank < 0 and bad_replay_rank < 0 else "eager"
+    assert forms == {want}, res
+    if fail_rank >= 0:
+        assert res[fail_rank][0]["captured"] is False and res[1 - fail_rank][0]["captured"] is True
+        assert all(res[r][0]["all_captured"] is False for r in (0, 1))
+    assert np.array_equal(res[0][1], res[1][1])
+    if want == "eager":
+        assert not np.array_equal(res[0][1], np.ones(8))  # the eager epochs ran

@@ -215,7 +215,8 @@ def test_rccl_world1_shard_update_equals_fused():
     assert np.array_equal(pa, pb) and np.array_equal(ma, mb_)
     # the data-parallel epoch captured as ONE HIP graph, RCCL all-reduces
     # included (graph_dp), replayed == eager == the single-rank fused update
-    assert graph_dp["captured"] is True, graph_dp
+    # (rdist.capture_all_or_none: captured on every rank, first replay == eager epoch bit for bit)
+    assert graph_dp["captured"] is True and graph_dp["form"] == "graph" and graph_dp["all_validated"], graph_dp
     assert np.array_equal(pa, pc) and np.array_equal(ma, mc)
     print(f"\nRCCL {ver}: {calls['n']} all-reduces, {calls['bytes']} B, shard update (eager and one graph per "
           "epoch) == fused bit for bit")

@@ -259,3 +259,29 @@ def test_spatial_sort_orders_envs_by_track_bin(n_agents, N):
     assert np.all(np.diff(key[perm]) >= 0), "envs not ascending by sort bin"
     assert len(np.unique(key)) > 30  # the cars have started to spread over the tracks
     v.close()
+
+
+def _stress_pool(n, seed):
+    """SURVEY.md §8(d) stress variant: np.random.seed(s); gen_tracks(n, seed=None) --
+    every env its own track (no per-track reseed, environment/track.py:47-56)."""
+    from rx.track import gen_tracks
+    np.random.seed(seed)
+    pool = gen_tracks(num_tracks=n, seed=None)
+    widths = [np.random.randint(6, 10) for _ in range(n)]
+    return pool, widths
+
+
+def test_stress_distinct_tracks_subset_bit_exact_vs_oracle(oracle_dev):
+    """The stress pool at 16,384 envs = 16,384 distinct track slots (P in [10, 14]):
+    2,048 random envs == the oracle bit for bit at every one of 200 steps, on the
+    schedule rx_assign picks for a pool of distinct tracks."""
+    from rx.track import TrackSet
+    from rx.vector_env import RacingVectorEnv
+    N = 16384
+    pool, widths = _stress_pool(N, 5)
+    v = RacingVectorEnv(pool, widths, device="cuda", autoreset="next_step", track_set=TrackSet.build(pool, widths))
+    assert len(v.tracks) == N
+    idx = np.sort(np.random.default_rng(23).choice(N, 2048, replace=False))
+    ended = _single_run(v, idx, oracle_dev, 200, seed=29)
+    assert ended > 200
+    v.close()
