@@ -96,7 +96,7 @@ def _flop(c, keys):
     return 64.0 * (add + mul + trans + 2.0 * fma)
 
 
-def compute_roofline(pmc, launch_ms, n, waves=None, win=None):
+def compute_roofline(pmc, launch_ms, n, waves=None):
     """The §8(d) compute roofline of the VALU-bound env step (SURVEY.md:456-457):
     EXECUTED FP64 flops per launch from the committed steady-state PMC counts
     (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64, same launch size) over the LIVE
@@ -145,34 +145,6 @@ def compute_roofline(pmc, launch_ms, n, waves=None, win=None):
         res["fp64_flop_per_env_step_executed"] = round(per_env, 1)
         res["executed_over_unculled"] = round(per_env / ALGO_UNCULLED_FLOP_PER_ENV_STEP, 4)
     res["valu_busy_frac"] = s2.get("valu_busy_frac")
-    c = pmc.get("k_window", {})
-    spl = c.get("steps_per_launch")
-    if win is not None and spl:
-        # k_window (multi-step form, the production kernel when win is given): PMC counts of
-        # launches of spl steps, scaled to the live launches' steps_per_launch
-        t = win["avg_launch_ms"]
-        scale = win["steps_per_launch"] / spl
-        d = {"launch_ms_live": round(t, 5), "steps_per_launch_live": win["steps_per_launch"],
-             "steps_per_launch_pmc": spl}
-        act, gui = c.get("SQ_ACTIVE_INST_VALU"), c.get("GRBM_GUI_ACTIVE")
-        if act is not None and gui is not None:
-            d.update(valu_busy_frac=round(4.0 * act / (1024.0 * gui / 8.0), 4),
-                     valu_insts_per_env_step=round(c.get("SQ_INSTS_VALU", 0) / (spl * n), 2))
-        f64, f32 = _flop(c, F64_KEYS), _flop(c, F32_KEYS)
-        if f64 is not None:
-            d["fp64_flop_per_env_step"] = round(f64 / (spl * n), 1)
-            tf = f64 * scale / (t * 1e-3) / 1e12
-            d["fp64_achieved_tflops"] = round(tf, 3)
-            d["fp64_frac"] = round(tf / FP64_VECTOR_PEAK_TFLOPS, 4)
-            res.update(kernel="k_window", achieved=d["fp64_achieved_tflops"], frac=d["fp64_frac"],
-                       fp64_flop_per_env_step_executed=d["fp64_flop_per_env_step"],
-                       executed_over_unculled=round(d["fp64_flop_per_env_step"] / ALGO_UNCULLED_FLOP_PER_ENV_STEP, 4))
-        if f32 is not None:
-            tf = f32 * scale / (t * 1e-3) / 1e12
-            d["fp32_achieved_tflops"] = round(tf, 3)
-            d["fp32_frac"] = round(tf / FP32_VECTOR_PEAK_TFLOPS, 4)
-        res["k_window"] = d
-        res["valu_busy_frac"] = d.get("valu_busy_frac", res["valu_busy_frac"])
     if waves:
         res["wave_slots"] = waves
         res["wave_slot_utilisation"] = waves.get("wave_slot_utilisation")
@@ -209,32 +181,6 @@ def wave_slots(env, n_launches, max_step2=16):
             "ray_end_us_by_class_max": {j: round(float(np.mean([g["ray_end_us_by_class_max"][j] for g in got])), 2)
                                         for j in classes},
             "slots": 8192, "source": "live: rx_profile per-wave stamps of the instrumented production launches"}
-
-
-def window_profile(env, n_launches):
-    """Per-workgroup view of the recorded k_window launches (rx_profile stamps: each
-    workgroup = one 64-env block for all the window's steps): the launch span, the
-    workgroups' start spread (every one resident at once: a workgroup that waited for
-    a slot would start a whole window late), and the drain -- last end minus the
-    median end."""
-    got = []
-    for k in range(n_launches):
-        try:
-            st, en, kind, _ = env.profile_waves(k)
-        except Exception:  # noqa: BLE001 -- past the record
-            break
-        if kind != "k_window":
-            continue
-        live = np.isfinite(st) & np.isfinite(en)
-        st, en = st[live], en[live]
-        if not len(st):
-            continue
-        got.append({"span_us": float(en.max() - st.min()), "start_spread_us": float(st.max() - st.min()),
-                    "wg_mean_us": float(np.mean(en - st)), "drain_us": float(en.max() - np.median(en)),
-                    "workgroups": int(len(st))})
-    if not got:
-        return None
-    return {k: round(float(np.mean([g[k] for g in got])), 2) for k in got[0]} | {"launches": len(got)}
 
 
 _MARKS = os.environ.get("RX_BENCH_MARKS") == "1"
@@ -860,9 +806,9 @@ def main():
                          "graph of the other K - H (the GPU starts on the head while the host submits the rest); "
                          "0 = one graph (default: H = 1 / 2 measured no better, profiles/r05/ab_graph_head.jsonl)")
     ap.add_argument("--multi-step", choices=("on", "off"), default="on",
-                    help="on (default): the production steps are rx_steps calls over the HBM-resident action bank -- "
-                         "with the window schedule the steps between two spatial re-sorts run as ONE k_window launch "
-                         "(a workgroup per 64-env block for all of them); off: one rx_step (k_kin1 + k_step2) per step")
+                    help="on (default): the production steps are rx_steps calls over the HBM-resident action bank "
+                         "(k_kin1 + k_step2 per step, the re-sort every sort_interval steps); off: one rx_step call "
+                         "per step")
     ap.add_argument("--rccl-world1", choices=("on", "off"), default="on",
                     help="at N = 1: also time the data-parallel PPO update over a 1-rank RCCL group "
                          "('ppo_train_rccl_world1': captured epoch graphs and eager)")
@@ -1109,24 +1055,6 @@ def main():
         prof = env0.profile_read()
         mark("instrumented_end")
         waves = wave_slots(env0, args.profile_steps * 3) if G == 1 else None
-    # ---- instrumented windows (multi-step form): whole re-sort windows only -- the steps are
-    # first aligned so the next one opens a window -- each k_window launch stamped per workgroup
-    win = None
-    if multi and args.profile_steps > 0:
-        iv = env0.sort_interval
-        if iv > 0:
-            run_steps((1 - env0.schedule()["dyn_calls"]) % iv)
-        n_win_steps = max(iv, args.profile_steps // iv * iv) if iv > 0 else args.profile_steps
-        mark("windows_begin")
-        env0.profile(1)
-        run_steps(n_win_steps)
-        env0.profile(0)
-        wp = env0.profile_read().get("k_window")
-        mark("windows_end")
-        if wp is not None:
-            win = {"steps": n_win_steps, "launches": wp[1], "steps_per_launch": n_win_steps / wp[1],
-                   "avg_launch_ms": wp[0], "ms_per_step": wp[0] * wp[1] / n_win_steps,
-                   "workgroups": window_profile(env0, wp[1])}
     # ---- executed-work counters (after timing): per ray wave its box tests and leaf scans,
     # per REWARD wave its waypoint-box tests and leaf scans (rx_io.counters, one atomic per wave)
     work = None
@@ -1198,31 +1126,14 @@ def main():
         pmc = load_pmc(n)
         step2_gbs = STEP2_BYTES_PER_ENV * n / (step2_ms * 1e-3) / 1e9
         ray_gbs = RAYS_BYTES_PER_ENV * n / (ray_ms * 1e-3) / 1e9
-        if win is not None:  # the production kernel is k_window: a launch = steps_per_launch whole steps
-            win_bytes = STEP_BYTES_PER_ENV * n * win["steps_per_launch"]
-            win_gbs = win_bytes / (win["avg_launch_ms"] * 1e-3) / 1e9
-            wpmc = pmc.get("k_window", {})
-            w_spl = wpmc.get("steps_per_launch")
-            roof = {"bound": "hbm", "kernel": "k_window", "achieved": round(win_gbs, 3), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": win_gbs / HBM_PEAK_GBS,
-                    "traffic": (wpmc["hbm_bytes_per_launch"] * win["steps_per_launch"] / w_spl
-                                if "hbm_bytes_per_launch" in wpmc and w_spl else None),
-                    "traffic_source": pmc.get("source") if "hbm_bytes_per_launch" in wpmc else None,
-                    "bytes_per_env_step": STEP_BYTES_PER_ENV, "envs_per_launch": n,
-                    "steps_per_launch": win["steps_per_launch"], "algorithmic_bytes_per_launch": win_bytes,
-                    "avg_launch_ms": round(win["avg_launch_ms"], 5),
-                    "note": "a k_window launch runs steps_per_launch whole env steps (KIN, REWARD, raycast) of "
-                            "every env: algorithmic bytes = SURVEY.md §8(d)'s 218 B per env-step x envs x steps; "
-                            "VALU-bound, see compute_roofline"}
-        else:
-            roof = {"bound": "hbm", "kernel": "k_step2", "achieved": round(step2_gbs, 3),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step2_gbs / HBM_PEAK_GBS,
-                    "traffic": pmc.get("k_step2", {}).get("hbm_bytes_per_launch"),
-                    "traffic_source": pmc.get("source"),
-                    "bytes_per_env": STEP2_BYTES_PER_ENV, "envs_per_launch": n,
-                    "avg_launch_ms": round(step2_ms, 5),
-                    "note": "the step is VALU-bound (branchy f64 ray/segment math): the HBM fraction is "
-                            "expected to be tiny; see compute_roofline"}
+        roof = {"bound": "hbm", "kernel": "k_step2", "achieved": round(step2_gbs, 3),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step2_gbs / HBM_PEAK_GBS,
+                "traffic": pmc.get("k_step2", {}).get("hbm_bytes_per_launch"),
+                "traffic_source": pmc.get("source"),
+                "bytes_per_env": STEP2_BYTES_PER_ENV, "envs_per_launch": n,
+                "avg_launch_ms": round(step2_ms, 5),
+                "note": "the step is VALU-bound (branchy f64 ray/segment math): the HBM fraction is "
+                        "expected to be tiny; see compute_roofline"}
         out = {
             "metric": "env-steps/sec (whole node) @65536 envs",
             "value": round(value, 1),
@@ -1249,11 +1160,8 @@ def main():
                              "episodes_ended_before_timing": ep_untimed[2],
                              "episodes_ended_in_timed_region": ep[2],
                              "timed_region": ("production steps only: rx_steps over the HBM-resident action bank "
-                                              f"(rx_config.window {schedule.get('window', 0)}: "
-                                              + ("k_window / k_flow launches between re-sorts"
-                                                 if schedule.get("window", 0) else "the per-step launches k_kin1 + "
-                                                 "k_step2, the re-sort every sort_interval steps") +
-                                              "), no instrumentation"
+                                              "(the per-step launches k_kin1 + k_step2, the re-sort every "
+                                              "sort_interval steps), no instrumentation"
                                               if multi else
                                               "production steps only: one rx_step (k_kin1 + k_step2) per step, "
                                               "no instrumentation"),
@@ -1264,12 +1172,10 @@ def main():
                                          "once untimed)")
                                         if step_graph is not None else
                                         ("one rx_steps call" if multi else "one rx_step call per step from Python"))},
-            # dominant kernel of the production step: k_window (multi-step form) or k_step2 (REWARD half
-            # beside the raycast, per-step form)
+            # dominant kernel of the production step: k_step2 (REWARD half beside the raycast)
             "roofline": roof,
-            "window": win,
             "compute_roofline": compute_roofline(pmc, {"k_step2": step2_ms, "k_kin1": kin_ms, "k_rays": ray_ms}, n,
-                                                 waves, win),
+                                                 waves),
             "executed_work": work,
             "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
             "kernel_launches": {k: v[1] for k, v in prof.items()},

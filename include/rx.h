@@ -39,7 +39,7 @@ extern "C" {
 #define RX_ENOMEM (-3)   /* device allocation failed */
 #define RX_ESTATE (-4)   /* call order: tracks/assignment/state not set */
 
-#define RX_ABI_VERSION 22
+#define RX_ABI_VERSION 23
 #define RX_EP_SHARDS 64  /* episode-statistics accumulator rows (rx_io.ep_stats) */
 
 /* state flag bits (rx_state.flags, per agent) */
@@ -119,20 +119,16 @@ typedef struct {
      launches (and after every spatial re-sort); in between the ray waves keep the previous
      order.  0 auto (2 up to 16,384 (env, car) pairs, 1 above), 1 .. 16 */
   int32_t task_sort;
-  /* ABI v21: rx_steps runs consecutive single-agent split steps as multi-step windows (k_window: a
-     workgroup per 64-env block for all steps between two spatial re-sorts) where the schedule allows
-     (one lane per ray and per env in REWARD, ray_order 2, task_sort 1); elsewhere, or with -1, it
-     enqueues the per-step launches of rx_step.  0 auto (off: measured slower at 65,536 envs, the
-     slowest blocks' 8-step chains end the window -- DESIGN.md §3), 1 on, 2 k_flow (the window's steps
-     as a task graph over per-XCD ready queues: any wave runs any ready (step, block) task), -1 off.
-     Scheduling only. */
-  int32_t window;
-  /* ABI v22: the ray-task ranking of the launches that sort the tasks (task_sort): 1 = a 4-wave workgroup
-     per 64-env block (k_kin1p: kinematics on one wave, the ranking on all four), 0 auto / -1 = the block's
-     one kinematics wave ranks its 704 tasks (k_kin1; auto is off: k_kin1p is 1.0 us faster but k_step2's
-     ray waves 1.6 us slower on its task order, profiles/r05/ab_kin_sort.jsonl).  The same counting sort
-     either way (rx_ray_tasks; tests/test_kin_sort_gpu.py).  Scheduling only. */
-  int32_t kin_sort;
+  /* ABI v23: lane-varying track slots.  Normally every wavefront holds envs of ONE track slot, so its
+     track-table reads are wave-uniform scalar loads; a pool of many distinct tracks (SURVEY.md §8(d)'s
+     stress variant: gen_tracks(N, seed=None), one slot per env) then leaves a wave with one env.  With
+     lane_tracks on, the single-agent kernels take waves of 64 consecutive envs of ANY slots and every lane
+     reads its own slot's tables with vector loads (culling decisions per lane).  0 auto: on when grouping
+     by slot would fill the dynamics waves less than half on average (more than 2 x ceil(N / 64) waves);
+     1 on; -1 off.  Single-agent envs on the split step at one lane per env and per ray only (wide kernels,
+     two-car envs: off).  Scheduling only: bit-identical results. */
+  int32_t lane_tracks;
+  int32_t reserved0;       /* ABI v23: must be 0 (was kin_sort, a dropped A/B schedule) */
 } rx_config;
 
 /* Per-env / per-agent SoA state, caller-owned device memory.  [N*A] arrays are
@@ -205,10 +201,10 @@ int rx_env_order(rx_env* h, int32_t* perm_out, int32_t* sort_bins, int32_t* sort
  * (0/1), k_dyn1 lanes per env, lanes per ray task, REWARD lanes per env,
  * closest-waypoint window half-width, segment pre-filter (0/1), quadrant box
  * tables (0/1), dynamics waves, ray waves, ray-wave dispatch order, tail
- * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval, rx_steps
- * multi-step windows (0/1, ABI v21), dynamics launches so far (the re-sort cadence counter: the
- * launch with count % sort_interval == 0 writes the re-sort keys; ABI v21), workgroup-wide
- * ray-task ranking (0/1, ABI v22).  Host only, no device call. */
+ * classes, tail lanes per ray, first tail wave (-1 = none), ray-task sort interval, lane-varying
+ * track slots (0/1, ABI v23), dynamics launches so far (the re-sort cadence counter: the launch
+ * with count % sort_interval == 0 writes the re-sort keys; ABI v21), 0 (reserved).  Host only,
+ * no device call. */
 #define RX_SCHEDULE_W 18
 int rx_schedule(const rx_env* h, int32_t* out);
 
@@ -284,18 +280,12 @@ int rx_step(rx_env* h, const rx_io* io, void* stream);
  * strides = NULL: all 0).  ep_stats and counters accumulate.  The actions of all
  * n_steps steps must be in device memory when the call is made: open-loop
  * action sequences (the env-throughput benchmark: a bank of random actions) --
- * a policy-in-the-loop rollout is rx_rollout_steps.  With rx_config.window on
- * (default) the steps between two spatial re-sorts of a single-agent split-step
- * handle run as ONE k_window launch: no kernel boundary per step
- * and no chip-wide drain per step.  Replaces n_steps iterations of
- * SyncVectorEnv.step (agent/ppo.py:112) with precomputed actions. */
+ * a policy-in-the-loop rollout is rx_rollout_steps.  Replaces n_steps iterations
+ * of SyncVectorEnv.step (agent/ppo.py:112) with precomputed actions. */
 typedef struct {
   int64_t actions, obs, reward, reward64, terminated, truncated, done_f32, info, ep_done;
 } rx_io_strides;
 int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* strides, void* stream);
-/* Diagnostics (ABI v21): nonzero when a k_flow wave gave up waiting for a task (a bounded spin
- * timed out: the launch's results are incomplete).  Synchronises the device. */
-int rx_flow_errors(rx_env* h, int32_t* out);
 
 /* rx_step split into its two kernels, for per-kernel timing with stream
  * events: phases bit 0 = dynamics/reward/done/autoreset (k_dyn), bit 1 =
@@ -321,8 +311,7 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream);
 #define RX_KERNEL_KIN 2    /* k_kin1: first kernel of the split step */
 #define RX_KERNEL_STEP2 3  /* k_step2: REWARD half + raycast in one launch (split step) */
 #define RX_KERNEL_REWARD 4 /* k_step2 with the REWARD half only (rx_step_phases dynamics) */
-#define RX_KERNEL_WINDOW 5 /* k_window: a multi-step window of rx_steps (its duration covers all its steps) */
-#define RX_KERNEL_KINDS 6
+#define RX_KERNEL_KINDS 5
 int rx_profile(rx_env* h, int32_t enable);
 int rx_profile_read(rx_env* h, double* mean_ms, int32_t* count);
 /* Diagnostics (ABI v18): the raw per-wave stamps of recorded launch `launch`
@@ -445,14 +434,8 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
  * *stop), then the clip + Adam update of params / exp_avg / exp_avg_sq
  * (rx_adam_clip_step's arithmetic; skipped when *stop is set).  params must be
  * b->params; cfg the rx_adam_clip_step layout of the same P parameters;
- * adam_ws holds rx_ppo_update_workspace_floats(obs_dim, cfg) floats and must be
- * ZERO-FILLED once when allocated (ABI v22): its last RX_PPO_TAIL_CTL words are
- * the control block of the single-launch reduce + clip + Adam variant (a build
- * option, RX_PPO_FUSED_TAIL=1, measured slower: DESIGN.md §5), whose word
- * RX_PPO_TAIL_ERR counts workgroups that gave up waiting for the published clip
- * coefficient (always 0 in the default build). */
-#define RX_PPO_TAIL_CTL 8
-#define RX_PPO_TAIL_ERR 6
+ * adam_ws holds rx_ppo_update_workspace_floats(obs_dim, cfg) floats (ABI v23: the
+ * per-tensor norm partials and Adam's two step scalars; no control block). */
 size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg);
 int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
                             float* ws_f32, double* ws_f64, float* grad, float* exp_avg, float* exp_avg_sq, float* step,

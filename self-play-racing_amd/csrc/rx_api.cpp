@@ -107,13 +107,7 @@ struct rx_env {
   int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
   int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
   int32_t task_sort = 1;                   // ray-task direction sort every task_sort dynamics launches
-  int32_t window = 0;                      // rx_steps: 0 per-step launches, 1 k_window, 2 k_flow (rx_assign's choice)
-  int32_t window_cap = 0;                  // k_window workgroups resident at once (occupancy x CUs)
-  DevBuf<rx_kargs> win_args;               // k_window / k_flow per-step argument blocks [RX_WIN_MAX_STEPS]
-  int32_t flow_grid = 0;                   // k_flow one-wave workgroups (resident capacity)
-  DevBuf<int32_t> flow_q, flow_ctl, flow_cnt;  // k_flow queues [8][cap], control words, block arrival counters
   DevBuf<uint8_t> policy_frag;  // the bf16 rollout's operand fragments of both trunks (k_policy_frag, rx_rollout_steps)
-  int32_t flow_cap = 0;
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
   std::vector<double> rel_angles_h;
@@ -331,10 +325,10 @@ int rx_create(const rx_config* cfg, rx_env** out) {
     return fail(RX_EINVAL, "ray_tail must be 0 (auto), -1 (none) or 1 .. 16 (got %d)", cfg->ray_tail);
   if (cfg->ray_tail_lpr != 0 && cfg->ray_tail_lpr != 2 && cfg->ray_tail_lpr != 4)
     return fail(RX_EINVAL, "ray_tail_lpr must be 0 (auto), 2 or 4 (got %d)", cfg->ray_tail_lpr);
-  if (cfg->kin_sort < -1 || cfg->kin_sort > 1)
-    return fail(RX_EINVAL, "kin_sort must be 0 (auto), 1 or -1 (got %d)", cfg->kin_sort);
-  if (cfg->window < -1 || cfg->window > 2)
-    return fail(RX_EINVAL, "window must be 0 (auto), 1 (k_window), 2 (k_flow) or -1 (got %d)", cfg->window);
+  if (cfg->lane_tracks < -1 || cfg->lane_tracks > 1)
+    return fail(RX_EINVAL, "lane_tracks must be 0 (auto), 1 or -1 (got %d)", cfg->lane_tracks);
+  if (cfg->reserved0 != 0)
+    return fail(RX_EINVAL, "reserved0 must be 0 (ABI v23 dropped the kin_sort schedule; got %d)", cfg->reserved0);
   if (cfg->task_sort < 0 || cfg->task_sort > 16)
     return fail(RX_EINVAL, "task_sort must be 0 (auto) or 1 .. 16 (got %d)", cfg->task_sort);
   if (cfg->n_agents == 2 && (cfg->dyn_lpe > 1 || cfg->reward_lpe > 2))
@@ -408,7 +402,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort, h->window, (int32_t)h->dyn_calls, h->cfg.kin_sort > 0 ? 1 : 0};
+                                    h->task_sort, 0, (int32_t)h->dyn_calls, 0};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -423,10 +417,7 @@ int rx_destroy(rx_env* h) {
                   &h->slot_n, &h->tasks})
     b->release();
   h->cs_scratch.release();
-  h->win_args.release();
-  h->flow_q.release();
-  h->flow_ctl.release();
-  h->flow_cnt.release();
+  h->policy_frag.release();
   h->prof_buf.release();
   h->resets.release();
   h->draw_rank.release();
@@ -692,48 +683,6 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->ray_waves_h = ray;
   h->n_dyn_waves = (int32_t)dyn.size();
   h->n_ray_waves = (int32_t)ray.size();
-  // rx_steps' multi-step windows (k_window): the single-agent split-step schedule at one lane
-  // per env and per ray with the direction sort every launch, and every block's workgroup
-  // resident at once (a workgroup that waits for a free slot would run its whole window after
-  // the others: the launch would take twice as long)
-  h->window = 0;
-  if (c.window > 0 && A == 1 && h->split && h->cfg.ray_order == 2 && h->ray_lpr == 1 && h->reward_lpe == 1 &&
-      h->task_sort == 1 && h->dyn_lpe == 1 && R <= 16 && h->cfg.autoreset != RX_AUTORESET_SAME_STEP) {
-    RX_HIP(hipSetDevice(h->cfg.device));
-    if (c.window == 1) {
-      if (h->window_cap == 0) h->window_cap = rx_window_capacity(h->cfg.device);
-      h->window = h->n_dyn_waves <= h->window_cap ? 1 : 0;
-    } else {
-      h->flow_grid = rx_flow_capacity(h->cfg.device);
-      h->window = h->flow_grid >= 8 ? 2 : 0;
-    }
-    // allocations here, not in rx_steps: none may happen inside a graph capture
-    if (h->window && !h->win_args.p) {
-      if (hipMalloc(&h->win_args.p, RX_WIN_MAX_STEPS * sizeof(rx_kargs)) != hipSuccess)
-        return fail(RX_ENOMEM, "rx_assign: window argument blocks");
-      h->win_args.n = RX_WIN_MAX_STEPS;
-    }
-    if (h->window == 2) {  // k_flow queues: per XCD (block b on queue b % 8) every task of a 64-step window
-      int per_step[8] = {0};
-      for (size_t b = 0; b < dyn.size(); ++b) per_step[b % 8] += 2 + (dyn[b].count * R + 63) / 64;
-      int mx = 0;
-      for (int x = 0; x < 8; ++x) mx = std::max(mx, per_step[x]);
-      h->flow_cap = mx * RX_WIN_MAX_STEPS;
-      h->flow_q.release();
-      h->flow_cnt.release();
-      if (hipMalloc(&h->flow_q.p, (size_t)8 * h->flow_cap * sizeof(int32_t)) != hipSuccess ||
-          hipMalloc(&h->flow_cnt.p, dyn.size() * sizeof(int32_t)) != hipSuccess)
-        return fail(RX_ENOMEM, "rx_assign: k_flow queues");
-      h->flow_q.n = (size_t)8 * h->flow_cap;
-      h->flow_cnt.n = dyn.size();
-      if (!h->flow_ctl.p) {
-        if (hipMalloc(&h->flow_ctl.p, RX_FLOW_CTL * sizeof(int32_t)) != hipSuccess)
-          return fail(RX_ENOMEM, "rx_assign: k_flow control words");
-        RX_HIP(hipMemset(h->flow_ctl.p, 0, RX_FLOW_CTL * sizeof(int32_t)));
-        h->flow_ctl.n = RX_FLOW_CTL;
-      }
-    }
-  }
   if (!h->policy_frag.p) {  // allocated here, not in rx_rollout_steps: it may run inside a graph capture
     RX_HIP(hipSetDevice(h->cfg.device));
     if (hipMalloc(&h->policy_frag.p, rx_policy_frag_bytes()) != hipSuccess)
@@ -862,7 +811,6 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.ray_tail_lpr = h->ray_tail_lpr;
   a.reward_lpe = h->reward_lpe;
   a.argmin_window = h->argmin_window;
-  a.kin_sort = h->cfg.kin_sort > 0 ? 1 : 0;
   a.slot_nenv = h->slot_n.p;
   a.wide = h->dyn_lpe == 64;
   a.n_wide_tasks = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;
@@ -1131,10 +1079,7 @@ int rx_step_phases(rx_env* h, const rx_io* io, int32_t phases, void* stream) {
   return launch(h, io, RX_MODE_STEP, nullptr, stream, phases);
 }
 
-// ABI v21: n_steps steps from one call.  With h->window (rx_assign) the steps run as
-// k_window launches, one per stretch of steps between two spatial re-sorts: the last
-// step of a stretch writes the sort keys (and counts the bins) exactly where the
-// per-step path would (dyn_calls % sort_interval == 0), and the re-sort follows it.
+// ABI v21: n_steps steps from one call, each the launches of rx_step on its io rows.
 static rx_io io_at(const rx_io* io, const rx_io_strides& st, int64_t s) {
   rx_io o = *io;
   o.actions = io->actions + s * st.actions;
@@ -1157,69 +1102,11 @@ int rx_steps(rx_env* h, const rx_io* io, int32_t n_steps, const rx_io_strides* s
   if (h->n_tracks <= 0 || !h->assigned || !h->bound)
     return fail(RX_ESTATE, "rx_steps needs rx_upload_tracks, rx_assign and rx_bind_state");
   const rx_io_strides st = strides ? *strides : rx_io_strides{};
-  hipStream_t s = (hipStream_t)stream;
   int rc;
-  int32_t k = 0;
-  while (k < n_steps) {
-    if (!h->window || h->sort_pending) {  // the per-step launches (a pending re-sort first runs in launch())
-      const rx_io o = io_at(io, st, k);
-      if ((rc = launch(h, &o, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
-      ++k;
-      continue;
-    }
-    // this window: up to and including the next step that writes the re-sort keys
-    int32_t len = std::min(n_steps - k, (int32_t)RX_WIN_MAX_STEPS);
-    bool keys = false;
-    const int iv = h->cfg.sort_interval;
-    if (iv > 0 && h->sort_on) {
-      const int64_t d = (int64_t)((iv - (int64_t)(h->dyn_calls % (uint64_t)iv)) % iv);  // steps before the key step
-      if (d < len) {
-        len = (int32_t)d + 1;
-        keys = true;
-      }
-    }
-    rx_kargs a{};
+  for (int32_t k = 0; k < n_steps; ++k) {
     const rx_io o = io_at(io, st, k);
-    make_kargs(h, &o, RX_MODE_STEP, nullptr, a);
-    if (h->window == 1) a.tasks_out = nullptr;  // k_window's ray tasks live in LDS (k_flow's in the task buffer)
-    if (keys) {
-      if (h->sort_hist_done) {  // counts of keys a previous launch wrote and no sort consumed
-        RX_HIP(hipMemsetAsync(h->sort_hist.p, 0, (size_t)h->sort_bins * sizeof(uint32_t), s));
-        h->sort_hist_done = false;
-      }
-      a.sort_keys = h->keys_in.p;
-      a.sort_hist = h->sort_hist.p;
-      a.sort_off = h->keys_off.p;
-    }
-    prof_arm(h, a, RX_KERNEL_WINDOW);
-    if (h->window == 2) {
-      const rx_flow f{h->flow_q.p, h->flow_ctl.p, h->flow_cnt.p, h->flow_cap, len};
-      if ((rc = rx_launch_flow(&a, &st, len, keys ? 1 : 0, h->win_args.p, &f, h->flow_grid, s)) != 0)
-        return fail(RX_EHIP, "k_flow launch failed: %s", hipGetErrorString((hipError_t)rc));
-    } else if ((rc = rx_launch_window(&a, &st, len, keys ? 1 : 0, h->win_args.p, s)) != 0) {
-      return fail(RX_EHIP, "k_window launch failed: %s", hipGetErrorString((hipError_t)rc));
-    }
-    h->dyn_calls += (uint64_t)len;
-    h->task_calls += (uint64_t)len;
-    h->tasks_stale = true;  // the global task buffer holds no order of these states
-    if (keys) {
-      rx_state work = h->work, tmp = h->work_tmp;
-      if ((rc = rx_sort_envs(h->keys_in.p, h->keys_off.p, h->cfg.n_envs, 1, h->sort_hist.p, h->sort_cursor.p,
-                             h->sort_bins, h->perm[0].p, h->perm[1].p, &work, &tmp, s, 1)) != 0)
-        return fail(RX_EHIP, "spatial sort failed: %s", hipGetErrorString((hipError_t)rc));
-    }
-    k += len;
+    if ((rc = launch(h, &o, RX_MODE_STEP, nullptr, stream)) != 0) return rc;
   }
-  return RX_OK;
-}
-
-int rx_flow_errors(rx_env* h, int32_t* out) {
-  if (!h || !out) return fail(RX_EINVAL, "rx_flow_errors: null argument");
-  *out = 0;
-  if (!h->flow_ctl.p) return RX_OK;
-  RX_HIP(hipSetDevice(h->cfg.device));
-  RX_HIP(hipDeviceSynchronize());
-  RX_HIP(hipMemcpy(out, h->flow_ctl.p + 256, sizeof(int32_t), hipMemcpyDeviceToHost));
   return RX_OK;
 }
 
@@ -1479,8 +1366,8 @@ int rx_ppo_minibatch_grad(const rx_ppo_batch* b, int32_t m, float* ws_f32, doubl
 
 size_t rx_ppo_update_workspace_floats(int32_t obs_dim, const rx_adam_config* cfg) {
   if ((obs_dim != 15 && obs_dim != 19) || adam_cfg_error(cfg) != RX_OK) return 0;
-  // + Adam's two step scalars + the fused tail's RX_PPO_TAIL_CTL control words (zero-filled by the caller once)
-  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors + 2 + RX_PPO_TAIL_CTL;
+  // the per-tensor sums of squares of every reduce block + Adam's two step scalars
+  return (size_t)rx_ppo_reduce_blocks(obs_dim) * cfg->n_tensors + 2;
 }
 
 int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_config* cfg, float* params,
@@ -1499,19 +1386,11 @@ int rx_ppo_minibatch_update(const rx_ppo_batch* b, int32_t m, const rx_adam_conf
   if (!ws_f32 || !ws_f64 || !grad || !exp_avg || !exp_avg_sq || !step || !lr || !stop || !kl_at_stop || !adam_ws)
     return fail(RX_EINVAL, "rx_ppo_minibatch_update: null buffer");
   const hipStream_t s = (hipStream_t)stream;
-#if RX_PPO_FUSED_TAIL
-  // gradient, then ONE launch that reduces it, hands the clip coefficient over and steps Adam
-  const rx_adam_tail tail{params, exp_avg, exp_avg_sq};
-  if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step, lr,
-                               &tail)))
-    return fail(RX_EHIP, "ppo update launch failed: %s", hipGetErrorString((hipError_t)rc));
-#else
   if ((rc = rx_launch_ppo_grad(b, m, 1.0f, stop, kl_at_stop, nullptr, ws_f32, ws_f64, grad, s, cfg, adam_ws, step, lr)))
     return fail(RX_EHIP, "ppo grad launch failed: %s", hipGetErrorString((hipError_t)rc));
   if ((rc = rx_launch_adam_apply(cfg, params, grad, exp_avg, exp_avg_sq, step, lr, stop, adam_ws,
                                  rx_ppo_reduce_blocks(b->obs_dim), s)))
     return fail(RX_EHIP, "adam launch failed: %s", hipGetErrorString((hipError_t)rc));
-#endif
   return RX_OK;
 }
 

@@ -168,7 +168,6 @@ struct rx_kargs {
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
   int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
   int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
-  int32_t kin_sort;       // sorting KIN launches: k_kin1p (the ranking over a 4-wave workgroup), else k_kin1
   int32_t ray_tail_from;  // ray waves >= this one (the dispatch tail) hold 64 / ray_tail_lpr tasks each, cast at
   int32_t ray_tail_lpr;   // ray_tail_lpr lanes per ray (2 or 4); -1 = no tail split (rx_config.ray_tail)
   // rx_set_start_draws (two-car envs): the start-slot order of the env that is the
@@ -186,31 +185,6 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
 #define RX_SPLIT_REWARD 1
 #define RX_SPLIT_REWARD_RAYS 2
 extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStream_t s);
-// k_window: n_steps single-agent split steps in one launch, a workgroup per
-// dynamics block (rx_steps); keys_last: the last step writes the re-sort keys
-// k_flow (rx_steps with rx_config.window = 2): the steps of a window as a task
-// graph over per-XCD ready queues.  q: [8][cap] task codes (-1 = not yet pushed);
-// ctl: per XCD x, at 32 x: head, tail (both in units of 64 per entry: one full-wave
-// atomic per pop / push), tasks of the window; ctl[256]: error flags (bounded-spin
-// timeouts; 0 = none); cnt: [n_blocks] arrival counters (64 per task).
-#define RX_FLOW_CTL 512
-struct rx_flow {
-  int32_t* q;
-  int32_t* ctl;
-  int32_t* cnt;
-  int32_t cap;      // queue entries per XCD
-  int32_t n_steps;  // steps of this window
-};
-extern "C" int rx_launch_flow(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last, rx_kargs* args,
-                              const rx_flow* f, int grid, hipStream_t s);
-extern "C" int rx_flow_capacity(int device);
-// k_window workgroups the device holds at once (occupancy API x CUs, less one
-// workgroup per CU where the SGPR count makes the API over-report: MI355X_MICROARCH.md)
-extern "C" int rx_window_capacity(int device);
-// args: device buffer of RX_WIN_MAX_STEPS argument blocks (k_window_args fills n_steps of them)
-#define RX_WIN_MAX_STEPS 64
-extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last,
-                                rx_kargs* args, hipStream_t s);
 // persistent small-N rollout (k_rollout): a->n_dyn_waves workgroups, one env
 // each, its slot staged in max_w * 96 bytes of dynamic LDS
 #define RX_ROLLOUT_MAX_W 1024
@@ -295,20 +269,7 @@ extern "C" int rx_launch_kl_check(const float* kl, float kl_target, uint8_t* sto
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
                                   const rx_adam_config* cfg = nullptr, float* norm_ws = nullptr,
-                                  float* step = nullptr, const double* lr = nullptr,
-                                  const struct rx_adam_tail* fused = nullptr);
-// the Adam state the fused minibatch tail updates (k_ppo_reduce<true>): with it
-// the reduce launch also clips and applies Adam (norm_ws: + the control block).
-// A/B build only (RX_PPO_FUSED_TAIL=1): 16.3 us against 5.0 + 5.1 us for the
-// reduce and k_adam_apply launches it replaces
-#ifndef RX_PPO_FUSED_TAIL
-#define RX_PPO_FUSED_TAIL 0
-#endif
-struct rx_adam_tail {
-  float* p;
-  float* m;
-  float* v;
-};
+                                  float* step = nullptr, const double* lr = nullptr);
 extern "C" int rx_ppo_reduce_blocks(int obs_dim);
 extern "C" int rx_launch_adam_apply(const rx_adam_config* cfg, float* p, float* g, float* m, float* v, float* step,
                                     const double* lr, const uint8_t* stop, float* ws, int nb, hipStream_t s);

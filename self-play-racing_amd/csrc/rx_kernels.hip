@@ -56,25 +56,14 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// State accesses of the env device functions.  C = false: plain loads and stores.
-// C = true (k_flow: a block's steps run as tasks on waves of any CU of its XCD, so
-// the state rows are handed from workgroup to workgroup): every load and store of
-// handed-off bytes is a global_load / global_store with sc1 -- the hand-off form of
-// MI355X_MICROARCH.md "Valid forms" (row 1: sc1 stores, vmcnt(0) before the flag,
-// sc1 loads after the poll; the L1 of the reading CU is never consulted).
-template <bool C, class T>
+// State accesses of the env device functions (plain loads and stores).
+template <class T>
 __device__ __forceinline__ T ldc(const T* p) {
-  if constexpr (C)
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    return *p;
+  return *p;
 }
-template <bool C, class T, class U>
+template <class T, class U>
 __device__ __forceinline__ void stc(T* p, U v) {
-  if constexpr (C)
-    __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = (T)v;
+  *p = (T)v;
 }
 
 // f32 np.clip with Python-float bounds (stays float32 under NEP 50)
@@ -434,15 +423,7 @@ __device__ __forceinline__ void write_sort_key(const rx_kargs& a, int pos, int k
 // env's position.  Runs every step with all 64 lanes of the wave (env lanes
 // have p >= 0).  The direction is the car's new angle
 // (the one k_rays casts from).  Scheduling only: no result depends on it.
-// Write-amplification A/B build only (profiles/r05/ab_write_amp.jsonl):
-// -DRX_WA_POSORDER=1 makes every io row of the single-agent split step (actions,
-// obs, reward, masks) the env's POSITION instead of its env id, so each wave's
-// rows are one contiguous, coalesced range -- an upper bound on what coalescing
-// the io traffic could buy.  Its outputs are permuted (not a product build).
-#ifndef RX_WA_POSORDER
-#define RX_WA_POSORDER 0
-#endif
-#define RX_IO_ROW(a, pos) (RX_WA_POSORDER ? (pos) : (a).perm[(pos)])
+#define RX_IO_ROW(a, pos) ((a).perm[(pos)])
 constexpr int kTaskSectors = 64;
 template <int A>
 __device__ __forceinline__ int sort_block_tasks_lds(const rx_kargs& a, int p, const double* ang, int32_t* cnt,
@@ -502,14 +483,14 @@ __device__ __forceinline__ int sort_block_tasks_lds(const rx_kargs& a, int p, co
 }
 
 // the block's sorted task ids from the LDS row to tasks_out[perm_start*A*R ..],
-// 64-lane contiguous stores (k_kin1 / k_dyn; k_window's ray tasks read the row in place)
-template <int A, bool C = false>
+// 64-lane contiguous stores (k_kin1 / k_dyn)
+template <int A>
 __device__ __forceinline__ void sort_block_tasks(const rx_kargs& a, int perm_start, int p, const double* ang,
                                                  int32_t* cnt, int32_t* stage) {
   const int total = sort_block_tasks_lds<A>(a, p, ang, cnt, stage);
   const int lane = threadIdx.x & 63;
   int32_t* out = a.tasks_out + (size_t)perm_start * (A * a.n_sensors);
-  for (int i = lane; i < total; i += 64) stc<C>(out + i, stage[i]);
+  for (int i = lane; i < total; i += 64) stc(out + i, stage[i]);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -569,7 +550,7 @@ struct rx_slot_lds {
   const double4* seg;
 };
 
-template <int LPE, int PART, bool C = false>
+template <int LPE, int PART>
 __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
                                          int sub_block = 0, const rx_slot_lds* sl = nullptr) {
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
@@ -599,28 +580,28 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   int e = REW ? -1 : RX_IO_ROW(a, p);  // REWARD: loaded after the argmins
 
   const rx_state& S = a.st;
-  uint8_t ef = ldc<C>(S.env_flags + p);
-  uint8_t fl = ldc<C>(S.flags + p);
+  uint8_t ef = ldc(S.env_flags + p);
+  uint8_t fl = ldc(S.flags + p);
   // every per-env load up front, so their latencies overlap (not one round
   // trip per use) -- except in the REWARD half, which runs under the raycast
   // at the raycast's 64-VGPR budget: its values not needed by the argmins
   // (velocity, last progress, episode counters, steps) load after them, so
   // they are not live across the argmin loops (fewer spills)
-  Car c{ldc<C>(S.x + p), ldc<C>(S.y + p), REW ? 0.0 : ldc<C>(S.angle + p), REW ? 0.0 : ldc<C>(S.vx + p), REW ? 0.0 : ldc<C>(S.vy + p), ldc<C>(S.progress + p),
+  Car c{ldc(S.x + p), ldc(S.y + p), REW ? 0.0 : ldc(S.angle + p), REW ? 0.0 : ldc(S.vx + p), REW ? 0.0 : ldc(S.vy + p), ldc(S.progress + p),
         (fl & RX_F_CRASHED) != 0};
-  double last_steering = REW ? 0.0 : ldc<C>(S.last_steering + p);
+  double last_steering = REW ? 0.0 : ldc(S.last_steering + p);
   const bool step_mode = a.mode == RX_MODE_STEP;  // wave-uniform
   const float2 act =
       (step_mode && !REW) ? reinterpret_cast<const float2*>(a.io.actions)[e] : make_float2(0.0f, 0.0f);
-  double last_progress = (KIN || REW) ? 0.0 : ldc<C>(S.last_progress + p);
-  double ep_ret0 = (KIN || REW) ? 0.0 : ldc<C>(S.ep_return + p);
-  int ep_len0 = (KIN || REW) ? 0 : ldc<C>(S.ep_length + p);
+  double last_progress = (KIN || REW) ? 0.0 : ldc(S.last_progress + p);
+  double ep_ret0 = (KIN || REW) ? 0.0 : ldc(S.ep_return + p);
+  int ep_len0 = (KIN || REW) ? 0 : ldc(S.ep_length + p);
   double speed_w = (KIN || REW) ? 0.0 : (S.speed_weight ? S.speed_weight[e] : a.speed_weight);  // caller's, env order
-  int steps = REW ? 0 : ldc<C>(S.steps + p);  // REWARD: already advanced by KIN
+  int steps = REW ? 0 : ldc(S.steps + p);  // REWARD: already advanced by KIN
   double cs[2] = {0.0, 0.0};
   if (REW) {
-    cs[0] = ldc<C>(a.cs_scratch + 2 * p);
-    cs[1] = ldc<C>(a.cs_scratch + 2 * p + 1);
+    cs[0] = ldc(a.cs_scratch + 2 * p);
+    cs[1] = ldc(a.cs_scratch + 2 * p + 1);
   }
   RX_STAMP(1);
   bool do_reset;
@@ -695,13 +676,13 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   if constexpr (REW) __asm__ volatile("" : "+v"(p));
   if (REW) {  // the REWARD half's late loads (see above)
     e = RX_IO_ROW(a, p);
-    c.vx = ldc<C>(S.vx + p);
-    c.vy = ldc<C>(S.vy + p);
-    last_progress = ldc<C>(S.last_progress + p);
-    ep_ret0 = ldc<C>(S.ep_return + p);
-    ep_len0 = ldc<C>(S.ep_length + p);
+    c.vx = ldc(S.vx + p);
+    c.vy = ldc(S.vy + p);
+    last_progress = ldc(S.last_progress + p);
+    ep_ret0 = ldc(S.ep_return + p);
+    ep_len0 = ldc(S.ep_length + p);
     speed_w = S.speed_weight ? S.speed_weight[e] : a.speed_weight;
-    steps = ldc<C>(S.steps + p);
+    steps = ldc(S.steps + p);
   }
   bool ended = false;
   double epr = 0.0, epl_d = 0.0;
@@ -737,8 +718,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     epr = ep_ret0 + r;
     const int epl = ep_len0 + 1;
     epl_d = (double)epl;
-    stc<C>(S.ep_return + p, epr);
-    stc<C>(S.ep_length + p, epl);
+    stc(S.ep_return + p, epr);
+    stc(S.ep_length + p, epl);
     ended = term || trunc;
     if (a.io.ep_done) a.io.ep_done[e] = ended;
     if (ended && a.autoreset == RX_AUTORESET_NEXT_STEP) ef |= RX_EF_PENDING_RESET;
@@ -768,8 +749,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     last_steering = 0.0;
     ef &= (uint8_t)~RX_EF_PENDING_RESET;
     if (KIN) ef |= RX_EF_RESET_NOW;
-    stc<C>(S.ep_return + p, 0.0);
-    stc<C>(S.ep_length + p, 0);
+    stc(S.ep_return + p, 0.0);
+    stc(S.ep_length + p, 0);
     if (a.io.info && (a.mode == RX_MODE_RESET || a.autoreset == RX_AUTORESET_NEXT_STEP)) {
       double* inf = a.io.info + (size_t)e * RX_INFO_W;
       inf[RX_INFO_SPEED] = 0.0;
@@ -780,48 +761,43 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   }
   if (REW && do_reset) ef &= (uint8_t)~RX_EF_RESET_NOW;
   if (FULL && (stepping || do_reset)) {
-    stc<C>(S.x + p, c.x);
-    stc<C>(S.y + p, c.y);
-    stc<C>(S.angle + p, c.angle);
-    stc<C>(S.vx + p, c.vx);
-    stc<C>(S.vy + p, c.vy);
-    stc<C>(S.progress + p, c.progress);
-    stc<C>(S.last_progress + p, c.progress);  // racing_env.py:165 (0.0 after reset)
-    stc<C>(S.last_steering + p, last_steering);
-    stc<C>(S.steps + p, steps);
-    stc<C>(S.flags + p, fl);
-    stc<C>(S.env_flags + p, ef);
+    stc(S.x + p, c.x);
+    stc(S.y + p, c.y);
+    stc(S.angle + p, c.angle);
+    stc(S.vx + p, c.vx);
+    stc(S.vy + p, c.vy);
+    stc(S.progress + p, c.progress);
+    stc(S.last_progress + p, c.progress);  // racing_env.py:165 (0.0 after reset)
+    stc(S.last_steering + p, last_steering);
+    stc(S.steps + p, steps);
+    stc(S.flags + p, fl);
+    stc(S.env_flags + p, ef);
   }
   if (KIN && (stepping || do_reset)) {
-    stc<C>(S.x + p, c.x);
-    stc<C>(S.y + p, c.y);
-    stc<C>(S.angle + p, c.angle);
-    stc<C>(S.vx + p, c.vx);
-    stc<C>(S.vy + p, c.vy);
-    stc<C>(S.last_steering + p, last_steering);
-    stc<C>(S.steps + p, steps);
+    stc(S.x + p, c.x);
+    stc(S.y + p, c.y);
+    stc(S.angle + p, c.angle);
+    stc(S.vx + p, c.vx);
+    stc(S.vy + p, c.vy);
+    stc(S.last_steering + p, last_steering);
+    stc(S.steps + p, steps);
     if (moving) {
-      if constexpr (C) {
-        stc<C>(a.cs_scratch + 2 * p, cs[0]);
-        stc<C>(a.cs_scratch + 2 * p + 1, cs[1]);
-      } else {
-        reinterpret_cast<double2*>(a.cs_scratch)[p] = make_double2(cs[0], cs[1]);
-      }
+      reinterpret_cast<double2*>(a.cs_scratch)[p] = make_double2(cs[0], cs[1]);
     }
     if (do_reset) {
-      stc<C>(S.progress + p, 0.0);
-      stc<C>(S.last_progress + p, 0.0);
-      stc<C>(S.flags + p, fl);
-      stc<C>(S.env_flags + p, ef);
+      stc(S.progress + p, 0.0);
+      stc(S.last_progress + p, 0.0);
+      stc(S.flags + p, fl);
+      stc(S.env_flags + p, ef);
     }
   }
   if (REW && (stepping || do_reset)) {
     if (stepping) {
-      stc<C>(S.progress + p, c.progress);
-      stc<C>(S.last_progress + p, c.progress);  // racing_env.py:165
-      stc<C>(S.flags + p, fl);
+      stc(S.progress + p, c.progress);
+      stc(S.last_progress + p, c.progress);  // racing_env.py:165
+      stc(S.flags + p, fl);
     }
-    stc<C>(S.env_flags + p, ef);
+    stc(S.env_flags + p, ef);
   }
   RX_STAMP(7);
   // ---------------------------------------------------------------- outputs
@@ -941,87 +917,6 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const unsigned long long t7 = __builtin_amdgcn_s_memtime();
   if (a.io.counters && (threadIdx.x & 63) == 0) a.io.counters[16 + 12 * wave + 9] = t7;
 #endif
-}
-
-// k_kin1 on the launches that sort the ray tasks (tasks_out set): a 4-wave
-// workgroup per 64-env block.  Wave 0 steps the block's kinematics
-// (dyn1_env<1, KIN>, as k_kin1); then every wave ranks the ray tasks of a
-// contiguous quarter of the sensors (rays [w*q, (w+1)*q), q = ceil(R/4)) in
-// per-wave sector counters with the LDS atomics of sort_block_tasks_lds -- 704
-// tasks on 256 lanes instead of 64, the phase that was 48 % of k_kin1's wave
-// (profiles/r04/kin_stamps.json) -- wave 0 turns the 4 x 64 counts into
-// offsets (sector-major, wave-minor), every wave scatters its tasks into the
-// LDS row and the whole workgroup stores the row.  A wave ranks its rays in
-// ray order and a wave instruction ranks its lanes in lane order, so the order
-// inside a sector is (ray, env position): the row k_kin1 writes, entry for entry.
-constexpr int kKinWaves = 4;
-__global__ __launch_bounds__(64 * kKinWaves) void k_kin1p(rx_kargs a) {
-  const int b = uniform((int)blockIdx.x);
-  const int wv = uniform((int)(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  __shared__ int32_t tcnt[kKinWaves][kTaskSectors];
-  __shared__ int32_t tstage[64 * 16];
-  __shared__ double sAng[64];
-  __shared__ int32_t sPos[64];
-  __shared__ int32_t sTotal;
-  if (b >= a.n_dyn_waves) return;
-  const unsigned long long prof_t0 = prof_start(a);
-  tcnt[wv][lane] = 0;
-  if (wv == 0) {
-    double ang[1], ep[3] = {0.0, 0.0, 0.0};
-    int e = -1;
-    dyn1_env<1, RX_PART_KIN>(a, b, ang, e, ep);
-    sAng[lane] = ang[0];
-    sPos[lane] = e;
-  }
-  __syncthreads();
-  constexpr int kRW = 16 / kKinWaves;  // rays per wave at most (n_sensors <= 16 with ray_order 2)
-  const int R = a.n_sensors, q = (R + kKinWaves - 1) / kKinWaves;
-  const int p_l = sPos[lane];
-  const double ang_l = sAng[lane];
-  const float inv = (float)kTaskSectors * 0.15915494309189535f;  // sectors per radian
-  int pk[kRW];
-#pragma unroll
-  for (int i = 0; i < kRW; ++i) {
-    const int r = wv * q + i;
-    pk[i] = -1;
-    if (i < q && r < R && p_l >= 0) {
-      const float th = (float)(ang_l + a.rel_angles[r]);
-      const int sec = (int)__builtin_floorf(th * inv) & (kTaskSectors - 1);
-      pk[i] = (atomicAdd(&tcnt[wv][sec], 1) << 6) | sec;
-    }
-  }
-  __syncthreads();
-  if (wv == 0) {  // counts -> exclusive offsets, sector-major then wave
-    int cw[kKinWaves], c0 = 0;
-#pragma unroll
-    for (int w = 0; w < kKinWaves; ++w) {
-      cw[w] = tcnt[w][lane];
-      c0 += cw[w];
-    }
-    int c = c0;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(c, o, 64);
-      if (lane >= o) c += v;
-    }
-    int base = c - c0;
-#pragma unroll
-    for (int w = 0; w < kKinWaves; ++w) {
-      tcnt[w][lane] = base;
-      base += cw[w];
-    }
-    if (lane == 63) sTotal = c;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kRW; ++i)
-    if (pk[i] >= 0) tstage[tcnt[wv][pk[i] & 63] + (pk[i] >> 6)] = p_l * R + wv * q + i;  // task (A p + q) R + r
-  __syncthreads();
-  const int total = sTotal;
-  int32_t* out = a.tasks_out + (size_t)uniform(a.dyn_waves[b].perm_start) * R;
-  for (int i = (int)threadIdx.x; i < total; i += 64 * kKinWaves) out[i] = tstage[i];
-  if (wv == 0) prof_end(a, b, prof_t0);
 }
 
 // ============================================================ k_dyn, A == 2
@@ -1877,9 +1772,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 
 // One ray wave: the wave record `we` (slot, tasks [task_start, task_start + count)
 // of `tasks`: the ray-wave table's record and the global task buffer in k_step2 /
-// k_rays; in k_window a record built from the block and the block's sorted task row
-// in LDS).  `wave` only indexes the profiling stamps.
-template <int A, int LPR, bool C = false>
+// k_rays).  `wave` only indexes the profiling stamps.
+template <int A, int LPR>
 __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
 #ifdef RX_RAY_STAMPS
   unsigned long long rstamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1904,7 +1798,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   const int task = we.task_start + (own ? tl : count - 1);
   int env_local = 0, q, ray, pos;
   if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
-    const int t = ldc<C>(tasks + task);
+    const int t = ldc(tasks + task);
     const int iq = t / R;
     ray = t - iq * R;
     pos = iq / A;
@@ -1923,8 +1817,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   }
   if (a.ray_order != 2) pos = we.perm_start + env_local;
   const int i = A * pos + q;  // working state (position order); the obs row is A * perm[pos] + q
-  const double ox = ldc<C>(a.st.x + i), oy = ldc<C>(a.st.y + i);
-  const double theta = ldc<C>(a.st.angle + i) + a.rel_angles[ray];  // racing_env.py:50
+  const double ox = ldc(a.st.x + i), oy = ldc(a.st.y + i);
+  const double theta = ldc(a.st.angle + i) + a.rel_angles[ray];  // racing_env.py:50
   RAY_STAMP(1);
   double sn, cs;
   rx_sincos(theta, &sn, &cs);
@@ -1955,7 +1849,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     const float csf = (float)cs, snf = (float)sn;
     const rx_f2 id2 = {1.0f / csf, 1.0f / snf};
     // visit chunks outward from the wave's first car
-    int w0 = (int)(ldc<C>(a.st.progress + i) * (double)W + 0.5);
+    int w0 = (int)(ldc(a.st.progress + i) * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
     const int c0 = uniform(w0 / G);
     // direction quadrant (sign bits of the f32 direction, as id2's signs): a
@@ -2198,316 +2092,6 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     rays_dispatch<A, LPR>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
-}
-
-// ============================================================ k_window
-// K consecutive single-agent split steps in ONE launch (rx_steps; DESIGN.md §3
-// "Multi-step window").  Inside a re-sort window the only cross-env dependency of
-// RacingEnv.step is none at all: step t + 1 of a 64-env dynamics block needs only
-// that block's step t (its state rows, its done flags).  So a workgroup owns one
-// block for all K steps and runs, per step,
-//   phase K : wave 0 = dyn1_env<1, KIN> (next-step autoreset, actions, kinematics,
-//             the non-ray obs columns) and the block's ray-task direction sort into
-//             an LDS row (never stored: the ray tasks read it in place);
-//   phase R : the block's REWARD (dyn1_env<1, REWARD>) and its ray waves (the
-//             sorted row in classes of 64 tasks), handed to the workgroup's waves
-//             from an LDS counter -- REWARD first, then the classes centre-first
-//             (their chains are the longest: longest-processing-time order);
-// with a workgroup barrier after each phase.  The device functions are those of
-// k_kin1 / k_step2, called on the same rows with the same operands, so every
-// output is bit-identical to K x rx_step (scheduling only; the ray-task order
-// inside the block never changes a result).  What changes is the schedule: no
-// launch boundary between steps and no chip-wide drain per step -- while one
-// block waits on its slowest ray wave, the other blocks sharing the CU run.
-// Every workgroup must be resident at once to keep that (rx_assign sizes the
-// waves per workgroup, RX_WIN_WAVES, so the grid fits); the only inter-workgroup
-// state is the episode-statistics / re-sort-count atomics.  The re-sort (which
-// moves envs between blocks) ends a window: the last step writes the sort keys
-// (and the bin counts), the host launches the re-sort after it.
-#ifndef RX_WIN_WAVES
-#define RX_WIN_WAVES 4  // waves per workgroup (one 64-env block)
-#endif
-#ifndef RX_WIN_MINW
-#define RX_WIN_MINW 6  // min waves per SIMD (80 VGPRs): 6 workgroups of 4 waves per CU >= 1,029 blocks at 65,536 envs
-#endif
-#ifndef RX_WIN_PSORT
-#define RX_WIN_PSORT 1  // phase K's ray-task ranking spread over the workgroup's waves
-#endif
-constexpr int kWinWaves = RX_WIN_WAVES;
-
-// phase R task t (0 = REWARD, 1 .. n = ray class) -> ray class, centre first:
-// 5, 4, 6, 3, 7, ... for 11 classes (|2j - (n - 1)| ascending, lower j first)
-__device__ __forceinline__ int win_class(int t, int n) {
-  const int c = (n - 1) >> 1;  // centre class (lower one for even n)
-  const int i = t - 1, h = (i + 1) >> 1;
-  return (n & 1) ? ((i & 1) ? c - h : c + h) : ((i & 1) ? c + h : c - h);
-}
-
-// The per-step argument blocks of a window: step s's = the launch's with the io
-// rows of step s and the re-sort keys on the last step only.  Written by
-// k_window_args (one lane per step) into a handle buffer before k_window runs;
-// k_window reads step s's block through the constant address space, so its
-// fields are scalar loads like kernel arguments -- a block copied inside the
-// kernel kept ~40 modified or hoisted fields live in SGPRs across the step loop
-// (349 SGPR spills).
-__global__ void k_window_args(rx_kargs a, rx_io_strides st, int n_steps, int keys_last, rx_kargs* out) {
-  const int s = threadIdx.x;
-  if (s >= n_steps) return;
-  rx_kargs o = a;
-  o.io.actions = a.io.actions + (ptrdiff_t)s * st.actions;
-  o.io.obs = a.io.obs + (ptrdiff_t)s * st.obs;
-  if (a.io.reward) o.io.reward = a.io.reward + (ptrdiff_t)s * st.reward;
-  if (a.io.reward64) o.io.reward64 = a.io.reward64 + (ptrdiff_t)s * st.reward64;
-  if (a.io.terminated) o.io.terminated = a.io.terminated + (ptrdiff_t)s * st.terminated;
-  if (a.io.truncated) o.io.truncated = a.io.truncated + (ptrdiff_t)s * st.truncated;
-  if (a.io.done_f32) o.io.done_f32 = a.io.done_f32 + (ptrdiff_t)s * st.done_f32;
-  if (a.io.info) o.io.info = a.io.info + (ptrdiff_t)s * st.info;
-  if (a.io.ep_done) o.io.ep_done = a.io.ep_done + (ptrdiff_t)s * st.ep_done;
-  const bool keys = keys_last && s == n_steps - 1;
-  o.sort_keys = keys ? a.sort_keys : nullptr;
-  o.sort_hist = keys ? a.sort_hist : nullptr;
-  out[s] = o;
-}
-
-typedef const __attribute__((address_space(4))) rx_kargs* rx_ckargs;
-
-__global__ __launch_bounds__(64 * kWinWaves, RX_WIN_MINW) void k_window(const rx_kargs* args, int n_steps) {
-  const int b = uniform((int)blockIdx.x);  // dynamics block
-  const int wv = uniform((int)(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  __shared__ int32_t tcnt[kTaskSectors];
-  __shared__ int32_t tstage[64 * 16];  // the block's direction-sorted ray tasks (A = 1: <= 64 x 16)
-  __shared__ int32_t next_task;        // phase R work counter
-#if RX_WIN_PSORT
-  __shared__ double sAng[64];  // phase K: the block's stepped angles and positions (-1: no env) for the ranking
-  __shared__ int32_t sPos[64];
-#endif
-  const rx_kargs& a0 = *(const rx_kargs*)(rx_ckargs)args;
-  if (b >= a0.n_dyn_waves) return;
-  // the block's record through the constant address space: scalar loads, SGPR results
-  typedef const __attribute__((address_space(4))) int32_t* rx_cip;
-  const rx_cip dwp = (rx_cip)(const int32_t*)(a0.dyn_waves + b);
-  const int dw_track = dwp[0], dw_perm = dwp[1];
-  const int n_tasks = dwp[3] * a0.n_sensors;
-  const int n_cls = (n_tasks + 63) >> 6;
-  const unsigned long long prof_t0 = prof_start(a0);
-  for (int s = 0; s < n_steps; ++s) {
-    const rx_kargs& as = *(const rx_kargs*)((rx_ckargs)args + s);
-    // ---- phase K: wave 0 steps the block's kinematics
-#if RX_WIN_PSORT
-    // ... and every wave ranks the ray tasks of its share of the sensors (ray r on
-    // wave r % kWinWaves; the LDS counting sort of sort_block_tasks_lds with the
-    // ranking spread over the workgroup: 704 tasks on 4 x 64 lanes, not 64).  The
-    // order inside a sector is the atomics' order either way: scheduling only.
-    if (wv == 0) {
-      tcnt[lane] = 0;
-      double ang[1], ep[3] = {0.0, 0.0, 0.0};
-      int e = -1;
-      dyn1_env<1, RX_PART_KIN>(as, b, ang, e, ep);
-      sAng[lane] = ang[0];
-      sPos[lane] = e;
-      if (lane == 0) next_task = 0;
-    }
-    __syncthreads();
-    constexpr int kRW = (16 + kWinWaves - 1) / kWinWaves;  // rays per wave (n_sensors <= 16)
-    const int R = a0.n_sensors;
-    const int p_l = sPos[lane];
-    const double ang_l = sAng[lane];
-    const float inv = (float)kTaskSectors * 0.15915494309189535f;  // sectors per radian
-    int pk[kRW];
-#pragma unroll
-    for (int i = 0; i < kRW; ++i) {
-      const int r = wv + kWinWaves * i;
-      pk[i] = -1;
-      if (r < R && p_l >= 0) {
-        const float th = (float)(ang_l + as.rel_angles[r]);
-        const int sec = (int)__builtin_floorf(th * inv) & (kTaskSectors - 1);
-        pk[i] = (atomicAdd(&tcnt[sec], 1) << 6) | sec;
-      }
-    }
-    __syncthreads();
-    if (wv == 0) {  // sector counts -> exclusive offsets
-      const int c0 = tcnt[lane];
-      int c = c0;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(c, o, 64);
-        if (lane >= o) c += v;
-      }
-      tcnt[lane] = c - c0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kRW; ++i)
-      if (pk[i] >= 0) tstage[tcnt[pk[i] & 63] + (pk[i] >> 6)] = p_l * R + wv + kWinWaves * i;  // task (A p + q) R + r
-    __syncthreads();
-#else
-    // ... and sorts its ray tasks (sort_block_tasks_lds)
-    if (wv == 0) {
-      tcnt[lane] = 0;
-      double ang[1], ep[3] = {0.0, 0.0, 0.0};
-      int e = -1;
-      dyn1_env<1, RX_PART_KIN>(as, b, ang, e, ep);
-      sort_block_tasks_lds<1>(as, e, ang, tcnt, tstage);
-      if (lane == 0) next_task = 0;
-    }
-    __syncthreads();
-#endif
-    // ---- phase R: REWARD and the ray classes over the workgroup's waves
-#ifdef RX_WIN_STATIC  // bring-up variant: task t on wave t % kWinWaves
-    for (int t = wv; t <= n_cls; t += kWinWaves) {
-#else
-    for (;;) {
-      // the wave takes the next task with ONE unconditional atomic from all 64 lanes
-      // (the loop head is uniform, every lane active): the compiler folds it into a
-      // single ds_add_rtn of 64 whose old value, a multiple of 64, every lane reads
-      // back into an SGPR -- so the loop exit is a scalar branch.  `if (lane == 0) t =
-      // atomicAdd(..)` + a cross-lane read was structurized into a nested divergent
-      // loop whose back edge skipped the atomic: the REWARD task ran forever (hung
-      // at 4,096 envs in 64-step windows); lane == 0 ? 1 : 0 from every lane was
-      // correct but cost a 64-iteration scan per task.
-      const int t = __builtin_amdgcn_readfirstlane(atomicAdd(&next_task, 1)) >> 6;
-      if (t > n_cls) break;
-#endif
-      if (t == 0) {
-        double ang[1], ep[3] = {0.0, 0.0, 0.0};
-        int e = -1;
-        dyn1_env<1, RX_PART_REWARD>(as, b, ang, e, ep);
-        add_episode_stats(as, ep);
-      } else {
-        const int j = win_class(t, n_cls);
-        const rx_wave rw{dw_track, dw_perm, 64 * j, min(64, n_tasks - 64 * j)};
-        rays_wave<1, 1>(as, rw, tstage, b);
-      }
-    }
-    __syncthreads();
-  }
-  if (wv == 0) prof_end(a0, b, prof_t0);
-}
-
-// ============================================================ k_flow
-// The same steps as k_window, scheduled as a task graph (rx_config.window = 2;
-// DESIGN.md §3 "Task-graph windows").  k_window keeps a block on one workgroup
-// for the whole window, so the window ends with the slowest block's 8-step chain
-// (its workgroups' durations spread 280-800 us at 65,536 envs).  Here every
-// (step, block) has the tasks of the split step -- KIN (dyn1_env<1, KIN> + the
-// block's ray-task sort), REWARD, and the block's ray classes -- and any wave of
-// the block's XCD runs any ready one: KIN(b, s) is ready when REWARD and every ray
-// class of (b, s - 1) have arrived (the last arrival pushes it), REWARD / rays of
-// (b, s) when KIN(b, s) is done (it pushes them).  One-wave workgroups pop task
-// codes from their XCD's queue (s_getreg XCC_ID; block b lives on queue b % 8,
-// so a block's tasks all run under one L2); the state rows a task hands to the
-// next go through sc1 stores and sc1 loads (ldc / stc, C = true) with the
-// storing wave's vmcnt(0) before the push or arrival -- MI355X_MICROARCH.md
-// "Valid forms", row 1.  Every wave of the window is a persistent worker; a
-// wave exits when its XCD's pops pass the window's task count.  Every spin is
-// bounded (the flag in ctl[256] records a timeout; rx_flow_errors reads it).
-// Bit-identical to K x rx_step by the same argument as k_window.
-#ifndef RX_FLOW_MINW
-#define RX_FLOW_MINW 6
-#endif
-#ifndef RX_FLOW_SLEEP
-#define RX_FLOW_SLEEP 2  // s_sleep between polls of an empty queue entry (x 64 cycles)
-#endif
-#ifndef RX_FLOW_SPIN_MAX
-#define RX_FLOW_SPIN_MAX (1 << 22)  // polls (~2 s with s_sleep 2) before a wave gives up
-#endif
-__device__ __forceinline__ int xcc_id() {
-  unsigned x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return (int)(x & 7);
-}
-
-// per window: KIN(b, 0) of every block queued on its XCD, the rest of each queue
-// emptied, counters zeroed, the window's task count per XCD.  Workgroup x = XCD x.
-__global__ __launch_bounds__(256) void k_flow_init(const rx_wave* __restrict__ dyn, int n_blocks, int R, rx_flow f) {
-  const int x = blockIdx.x;
-  int32_t* q = f.q + (size_t)x * f.cap;
-  int32_t* ctl = f.ctl + 32 * x;
-  int nb = 0, per_step = 0;
-  for (int b = x; b < n_blocks; b += 8) {
-    ++nb;
-    per_step += 2 + (dyn[b].count * R + 63) / 64;  // KIN, REWARD, ray classes
-  }
-  for (int i = threadIdx.x; i < f.cap; i += blockDim.x) {
-    const int b = x + 8 * i;
-    q[i] = i < nb ? ((b << 4) | 0) : -1;  // KIN(b, step 0)
-  }
-  for (int b = x + 8 * (int)threadIdx.x; b < n_blocks; b += 8 * (int)blockDim.x) f.cnt[b] = 0;
-  if (threadIdx.x == 0) {
-    ctl[0] = 0;        // head
-    ctl[1] = 64 * nb;  // tail
-    ctl[2] = per_step * f.n_steps;
-    if (x == 0) f.ctl[256] = 0;
-  }
-}
-
-__global__ __launch_bounds__(64, RX_FLOW_MINW) void k_flow(const rx_kargs* args, rx_flow f) {
-  const int lane = threadIdx.x & 63;
-  const rx_kargs& a0 = *(const rx_kargs*)(rx_ckargs)args;
-  const int x = xcc_id();
-  int32_t* q = f.q + (size_t)x * f.cap;
-  int32_t* ctl = f.ctl + 32 * x;
-  const int nb = a0.n_dyn_waves, R = a0.n_sensors;
-  const int total = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const unsigned long long prof_t0 = prof_start(a0);
-  __shared__ int32_t tcnt[kTaskSectors];
-  __shared__ int32_t tstage[64 * 16];
-  for (;;) {
-    // pop: one full-wave atomic (64 per entry), the old value read back into an SGPR
-    const int idx = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 0, 1)) >> 6;
-    if (idx >= total) break;
-    int code = -1;
-    for (int spin = 0; spin < RX_FLOW_SPIN_MAX; ++spin) {
-      code = __builtin_amdgcn_readfirstlane(__hip_atomic_load(q + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (code >= 0) break;
-      __builtin_amdgcn_s_sleep(RX_FLOW_SLEEP);
-    }
-    if (code < 0) {  // the producer never pushed: give up (recorded, the host raises)
-      if (lane == 0) atomicOr(f.ctl + 256, 1);
-      break;
-    }
-    const int kind = code & 15, sb = code >> 4, s = sb / nb, b = sb - s * nb;
-    const rx_kargs& as = *(const rx_kargs*)((rx_ckargs)args + s);
-    typedef const __attribute__((address_space(4))) int32_t* rx_cip;
-    const rx_cip dwp = (rx_cip)(const int32_t*)(as.dyn_waves + b);
-    const int n_tasks = dwp[3] * R, n_cls = (n_tasks + 63) >> 6, perm_start = dwp[1];
-    if (kind == 0) {
-      // ---- KIN(b, s): kinematics + the block's ray-task sort, then push REWARD + the classes
-      tcnt[lane] = 0;
-      double ang[1], ep[3] = {0.0, 0.0, 0.0};
-      int e = -1;
-      dyn1_env<1, RX_PART_KIN, true>(as, b, ang, e, ep);
-      sort_block_tasks<1, true>(as, perm_start, e, ang, tcnt, tstage);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int n = 1 + n_cls;
-      const int slot = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 1, n)) >> 6;
-      if (lane < n) {  // REWARD first, then the classes centre-first (longest chains first)
-        const int kd = lane == 0 ? 1 : 2 + win_class(lane, n_cls);
-        __hip_atomic_store(q + slot + lane, (sb << 4) | kd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      if (kind == 1) {
-        double ang[1], ep[3] = {0.0, 0.0, 0.0};
-        int e = -1;
-        dyn1_env<1, RX_PART_REWARD, true>(as, b, ang, e, ep);
-        add_episode_stats(as, ep);
-      } else {
-        const int j = kind - 2;
-        const rx_wave rw{dwp[0], perm_start, 64 * j, min(64, n_tasks - 64 * j)};
-        rays_wave<1, 1, true>(as, rw, as.tasks_out + (size_t)perm_start * R, b);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // arrival; the step's last one queues KIN(b, s + 1)
-      const int old = __builtin_amdgcn_readfirstlane(atomicAdd(f.cnt + b, 1)) >> 6;
-      if (old == (s + 1) * (1 + n_cls) - 1 && s + 1 < f.n_steps) {
-        const int slot = __builtin_amdgcn_readfirstlane(atomicAdd(ctl + 1, 1)) >> 6;
-        if (lane == 0)
-          __hip_atomic_store(q + slot, ((sb + nb) << 4) | 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  prof_end(a0, (int)blockIdx.x, prof_t0);
 }
 
 // ============================================================ k_rollout
@@ -2901,11 +2485,7 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
-    if (a->kin_sort && a->tasks_out && a->n_sensors <= 16)  // sorting launches: the 4-wave ranking
-      hipLaunchKernelGGL(k_kin1p, dim3(a->n_dyn_waves), dim3(64 * kKinWaves), 0, s, *a);
-    else
-      hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 1, 1), s,
-                         *a);
+    hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN>), dim3(a->n_dyn_waves), dim3(64), task_sort_lds_bytes(a, 1, 1), s, *a);
     return (int)hipGetLastError();
   }
   // RX_SPLIT_REWARD: the REWARD half alone; RX_SPLIT_REWARD_RAYS: both halves in one launch
@@ -2949,45 +2529,6 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
     else
       hipLaunchKernelGGL(k_rays<2>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
   }
-  return (int)hipGetLastError();
-}
-
-// Dynamic LDS requested by every k_window workgroup beyond its static rows: it
-// only caps the workgroups a CU admits (the hardware packs workgroups onto CUs as
-// long as resources allow, it does not spread them evenly).  A/B knob.
-#ifndef RX_WIN_LDS_PAD
-#define RX_WIN_LDS_PAD 0
-#endif
-extern "C" int rx_window_capacity(int device) {
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_window, 64 * kWinWaves, RX_WIN_LDS_PAD) != hipSuccess)
-    return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-  return per_cu * cus;
-}
-
-extern "C" int rx_launch_window(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last,
-                                rx_kargs* args, hipStream_t s) {
-  if (n_steps < 1 || n_steps > RX_WIN_MAX_STEPS) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
-  hipLaunchKernelGGL(k_window, dim3(a->n_dyn_waves), dim3(64 * kWinWaves), RX_WIN_LDS_PAD, s, (const rx_kargs*)args,
-                     n_steps);
-  return (int)hipGetLastError();
-}
-
-extern "C" int rx_flow_capacity(int device) {
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_flow, 64, 0) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-  return per_cu * cus;
-}
-
-extern "C" int rx_launch_flow(const rx_kargs* a, const rx_io_strides* st, int n_steps, int keys_last, rx_kargs* args,
-                              const rx_flow* f, int grid, hipStream_t s) {
-  if (n_steps < 1 || n_steps > RX_WIN_MAX_STEPS || f->n_steps != n_steps) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_window_args, dim3(1), dim3(RX_WIN_MAX_STEPS), 0, s, *a, *st, n_steps, keys_last, args);
-  hipLaunchKernelGGL(k_flow_init, dim3(8), dim3(256), 0, s, a->dyn_waves, a->n_dyn_waves, a->n_sensors, *f);
-  hipLaunchKernelGGL(k_flow, dim3(grid), dim3(64), 0, s, (const rx_kargs*)args, *f);
   return (int)hipGetLastError();
 }
 

@@ -1017,138 +1017,11 @@ struct norm_args {
   const double* lr;
 };
 
-// FUSED (rx_ppo_minibatch_update): the clip + Adam step rides on the same
-// launch, each block stepping its own 64 parameters.  Every block stores its
-// per-tensor norm partials with sc1 stores, loads its parameters' Adam state,
-// waits vmcnt(0) on its storing wave and arrives on an agent-scope counter.
-// The last arrival (told by the value its add returned) folds the partials into
-// the clip coefficient in k_adam_apply's order, runs the KL check and the step
-// bump (k_ppo_reduce's block 0 wave 1 in the unfused launch), publishes
-// {coef, go, step_size, bc2_sqrt} with sc1 stores, waits vmcnt(0) and raises
-// the generation word; every other block's wave 0 polls that word (sc1 loads,
-// s_sleep), loads the record with sc1 loads and applies rx_adam_elem to its
-// 64 entries -- MI355X_MICROARCH.md "Valid forms", table row 1, both ways.
-// The poll needs every block resident at once: 1,024-thread blocks at one per
-// CU (<= 173 of them for either policy on 256 CUs); a poll that outlives
-// kFusedSpin sleeps counts an error in the record and leaves its block's
-// parameters unstepped instead of hanging (rx_ppo_tail_errors).
-// Same arithmetic as k_ppo_reduce + k_adam_apply: bit-identical results.
-struct fused_adam {
-  float* p;
-  float* m;
-  float* v;
-  unsigned* ctl;  // RX_PPO_TAIL_CTL words in norm.ws after Adam's scalars (zero-filled once)
-};
-// ctl words: arrival counter (cumulative, 64 per block), published generation,
-// the record (coef, go, step_size, bc2_sqrt), spin timeouts
-enum { kCtlArrive = 0, kCtlGen = 1, kCtlCoef = 2, kCtlGo = 3, kCtlStep = 4, kCtlBc2 = 5, kCtlErr = RX_PPO_TAIL_ERR };
-static_assert(kCtlErr > kCtlBc2 && kCtlErr < RX_PPO_TAIL_CTL, "rx.h control block layout");
-constexpr int kFusedSpin = 1 << 20;
-
-template <class T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The last block: clip coefficient, KL check, step bump -> the published record.
-__device__ __forceinline__ void fused_last_block(const double* __restrict__ klp, int n_wg, int mb, float kl_target,
-                                                 uint8_t* stop, float* kl_at_stop, const norm_args& norm,
-                                                 const fused_adam& fa, unsigned gen, float* rec) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int n_t = norm.cfg.n_tensors, nb = gridDim.x;
-  __shared__ float norms[RX_ADAM_MAX_TENSORS];
-  // every load goes out before the first wait: the clip-norm partials (sc1: stored by
-  // the other blocks of this launch), the KL partials, the step count and lr
-  const bool clip = norm.cfg.max_grad_norm > 0.0;
-  const int u = tid >> 4, j = tid & 15;
-  int b_lo = 0, b_hi = -1;
-  {  // the wave's 4 tensors' offsets through scalar loads (a per-lane index would be a vector load + wait)
-    const int u0 = 4 * __builtin_amdgcn_readfirstlane(tid >> 6);
-    int64_t ob[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) ob[k] = norm.cfg.offsets[min(u0 + k, n_t)];
-    const int sub = u & 3;
-    const int64_t lo = sub == 0 ? ob[0] : sub == 1 ? ob[1] : sub == 2 ? ob[2] : ob[3];
-    const int64_t hi = sub == 0 ? ob[1] : sub == 1 ? ob[2] : sub == 2 ? ob[3] : ob[4];
-    if (clip && u < n_t && hi > lo) b_lo = (int)(lo / RX_ADAM_NORM_ELEMS), b_hi = (int)((hi - 1) / RX_ADAM_NORM_ELEMS);
-  }
-  float w[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) w[k] = ld_sc1(norm.ws + (size_t)min(b_lo + j + 16 * k, nb - 1) * n_t + (u < n_t ? u : 0));
-  if ((tid >> 6) == 15) {  // approx_kl (agent/ppo.py:178-182), k_ppo_reduce's block 0 wave 1 in the same order
-    const float step0 = *norm.step;
-    const double lr = *norm.lr;
-    double k = 0.0;
-    for (int w0 = lane; w0 < n_wg; w0 += 64 * 8) {
-      double kv[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) kv[q] = klp[min(w0 + 64 * q, n_wg - 1)];
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (w0 + 64 * q < n_wg) k += kv[q];  // w = lane, lane + 64, ...
-    }
-    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o, 64);
-    const float kl = (float)(k / (double)mb);
-    if (lane == 0) {
-      if (kl > kl_target) {
-        *kl_at_stop = kl;
-        *stop = 1;
-        rec[1] = 0.0f;
-      } else {
-        const float st = step0 + 1.0f;  // the Adam step this minibatch takes
-        *norm.step = st;
-        rx_adam_scalars(norm.cfg, st, lr, rec + 2);
-        norm.ws[(size_t)nb * n_t] = rec[2];
-        norm.ws[(size_t)nb * n_t + 1] = rec[3];
-        rec[1] = 1.0f;
-      }
-    }
-  }
-  // clip_grad_norm_: 16-lane group u folds tensor u's partials in k_adam_apply's order
-  if (clip) {
-    float l = 0.0f;
-    for (int b0 = b_lo + j; b0 <= b_hi; b0 += 16 * 8) {  // (the first 8 are in w: tensors of <= 128 blocks)
-      if (b0 != b_lo + j) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = ld_sc1(norm.ws + (size_t)min(b0 + 16 * k, nb - 1) * n_t + u);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) l += b0 + 16 * k <= b_hi ? w[k] : 0.0f;
-    }
-    for (int o = 1; o < 16; o <<= 1) l += __shfl_xor(l, o, 16);
-    if (j == 0 && u < n_t) norms[u] = sqrtf(l);
-  }
-  __syncthreads();
-  if (tid < 64) {  // wave 0: the coefficient, then the record and the generation word
-    float coef = 1.0f;
-    if (clip) {
-      float tot2 = 0.0f;
-      for (int t = 0; t < n_t; ++t) tot2 += norms[t] * norms[t];
-      const float total = sqrtf(tot2);
-      coef = fminf((float)norm.cfg.max_grad_norm / (total + 1e-6f), 1.0f);
-    }
-    rec[0] = coef;
-    if (tid == 0) {
-      st_sc1(reinterpret_cast<float*>(fa.ctl + kCtlCoef), coef);
-      st_sc1(reinterpret_cast<float*>(fa.ctl + kCtlGo), rec[1]);
-      st_sc1(reinterpret_cast<float*>(fa.ctl + kCtlStep), rec[2]);
-      st_sc1(reinterpret_cast<float*>(fa.ctl + kCtlBc2), rec[3]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_sc1(fa.ctl + kCtlGen, gen + 1u);
-    }
-  }
-}
-
-template <bool FUSED>
 __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
                                                      const double* __restrict__ klp, int n_wg, int P, int Pp, int mb,
                                                      float kl_target, float scale, float* grad, uint8_t* stop,
                                                      float* kl_at_stop, float* kl_out, const norm_args* norm_p,
-                                                     norm_args norm, fused_adam fa) {
+                                                     norm_args norm) {
   // tested after the partial loads are issued (one round trip, not two), and made
   // block-uniform through LDS: block 0's wave 1 may raise *stop during this very
   // launch, so two waves of a later block could read different values
@@ -1157,18 +1030,6 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
   __shared__ int s_stopped;
   const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
   const int p4 = blockIdx.x * (4 * kRedCols) + c * 4;  // first of this thread's 4 parameters
-  float pm[4] = {}, pv[4] = {}, pp[4] = {};  // FUSED: the Adam state of the lane's 4 parameters, loaded first
-  if constexpr (FUSED) {
-    if (threadIdx.x < kRedCols) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = min(p4 + q, P - 1);
-        pm[q] = fa.m[i];
-        pv[q] = fa.v[i];
-        pp[q] = fa.p[i];
-      }
-    }
-  }
   float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (p4 < Pp)
     for (int w0 = sl; w0 < n_wg; w0 += kRedBatch * kRedSlices) {
@@ -1216,8 +1077,7 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
       t.w += v.w;
     }
     o4[0] = t.x, o4[1] = t.y, o4[2] = t.z, o4[3] = t.w;
-    if constexpr (!FUSED)  // (FUSED: stored clipped, after the hand-off)
-      for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o4[q] * scale;
+    for (int q = 0; q < 4 && p4 + q < P; ++q) grad[p4 + q] = o4[q] * scale;
     if (norm_p) {  // per-tensor sums of squares of this block's 64 entries, lanes 0..15 in a fixed tree
       const int nt = norm.cfg.n_tensors;
       const int64_t b0 = (int64_t)blockIdx.x * 4 * kRedCols, b1 = b0 + 4 * kRedCols;
@@ -1231,62 +1091,9 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
           }
           for (int off = 1; off < kRedCols; off <<= 1) sq += __shfl_xor(sq, off, kRedCols);
         }
-        if (threadIdx.x == 0) {
-          if constexpr (FUSED)
-            st_sc1(norm.ws + (size_t)blockIdx.x * nt + u, sq);
-          else
-            norm.ws[(size_t)blockIdx.x * nt + u] = sq;
-        }
+        if (threadIdx.x == 0) norm.ws[(size_t)blockIdx.x * nt + u] = sq;
       }
     }
-  }
-  if constexpr (FUSED) {
-    __shared__ unsigned s_arrive;
-    __shared__ float rec[4];  // coef, go, step_size, bc2_sqrt
-    const int lane = threadIdx.x & 63;
-    if (threadIdx.x < 64) {  // the storing wave: its stores drained, then the arrival
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // a full-wave add (the atomic optimizer folds it into one add of 64): the counter
-      // advances 64 per block and old >> 6 is the block's arrival index
-      const unsigned old = __builtin_amdgcn_readfirstlane(atomicAdd(fa.ctl + kCtlArrive, 1u));
-      if (lane == 0) s_arrive = old >> 6;
-    }
-    __syncthreads();
-    const unsigned arrival = s_arrive, gen = arrival / gridDim.x;
-    float coef, go, step_size, bc2_sqrt;
-    if (arrival % gridDim.x == gridDim.x - 1) {
-      fused_last_block(klp, n_wg, mb, kl_target, stop, kl_at_stop, norm, fa, gen, rec);
-      __syncthreads();
-      if (threadIdx.x >= 64) return;
-      coef = rec[0], go = rec[1], step_size = rec[2], bc2_sqrt = rec[3];
-    } else {
-      if (threadIdx.x >= 64) return;
-      int it = 0;
-      while ((int)(__builtin_amdgcn_readfirstlane(ld_sc1(fa.ctl + kCtlGen)) - (int)(gen + 1u)) < 0) {
-        if (++it > kFusedSpin) {  // never on a device the launch has to itself: count it, step nothing
-          if (lane == 0) atomicAdd(fa.ctl + kCtlErr, 1u);
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const float* r = reinterpret_cast<const float*>(fa.ctl);  // the record: sc1 loads after the poll matched
-      coef = ld_sc1(r + kCtlCoef), go = ld_sc1(r + kCtlGo), step_size = ld_sc1(r + kCtlStep);
-      bc2_sqrt = ld_sc1(r + kCtlBc2);
-    }
-    if (threadIdx.x >= kRedCols || go == 0.0f) return;  // KL early stop: nothing stepped
-    const float w1 = (float)(1.0 - norm.cfg.beta1), fb2 = (float)norm.cfg.beta2, w2 = (float)(1.0 - norm.cfg.beta2);
-    const float eps = (float)norm.cfg.eps;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (p4 + q >= P) break;
-      float g = o4[q] * scale;
-      rx_adam_elem(g, pm[q], pv[q], pp[q], coef, w1, fb2, w2, eps, step_size, bc2_sqrt);
-      grad[p4 + q] = g;
-      fa.m[p4 + q] = pm[q];
-      fa.v[p4 + q] = pv[q];
-      fa.p[p4 + q] = pp[q];
-    }
-    return;
   }
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
@@ -1519,8 +1326,7 @@ extern "C" int rx_ppo_reduce_blocks(int obs_dim) {
 
 extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uint8_t* stop, float* kl_at_stop,
                                   float* kl_out, float* partial, double* klp, float* grad, hipStream_t s,
-                                  const rx_adam_config* cfg, float* norm_ws, float* step, const double* lr,
-                                  const rx_adam_tail* fused) {
+                                  const rx_adam_config* cfg, float* norm_ws, float* step, const double* lr) {
   const int rp = rows_per_wg(b->mb);
   const int n_wg = (b->mb + rp - 1) / rp;
   ppo_args a{*b, m, rp, stop, klp};
@@ -1550,15 +1356,8 @@ extern "C" int rx_launch_ppo_grad(const rx_ppo_batch* b, int m, float scale, uin
     np = &na;  // only its non-nullness reaches the device: the struct travels by value
   }
   const int nb = rx_ppo_reduce_blocks(b->obs_dim);
-  if (fused) {  // control words after the partials and Adam's two scalars (rx_ppo_update_workspace_floats)
-    const fused_adam fa{fused->p, fused->m, fused->v,
-                        reinterpret_cast<unsigned*>(norm_ws + (size_t)nb * cfg->n_tensors + 2)};
-    hipLaunchKernelGGL(k_ppo_reduce<true>, dim3(nb), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb, b->kl_target,
-                       scale, grad, stop, kl_at_stop, kl_out, np, na, fa);
-  } else {
-    hipLaunchKernelGGL(k_ppo_reduce<false>, dim3(nb), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb,
-                       b->kl_target, scale, grad, stop, kl_at_stop, kl_out, np, na, fused_adam{});
-  }
+  hipLaunchKernelGGL(k_ppo_reduce, dim3(nb), dim3(1024), 0, s, partial, klp, n_wg, P, Pp, b->mb, b->kl_target, scale,
+                     grad, stop, kl_at_stop, kl_out, np, na);
   return (int)hipGetLastError();
 }
 

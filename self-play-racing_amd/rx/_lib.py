@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede librx: shared HIP runtime, see above)
 
 from . import _build
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 RX_EP_SHARDS = 64  # rx_io.ep_stats rows (include/rx.h)
 RX_OK, RX_EINVAL, RX_EHIP, RX_ENOMEM, RX_ESTATE = 0, -1, -2, -3, -4
 RX_F_CRASHED, RX_F_FINISHED, RX_F_CP25, RX_F_CP50, RX_F_CP75, RX_F_HAS_CRASHED = 1, 2, 4, 8, 16, 32
@@ -32,8 +32,8 @@ EXPORTS = ("rx_last_error", "rx_abi_version", "rx_create", "rx_destroy", "rx_sen
            "rx_profile", "rx_profile_read", "rx_ppo_update_workspace_floats", "rx_ppo_minibatch_update", "rx_env_order",
            "rx_state_import", "rx_state_export", "rx_schedule",
            "rx_ppo_adv_workspace_doubles", "rx_ppo_adv_stats_ws", "rx_profile_waves", "rx_ray_waves", "rx_ray_tasks", "rx_set_start_draws",
-           "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps", "rx_flow_errors")
-RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward", "k_window")
+           "rx_rollout_steps", "rx_selfplay_rollout_steps", "rx_steps")
+RX_KERNEL_NAMES = ("k_dyn", "k_rays", "k_kin1", "k_step2", "k_step2_reward")
 ADAM_MAX_TENSORS = 32
 RX_PHASE_DYNAMICS, RX_PHASE_RAYS = 1, 2
 RX_PREC_FP32, RX_PREC_BF16 = 0, 1
@@ -48,18 +48,17 @@ class RxConfig(ctypes.Structure):
                 ("ray_order", ctypes.c_int32), ("cull_super", ctypes.c_int32)] + \
                [(k, ctypes.c_int32) for k in ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window",
                                                "seg_filter", "box_quadrants", "ray_dispatch", "ray_tail",
-                                               "ray_tail_lpr", "task_sort", "window", "kin_sort")]
+                                               "ray_tail_lpr", "task_sort", "lane_tracks", "reserved0")]
 
 
-# rx_config launch-schedule fields (ABI v17, v19, v20, v21): 0 = auto, -1 = off / none (include/rx.h).
+# rx_config launch-schedule fields (ABI v17, v19, v20, v23): 0 = auto, -1 = off / none (include/rx.h).
 # Scheduling only: every value gives bit-identical results.
-RX_PPO_TAIL_CTL, RX_PPO_TAIL_ERR = 8, 6  # rx_ppo_minibatch_update's control block at the end of adam_ws (rx.h)
 SCHEDULE_W = 18  # rx_schedule: resolved schedule (include/rx.h)
 SCHEDULE_KEYS = ("split", "wide", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
                  "dyn_waves", "ray_waves", "ray_dispatch", "ray_tail", "ray_tail_lpr", "ray_tail_from", "task_sort",
-                 "window", "dyn_calls", "kin_sort")
+                 "lane_tracks", "dyn_calls", "reserved")
 SCHED_FIELDS = ("split", "wide_n", "dyn_lpe", "ray_lpr", "reward_lpe", "argmin_window", "seg_filter", "box_quadrants",
-                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "window", "kin_sort")
+                "ray_dispatch", "ray_tail", "ray_tail_lpr", "task_sort", "lane_tracks")
 
 
 STATE_FIELDS = ("x", "y", "angle", "vx", "vy", "progress", "last_progress", "last_steering", "finished_step", "flags",
@@ -152,7 +151,6 @@ def load(build_if_missing=True):
     L.rx_step.argtypes = [_P, ctypes.POINTER(RxIO), _P]
     L.rx_step_phases.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, _P]
     L.rx_steps.argtypes = [_P, ctypes.POINTER(RxIO), ctypes.c_int32, ctypes.POINTER(RxIOStrides), _P]
-    L.rx_flow_errors.argtypes = [_P, _P]
     gae_args = [ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, _P, _P, _P]
     L.rx_gae.argtypes = gae_args
     L.rx_gae_scan.argtypes = gae_args

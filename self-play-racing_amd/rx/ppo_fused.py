@@ -112,16 +112,6 @@ class FusedMinibatchGrad:
             _lib.ptr(f.flat_grad), _lib.ptr(f.exp_avg), _lib.ptr(f.exp_avg_sq), _lib.ptr(f.step_t), _lib.ptr(f.lr_t),
             _lib.ptr(stop), _lib.ptr(kl_at_stop), _lib.ptr(ws), _lib.stream_ptr(stream)), "rx_ppo_minibatch_update")
 
-    def tail_errors(self):
-        """Workgroups of the fused update launch that gave up waiting for the
-        published clip coefficient (rx.h RX_PPO_TAIL_ERR; 0 unless two updates
-        shared the device at once).  Synchronises the device."""
-        ws = self.__dict__.get("adam_ws")
-        if ws is None:
-            return 0
-        ctl = ws[-_lib.RX_PPO_TAIL_CTL:].view(torch.int32)
-        return int(ctl[_lib.RX_PPO_TAIL_ERR])
-
     def epoch(self, stop, kl_at_stop, stats=True):
         """All minibatch steps of one epoch over the current perm (``stats``:
         its advantage statistics first; False when the caller has already put

@@ -475,8 +475,7 @@ class RacingVectorEnv:
         ``obs_out`` / ``reward_out`` / ``done_out``: None = the env's own rows (each
         step overwrites them: they end with the last step's outputs), or [K, ...]
         buffers whose row k receives step k.  Returns the last step's (obs, reward,
-        done_f32).  Where the schedule allows (single-agent split step at one lane per
-        ray), the steps between two spatial re-sorts run as ONE k_window launch."""
+        done_f32)."""
         dev_idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         on_dev = lambda t: t.is_cuda and t.device.index == dev_idx  # noqa: E731  ("cuda" == "cuda:0")
         if not isinstance(actions, torch.Tensor) or not on_dev(actions) or \

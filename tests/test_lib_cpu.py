@@ -100,11 +100,14 @@ def test_schedule_config_is_validated_and_the_library_reads_no_environment():
     base = [16, 1, 11, 3000, 0, 0, 0, 1.0471975511965976, 8.0, 8, 16, 2, 8]
     bad = {"split": 2, "wide_n": -2, "dyn_lpe": 3, "ray_lpr": 8, "reward_lpe": 64, "argmin_window": 33,
            "seg_filter": 5, "box_quadrants": -3, "ray_dispatch": 4, "ray_tail": 17, "ray_tail_lpr": 3,
-           "task_sort": 17, "window": 3, "kin_sort": 2}
+           "task_sort": 17, "lane_tracks": 2}
     for k, v in bad.items():
         sched = [v if f == k else 0 for f in _lib.SCHED_FIELDS]
         assert L.rx_create(_lib.RxConfig(*base, *sched), h) == _lib.RX_EINVAL, k
         assert k.encode() in L.rx_last_error(), (k, L.rx_last_error())
+    # ABI v23: the dropped kin_sort slot is reserved0 and must be 0
+    assert L.rx_create(_lib.RxConfig(*base, *[0] * len(_lib.SCHED_FIELDS), 1), h) == _lib.RX_EINVAL
+    assert b"reserved0" in L.rx_last_error()
     two = list(base)
     two[1] = 2
     assert L.rx_create(_lib.RxConfig(*two, *[2 if f == "dyn_lpe" else 0 for f in _lib.SCHED_FIELDS]), h) \
@@ -117,8 +120,7 @@ def test_schedule_config_is_validated_and_the_library_reads_no_environment():
         for k, vals in {"split": (-1, 1), "wide_n": (-1, 5), "dyn_lpe": (1, 2, 4, 64), "ray_lpr": (1, 2, 4),
                         "reward_lpe": (1, 2, 4), "argmin_window": (-1, 1, 32), "seg_filter": (-1, 1),
                         "box_quadrants": (-1, 1), "ray_dispatch": (-1, 1, 2, 3), "ray_tail": (-1, 1, 16),
-                        "ray_tail_lpr": (2, 4), "task_sort": (1, 2, 16), "window": (-1, 1, 2),
-                        "kin_sort": (-1, 1)}.items():
+                        "ray_tail_lpr": (2, 4), "task_sort": (1, 2, 16), "lane_tracks": (-1, 1)}.items():
             for v in vals:
                 sched = [v if f == k else 0 for f in _lib.SCHED_FIELDS]
                 assert L.rx_create(_lib.RxConfig(*base, *sched), h) != _lib.RX_EINVAL, (k, v)
