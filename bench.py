@@ -217,20 +217,10 @@ def stress_pool(n, seed=2):
     return pool, widths
 
 
-def stress_leg(dev, n, steps, untimed, sched, profile_steps=32, seed=2):
-    """The headline workload (configs[2]: n single-agent envs, uniform random actions
-    resident in HBM, next-step autoreset, one HIP graph of `steps` production steps)
-    on the all-distinct-track pool of stress_pool: every env its own track slot."""
-    from rx.track import TrackSet
-    from rx.vector_env import RacingVectorEnv
-    t0 = time.perf_counter()
-    pool, widths = stress_pool(n, seed)
-    ts = TrackSet.build(pool, widths)
-    build_s = time.perf_counter() - t0
-    env = RacingVectorEnv(pool, widths, n_agents=1, n_sensors=11, device=dev, autoreset="next_step", track_set=ts,
-                          sched=sched)
-    n_slots = len(env.tracks)
-    P = np.bincount([len(c) for c in pool], minlength=15)[10:15]
+def _stress_run(env, dev, n, steps, untimed, profile_steps):
+    """One env handle through the headline protocol: untimed steps, a HIP graph of
+    `steps` production steps captured and replayed once untimed, one timed replay,
+    then instrumented steps (kernel durations, wave slots) and counter steps."""
     g = torch.Generator(device=dev).manual_seed(4321)
     bank = max(1, min(steps + untimed + profile_steps, (256 << 20) // (8 * n)))
     acts = torch.rand((bank, n, 2), device=dev, generator=g) * torch.tensor([2.0, 1.0], device=dev) + \
@@ -274,14 +264,12 @@ def stress_leg(dev, n, steps, untimed, sched, profile_steps=32, seed=2):
     cnt = env.read_counters()
     env.enable_counters(False)
     sch = env.schedule()
-    env.close()
     del graph
     step2 = prof.get("k_step2", (float("nan"), 0))[0]
     kin = prof.get("k_kin1", (float("nan"), 0))[0]
     gbs = STEP2_BYTES_PER_ENV * n / (step2 * 1e-3) / 1e9
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "envs": n, "track_slots": n_slots,
-            "control_points_hist_P10_to_P14": P.tolist(), "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
-            "episodes_ended_in_timed_region": ep[2], "table_build_s": round(build_s, 2),
+    return {"value": round(n * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+            "episodes_ended_in_timed_region": ep[2], "lane_tracks": sch["lane_tracks"],
             "kernels_ms": {k: round(v[0], 5) for k, v in prof.items()},
             "roofline": {"bound": "hbm", "kernel": "k_step2", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "bytes_per_env": STEP2_BYTES_PER_ENV,
@@ -290,12 +278,44 @@ def stress_leg(dev, n, steps, untimed, sched, profile_steps=32, seed=2):
             "wave_slots": waves,
             "executed_work": {"ray_box_tests_per_ray_wave": round(cnt["ray_chunk_tests"] / (8 * sch["ray_waves"]), 2),
                               "ray_leaf_scans_per_env_step": round(cnt["ray_chunks_scanned"] / (8 * n), 3),
-                              "wp_leaf_scans_per_env_step": round(cnt["wp_chunks_scanned"] / (8 * n), 3)},
-            "schedule": sch,
-            "workload": f"configs[2] on the stress pool: np.random.seed({seed}); gen_tracks({n}, seed=None) "
+                              "wp_leaf_scans_per_env_step": round(cnt["wp_chunks_scanned"] / (8 * n), 3),
+                              "counted": "per lane" if sch["lane_tracks"] else "per wave"},
+            "schedule": sch}
+
+
+def stress_leg(dev, n, steps, untimed, sched, profile_steps=32, seed=2, compare=True):
+    """The headline workload (configs[2]: n single-agent envs, uniform random actions
+    resident in HBM, next-step autoreset, one HIP graph of `steps` production steps)
+    on the all-distinct-track pool of stress_pool: every env its own track slot.  The
+    line's numbers come from the schedule rx_assign picks (lane-varying slots);
+    ``compare`` also times the slot-grouped schedule (lane_tracks = -1: one env per
+    wave) on the same pool, the form the kernels had before ABI v23."""
+    from rx.track import TrackSet
+    from rx.vector_env import RacingVectorEnv
+    t0 = time.perf_counter()
+    pool, widths = stress_pool(n, seed)
+    ts = TrackSet.build(pool, widths)
+    build_s = time.perf_counter() - t0
+    P = np.bincount([len(c) for c in pool], minlength=15)[10:15]
+    env = RacingVectorEnv(pool, widths, n_agents=1, n_sensors=11, device=dev, autoreset="next_step", track_set=ts,
+                          sched=sched)
+    n_slots = len(env.tracks)
+    res = _stress_run(env, dev, n, steps, untimed, profile_steps)
+    env.close()
+    if compare:
+        env = RacingVectorEnv(pool, widths, n_agents=1, n_sensors=11, device=dev, autoreset="next_step",
+                              track_set=ts, sched=dict(sched, lane_tracks=-1))
+        r2 = _stress_run(env, dev, n, steps, untimed, profile_steps)
+        env.close()
+        res["slot_grouped"] = {k: r2[k] for k in ("value", "ms_per_step", "kernels_ms", "wave_slot_utilisation",
+                                                  "roofline", "executed_work")}
+    res.update(unit="env-steps/s", envs=n, track_slots=n_slots, control_points_hist_P10_to_P14=P.tolist(),
+               steps=steps, table_build_s=round(build_s, 2),
+               workload=f"configs[2] on the stress pool: np.random.seed({seed}); gen_tracks({n}, seed=None) "
                         "(track.py:47-56, no per-track reseed), widths randint(6, 10): every env its own track; "
                         "uniform random actions resident in HBM, next-step autoreset, one HIP graph replay of "
-                        f"{steps} steps after {untimed} + {steps} untimed"}
+                        f"{steps} steps after {untimed} + {steps} untimed")
+    return res
 
 
 def gae_roofline(n_envs, dev, T=512, reps=20):

@@ -107,6 +107,8 @@ struct rx_env {
   int32_t ray_dispatch = RX_RAY_DISPATCH;  // resolved class order of the ray-wave table (rx_config.ray_dispatch)
   int32_t ray_tail = 0, ray_tail_lpr = 2;  // tail classes cast at ray_tail_lpr lanes per ray (0 = none)
   int32_t task_sort = 1;                   // ray-task direction sort every task_sort dynamics launches
+  int32_t lane_tracks = 0;                 // lane-varying slots (rx_config.lane_tracks, rx_assign's choice)
+  DevBuf<int32_t> pos_slot;                // with lane_tracks: [N] slot of the env at each position
   DevBuf<uint8_t> policy_frag;  // the bf16 rollout's operand fragments of both trunks (k_policy_frag, rx_rollout_steps)
   int32_t ray_tail_from = -1;              // first ray wave of the tail (-1 = none)
   DevBuf<double> rel_angles;
@@ -402,7 +404,7 @@ int rx_schedule(const rx_env* h, int32_t* out) {
                                     h->argmin_window, h->cfg.seg_filter >= 0 ? 1 : 0,
                                     h->cfg.box_quadrants >= 0 ? 1 : 0, h->n_dyn_waves, h->n_ray_waves,
                                     h->ray_dispatch, h->ray_tail, h->ray_tail_lpr, h->ray_tail_from,
-                                    h->task_sort, 0, (int32_t)h->dyn_calls, 0};
+                                    h->task_sort, h->lane_tracks, (int32_t)h->dyn_calls, 0};
   std::copy(v, v + RX_SCHEDULE_W, out);
   return RX_OK;
 }
@@ -418,6 +420,7 @@ int rx_destroy(rx_env* h) {
     b->release();
   h->cs_scratch.release();
   h->policy_frag.release();
+  h->pos_slot.release();
   h->prof_buf.release();
   h->resets.release();
   h->draw_rank.release();
@@ -524,10 +527,35 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
   h->ray_tail = c.ray_tail == 0 ? RX_RAY_TAIL : (c.ray_tail < 0 ? 0 : c.ray_tail);
   if (h->cfg.ray_order != 2 || h->ray_lpr != 1 || h->ray_dispatch == 0 || h->dyn_lpe == 64) h->ray_tail = 0;
   h->ray_tail_from = -1;
-  const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
   std::vector<int32_t> slot_n(h->n_tracks, 0);
   for (int e = 0; e < N; ++e) ++slot_n[track_of_env[e]];
-  int g0 = 0;
+  // Lane-varying track slots (ABI v23): grouping envs by slot gives every slot
+  // ceil(n_k / 64) dynamics waves; with many distinct slots (gen_tracks(N, seed=None): one env
+  // each) those waves hold a lane or two.  Auto rule: take waves of 64 consecutive positions of
+  // ANY slots (per-lane track loads) when the grouping would need more than twice ceil(N / 64)
+  // waves.  Single-agent envs at one lane per env (the split step or the one-kernel k_dyn1<1>);
+  // it implies one lane per ray and per REWARD env and no ray-task sort or spatial re-sort.
+  {
+    long long grouped = 0;
+    for (int k = 0; k < h->n_tracks; ++k) grouped += (slot_n[k] + 63) / 64;
+    const long long full = (N + 63) / 64;
+    const bool can = A == 1 && h->dyn_lpe == 1;
+    h->lane_tracks = can && c.lane_tracks >= 0 && (c.lane_tracks == 1 || grouped > 2 * full) ? 1 : 0;
+  }
+  if (h->lane_tracks) {
+    h->ray_lpr = 1;
+    h->reward_lpe = 1;
+    h->ray_dispatch = 0;
+    h->ray_tail = 0;
+  }
+  const int tpw = 64 / h->ray_lpr;  // ray tasks per wave
+  int g0 = h->lane_tracks ? N : 0;
+  for (int ps = 0; h->lane_tracks && ps < N; ps += 64) {  // 64 consecutive positions, (env, agent, ray) tasks
+    const int cnt = std::min(64, N - ps), nt = cnt * A * R;
+    dyn.push_back(rx_wave{-1, ps, 0, cnt});
+    for (int j = 0; j < nt; j += 64) ray.push_back(rx_wave{-1, ps, j, std::min(64, nt - j)});
+    ray_groups.push_back((int)ray.size());
+  }
   while (g0 < N) {
     const int k = track_of_env[perm[g0]];
     int g1 = g0;
@@ -554,7 +582,7 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     }
     g0 = g1;
   }
-  if (h->cfg.ray_order >= 1) {
+  if (h->cfg.ray_order >= 1 || h->lane_tracks) {
     // XCD-aware placement: workgroups are dealt round-robin over the 8 XCDs
     // (MI355X_MICROARCH.md, workgroup dispatch), and every wave of one 64-env
     // block writes into the same obs rows, so the (up to) A*R waves of block g
@@ -639,7 +667,11 @@ int rx_assign(rx_env* h, const int32_t* track_of_env) {
     if ((rc = upload(h->resets, z.data(), z.size()))) return rc;
   }
   h->sort_on = false;
-  if (h->cfg.sort_interval > 0) {
+  if (h->lane_tracks) {  // the kernels read each position's slot: the order stays fixed
+    std::vector<int32_t> ps(N);
+    for (int p = 0; p < N; ++p) ps[p] = track_of_env[perm[p]];
+    if ((rc = upload(h->pos_slot, ps.data(), ps.size()))) return rc;
+  } else if (h->cfg.sort_interval > 0) {
     // spatial sort bins: slot k owns (W_k >> shift) + 1 consecutive bins from
     // sort_base[k]; the smallest shift that keeps all bins <= RX_SORT_MAX_BINS.
     // More slots than that (at most ~1 env per slot): nothing to regroup, no sort.
@@ -815,7 +847,9 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.wide = h->dyn_lpe == 64;
   a.n_wide_tasks = h->cfg.n_envs * h->cfg.n_agents * h->cfg.n_sensors;
   a.tasks = h->tasks.p;
-  a.tasks_out = (h->cfg.ray_order == 2 && !a.wide) ? h->tasks.p : nullptr;
+  a.tasks_out = (h->cfg.ray_order == 2 && !a.wide && !h->lane_tracks) ? h->tasks.p : nullptr;
+  a.lane_tracks = h->lane_tracks;
+  a.pos_slot = h->lane_tracks ? h->pos_slot.p : nullptr;
   a.cs_scratch = h->cs_scratch.p;
   a.sort_base = h->sort_base.p;
   a.sort_shift = h->sort_shift;

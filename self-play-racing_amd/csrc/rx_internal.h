@@ -168,6 +168,8 @@ struct rx_kargs {
   int32_t seg_filter;     // k_rays: float32 pre-filter before each exact segment test (RX_SEG_FILTER=0: off)
   int32_t ray_lpr;        // culled raycast: lanes per ray task (1; 4 for few envs, 16 tasks a ray wave)
   int32_t reward_lpe;     // k_step2<1> REWARD half: lanes per env (1, 2 or 4; more for few envs)
+  int32_t lane_tracks;    // lane-varying slots (rx_config.lane_tracks): waves of 64 positions of any slots
+  const int32_t* pos_slot;  // with lane_tracks: [N] the slot of the env at each position (the order is fixed)
   int32_t ray_tail_from;  // ray waves >= this one (the dispatch tail) hold 64 / ray_tail_lpr tasks each, cast at
   int32_t ray_tail_lpr;   // ray_tail_lpr lanes per ray (2 or 4); -1 = no tail split (rx_config.ray_tail)
   // rx_set_start_draws (two-car envs): the start-slot order of the env that is the

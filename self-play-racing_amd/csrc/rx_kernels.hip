@@ -93,6 +93,35 @@ __device__ __forceinline__ float4 ldu(const float4* p) {
   return make_float4(q[0], q[1], q[2], q[3]);
 }
 
+// Lane-varying track slots (rx_config.lane_tracks, DESIGN.md §3 "Lane-varying
+// track slots"): with LV the lanes of a wave may belong to different slots, so a
+// track-table read is a per-lane vector load and every culling decision is the
+// lane's own; without it the wave's slot is uniform -- scalar loads (ldu), wave
+// votes, SGPR indices.  The arithmetic is the same either way, and no result
+// depends on which boxes a lane skips (the culling is exact), so both forms give
+// bit-identical outputs.
+template <bool LV, class T>
+__device__ __forceinline__ T ldt(const T* p) {
+  if constexpr (LV)
+    return *p;
+  else
+    return ldu(p);
+}
+template <bool LV>
+__device__ __forceinline__ int uni(int v) {
+  if constexpr (LV)
+    return v;
+  else
+    return uniform(v);
+}
+template <bool LV>
+__device__ __forceinline__ bool vote(bool b) {
+  if constexpr (LV)
+    return b;
+  else
+    return __any(b);
+}
+
 __device__ __forceinline__ float clipf(float a, float lo, float hi) {
   float y = a < lo ? lo : a;
   return y > hi ? hi : y;
@@ -160,10 +189,16 @@ __device__ __forceinline__ void argmin_take(double d, int i, double& best, int& 
 // 2^-40 relative + 1e-12) can hold no waypoint at distance <= any of the car's
 // bests.  One distance bound per car instead of one per point.
 #define RX_CAR_RADIUS 2.23607  // >= |corner - centre| = sqrt(2^2 + 1^2) = 2.2360680 (car.py:26-43)
-template <int NC>
+template <int NC, bool LV = false>
 __device__ __forceinline__ bool box_may_hold_c(const double* __restrict__ b, const double cxs[NC], const double cys[NC],
                                                const double T[NC]) {
-  const double x0 = ldu(b), y0 = ldu(b + 1), x1 = ldu(b + 2), y1 = ldu(b + 3);
+  double x0, y0, x1, y1;
+  if constexpr (LV) {  // one 32-byte box: two dwordx4 vector loads
+    const double4 v = *reinterpret_cast<const double4*>(b);
+    x0 = v.x, y0 = v.y, x1 = v.z, y1 = v.w;
+  } else {
+    x0 = ldu(b), y0 = ldu(b + 1), x1 = ldu(b + 2), y1 = ldu(b + 3);
+  }
   bool need = false;
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
@@ -196,7 +231,7 @@ __device__ __forceinline__ void car_thresholds(const double best[NP], double T[N
 // The bound is shrunk by 2^-46 relative, far beyond the few-ulp rounding of
 // both the bound and the per-waypoint distances, so a skipped chunk can
 // neither beat nor tie the best (ties are broken by index, argmin_take).
-template <int NP, int NC>
+template <int NP, int NC, bool LV = false>
 __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, const double* __restrict__ wbox,
                                               const double* __restrict__ wsbox, int W,
                                               const double px[NP], const double py[NP], const int prev[NC],
@@ -242,15 +277,15 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
   car_thresholds<NP, NC>(best, T, active);
 #pragma unroll 4
   for (int u = 0; u < nws; ++u)
-    smask |= (unsigned long long)(__any(box_may_hold_c<NC>(wsbox + 4 * u, cxs, cys, T)) ? 1 : 0) << u;
-  smask = uniform64(smask);
+    smask |= (unsigned long long)(vote<LV>(box_may_hold_c<NC, LV>(wsbox + 4 * u, cxs, cys, T)) ? 1 : 0) << u;
+  if constexpr (!LV) smask = uniform64(smask);
 #ifdef RX_DYN_STAMPS
   if (stamps) {
     __builtin_amdgcn_s_waitcnt(0);
     stamps[1] = __builtin_amdgcn_s_memtime();
   }
 #endif
-  const int u0 = uniform(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
+  const int u0 = uni<LV>(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
   int scanned = 0, tested = nws;
   for (int s = 0; s < nws; ++s) {
     const int off = (s + 1) >> 1;
@@ -262,12 +297,12 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     for (int q = 0; q < nl; ++q) {
       const int c = l0 + (back ? nl - 1 - q : q);
       ++tested;  // T is current: the bests change only inside a leaf scan, which refreshes it
-      if (!__any(box_may_hold_c<NC>(wbox + 4 * c, cxs, cys, T))) continue;
+      if (!vote<LV>(box_may_hold_c<NC, LV>(wbox + 4 * c, cxs, cys, T))) continue;
       ++scanned;
       const int i1 = min(W, (c + 1) * RX_WP_CHUNK);
       int i = c * RX_WP_CHUNK;
       for (; i + 4 <= i1; i += 4) {  // four waypoints per batch of scalar loads
-        const double2 w[4] = {ldu(wp + i), ldu(wp + i + 1), ldu(wp + i + 2), ldu(wp + i + 3)};  // uniform -> s_load
+        const double2 w[4] = {ldt<LV>(wp + i), ldt<LV>(wp + i + 1), ldt<LV>(wp + i + 2), ldt<LV>(wp + i + 3)};
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
 #pragma unroll
@@ -278,7 +313,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
         }
       }
       for (; i < i1; ++i) {
-        const double2 w = ldu(wp + i);
+        const double2 w = ldt<LV>(wp + i);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const double dx = w.x - px[p], dy = w.y - py[p];
@@ -289,8 +324,8 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
     }
   }
 #ifndef RX_DYN_STAMPS  // the stamp build reuses io.counters for its stamps: no culling counts there
-  if (counters && (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
-    atomicAdd(&counters[2], (unsigned long long)tested);
+  if (counters && (LV || (threadIdx.x & 63) == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))) {
+    atomicAdd(&counters[2], (unsigned long long)tested);  // LV: every lane its own tests
     atomicAdd(&counters[3], (unsigned long long)scanned);
   }
 #endif
@@ -550,9 +585,10 @@ struct rx_slot_lds {
   const double4* seg;
 };
 
-template <int LPE, int PART>
+template <int LPE, int PART, bool LV = false>
 __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* ang_out, int& e_out, double ep_out[3],
                                          int sub_block = 0, const rx_slot_lds* sl = nullptr) {
+  static_assert(!LV || LPE == 1, "lane-varying slots: one lane per env");
   constexpr bool FULL = PART == RX_PART_FULL, KIN = PART == RX_PART_KIN, REW = PART == RX_PART_REWARD;
 #ifdef RX_DYN_STAMPS
   unsigned long long stamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -566,9 +602,10 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   // wave was built for one lane per env: the REWARD half at LPE = 2)
   const int lane = (threadIdx.x & 63) / LPE + sub_block * (64 / LPE);
   const int sub = threadIdx.x & (LPE - 1);
-  const int k = uniform(we.track);
-  const int wp0 = uniform(a.tr.wp_off[k]);
-  const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
+  // LV: the lane's own slot (the wave's 64 positions may hold 64 slots)
+  const int k = LV ? (lane < we.count ? a.pos_slot[we.perm_start + lane] : 0) : uniform(we.track);
+  const int wp0 = uni<LV>(a.tr.wp_off[k]);
+  const int W = uni<LV>(a.tr.wp_off[k + 1]) - wp0;
   const double2* __restrict__ wp = sl ? sl->wp : reinterpret_cast<const double2*>(a.tr.wp) + wp0;
   const double2* __restrict__ nrm = sl ? sl->nrm : reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
   const double* __restrict__ meta = a.tr.meta + 8 * k;
@@ -645,8 +682,8 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     } else if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
       const double ccx[1] = {c.x}, ccy[1] = {c.y};
-      argmin_culled<NPL, 1>(wp, a.tr.wchunk_box + 4 * (size_t)uniform(a.tr.wchunk_off[k]),
-                            a.tr.wsuper_box + 4 * (size_t)uniform(a.tr.wsuper_off[k]), W, qx, qy, prev, ccx, ccy,
+      argmin_culled<NPL, 1, LV>(wp, a.tr.wchunk_box + 4 * (size_t)uni<LV>(a.tr.wchunk_off[k]),
+                            a.tr.wsuper_box + 4 * (size_t)uni<LV>(a.tr.wsuper_off[k]), W, qx, qy, prev, ccx, ccy,
                             a.argmin_window, idx, a.io.counters
 #ifdef RX_DYN_STAMPS
                             , stamp + 3
@@ -890,7 +927,7 @@ __device__ __forceinline__ void prof_end(const rx_kargs& a, int wave, unsigned l
 }
 
 // k_dyn1 (PART = FULL) and k_kin1 (PART = KIN): 4 waves per workgroup.
-template <int LPE, int PART>
+template <int LPE, int PART, bool LV = false>
 __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wave >= a.n_dyn_waves) return;
@@ -908,7 +945,7 @@ __global__ __launch_bounds__(256) void k_dyn1(rx_kargs a) {
   const unsigned long long prof_t0 = prof_start(a);
   double ang[1], ep[3] = {0.0, 0.0, 0.0};
   int e = -1;  // set on the lane that finishes an env (sub 0)
-  dyn1_env<LPE, PART>(a, wave, ang, e, ep);
+  dyn1_env<LPE, PART, LV>(a, wave, ang, e, ep);
   if (PART == RX_PART_FULL) add_episode_stats(a, ep);
   if (sorting) sort_block_tasks<1>(a, uniform(a.dyn_waves[wave].perm_start), e, ang, cnt, stage);
   prof_end(a, wave, prof_t0);
@@ -1523,18 +1560,18 @@ __device__ __forceinline__ void seg_may_hit2(const float4 f0, const float4 f1, c
 // time (each test ends in a divergent branch, so a plain loop would wait for
 // every s_load on its own).  FILT: the exact test of a segment runs only if
 // the float32 pre-filter passes for some lane.
-template <bool FILT>
+template <bool FILT, bool LV = false>
 __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
                                              double v3x, double v3y, double& best, float& bestf, const seg_pref& pf) {
   int j = j0;
   if constexpr (FILT) {
     for (; j + 4 <= j1; j += 4) {
-      const float4 f0 = ldu(pf.segf + j), f1 = ldu(pf.segf + j + 1), f2 = ldu(pf.segf + j + 2),
-                   f3 = ldu(pf.segf + j + 3);
+      const float4 f0 = ldt<LV>(pf.segf + j), f1 = ldt<LV>(pf.segf + j + 1), f2 = ldt<LV>(pf.segf + j + 2),
+                   f3 = ldt<LV>(pf.segf + j + 3);
       bool m0, m1, m2, m3;
       seg_may_hit2(f0, f1, pf, m0, m1);
       seg_may_hit2(f2, f3, pf, m2, m3);
-      const bool h0 = __any(m0), h1 = __any(m1), h2 = __any(m2), h3 = __any(m3);
+      const bool h0 = vote<LV>(m0), h1 = vote<LV>(m1), h2 = vote<LV>(m2), h3 = vote<LV>(m3);
 #ifdef RX_RAY_STAMPS
       pf.cnt[0] += 4;
       const bool hh[4] = {h0, h1, h2, h3};
@@ -1547,24 +1584,24 @@ __device__ __forceinline__ void ray_segments(const double4* __restrict__ seg, in
       }
       continue;
 #endif
-      if (h0) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
-      if (h1) seg_test(ldu(seg + j + 1), ox, oy, v3x, v3y, best);
-      if (h2) seg_test(ldu(seg + j + 2), ox, oy, v3x, v3y, best);
-      if (h3) seg_test(ldu(seg + j + 3), ox, oy, v3x, v3y, best);
+      if (h0) seg_test(ldt<LV>(seg + j), ox, oy, v3x, v3y, best);
+      if (h1) seg_test(ldt<LV>(seg + j + 1), ox, oy, v3x, v3y, best);
+      if (h2) seg_test(ldt<LV>(seg + j + 2), ox, oy, v3x, v3y, best);
+      if (h3) seg_test(ldt<LV>(seg + j + 3), ox, oy, v3x, v3y, best);
     }
     for (; j < j1; ++j)
-      if (__any(seg_may_hit(ldu(pf.segf + j), pf))) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
+      if (vote<LV>(seg_may_hit(ldt<LV>(pf.segf + j), pf))) seg_test(ldt<LV>(seg + j), ox, oy, v3x, v3y, best);
     bestf = f32_up(best);
     return;
   }
   for (; j + 4 <= j1; j += 4) {
-    const double4 g0 = ldu(seg + j), g1 = ldu(seg + j + 1), g2 = ldu(seg + j + 2), g3 = ldu(seg + j + 3);  // uniform -> s_load
+    const double4 g0 = ldt<LV>(seg + j), g1 = ldt<LV>(seg + j + 1), g2 = ldt<LV>(seg + j + 2), g3 = ldt<LV>(seg + j + 3);
     seg_test(g0, ox, oy, v3x, v3y, best);
     seg_test(g1, ox, oy, v3x, v3y, best);
     seg_test(g2, ox, oy, v3x, v3y, best);
     seg_test(g3, ox, oy, v3x, v3y, best);
   }
-  for (; j < j1; ++j) seg_test(ldu(seg + j), ox, oy, v3x, v3y, best);
+  for (; j < j1; ++j) seg_test(ldt<LV>(seg + j), ox, oy, v3x, v3y, best);
   bestf = f32_up(best);
 }
 
@@ -1585,12 +1622,13 @@ __device__ __forceinline__ double quad_dpp(double v) {
 // LPR, ...), then take the minimum of their bests, so every lane goes on with
 // the ray's best -- the minimum over the leaf's exact hits, whoever tested
 // which segment.
-template <bool FILT, int LPR>
+template <bool FILT, int LPR, bool LV = false>
 __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
                                               double v3x, double v3y, double& best, float& bestf, const seg_pref& pf) {
   if constexpr (LPR == 1) {
-    ray_segments<FILT>(seg, j0, j1, ox, oy, v3x, v3y, best, bestf, pf);
+    ray_segments<FILT, LV>(seg, j0, j1, ox, oy, v3x, v3y, best, bestf, pf);
   } else {
+    static_assert(!LV, "lane-varying slots: one lane per ray");
     static_assert(LPR == 2 || LPR == 4, "2 or 4 lanes per ray");
     const int sub = threadIdx.x & (LPR - 1);
     for (int jb = j0; jb < j1; jb += LPR) {
@@ -1653,9 +1691,10 @@ __device__ __forceinline__ bool slab_keep(float lo, float hi, float bm) {
   asm("v_fma_f32 %0, |%1|, %2, %1" : "=v"(y) : "v"(hi), "s"(k));
   return !(x - y > 1e-6f) && x < bm;
 }
+template <bool LV = false>
 __device__ __forceinline__ bool chunk_needed_f(const float* __restrict__ box, rx_f2 clo, rx_f2 chi, rx_f2 id2,
                                                float mtf, float bm) {
-  const float4 b = ldu(reinterpret_cast<const float4*>(box));
+  const float4 b = ldt<LV>(reinterpret_cast<const float4*>(box));
   const rx_f2 t1 = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, clo);
   const rx_f2 t2 = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, chi);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1.x, t2.x), __builtin_fminf(t1.y, t2.y)), -mtf);
@@ -1675,9 +1714,10 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
 // plane's t and max(t1, t2) the far one's; only where chunk_needed_f meets a
 // NaN (0 * inf: origin on a slab plane, f32 direction component 0) does this
 // test drop the NaN and keep the box -- more conservative, never less.
+template <bool LV = false>
 __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx_f2 cn, rx_f2 cf, rx_f2 id2,
                                                float mtf, float bm) {
-  const float4 b = ldu(reinterpret_cast<const float4*>(box));
+  const float4 b = ldt<LV>(reinterpret_cast<const float4*>(box));
   const rx_f2 tn = __builtin_elementwise_fma(rx_f2{b.x, b.y}, id2, cn);
   const rx_f2 tf = __builtin_elementwise_fma(rx_f2{b.z, b.w}, id2, cf);
   const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), -mtf);
@@ -1689,17 +1729,17 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
 // `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far) * id;
 // otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi) * id.
-template <bool FAST, bool FILT, int LPR>
+template <bool FAST, bool FILT, int LPR, bool LV = false>
 __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
                                           int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
                                           double oy, double v3x, double v3y, double& best, float& bestf, int& tested,
                                           int& scanned, const seg_pref& pf) {
   const int G = a.cull_chunk;
   const float* __restrict__ fboxes =
-      a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uniform(a.tr.chunk_off[k]));
+      a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uni<LV>(a.tr.chunk_off[k]));
   float bm = bestf + mtf;  // refreshed with bestf after every leaf scan
   auto needed = [&](const float* box) {
-    return FAST ? chunk_needed_q(box, n1, n2, id2, mtf, bm) : chunk_needed_f(box, n1, n2, id2, mtf, bm);
+    return FAST ? chunk_needed_q<LV>(box, n1, n2, id2, mtf, bm) : chunk_needed_f<LV>(box, n1, n2, id2, mtf, bm);
   };
   const int SG = a.cull_super;
   if (SG <= 0) {
@@ -1710,10 +1750,10 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
         ++tested;
-        if (__any(needed(fboxes + 4 * (side * nch + c)))) {
+        if (vote<LV>(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
-                                   bestf, pf);
+          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+                                       best, bestf, pf);
           bm = bestf + mtf;
         }
       }
@@ -1727,8 +1767,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
   // contains the segments).
   const int nsup = (nch + SG - 1) / SG;
   const float* __restrict__ sboxes =
-      a.tr.super_box_f + 4 * ((size_t)block * a.tr.n_super_boxes + (size_t)uniform(a.tr.super_off[k]));
-  const int u0 = uniform(c0 / SG);
+      a.tr.super_box_f + 4 * ((size_t)block * a.tr.n_super_boxes + (size_t)uni<LV>(a.tr.super_off[k]));
+  const int u0 = uni<LV>(c0 / SG);
   for (int s = 0; s < nsup; ++s) {
     const int off = (s + 1) >> 1;
     const bool back = (s & 1) != 0;
@@ -1738,14 +1778,14 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       ++tested;
-      if (!__any(needed(sboxes + 4 * (side * nsup + u)))) continue;
+      if (!vote<LV>(needed(sboxes + 4 * (side * nsup + u)))) continue;
       for (int q = 0; q < nl; ++q) {
         const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
         ++tested;
-        if (__any(needed(fboxes + 4 * (side * nch + c)))) {
+        if (vote<LV>(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          leaf_segments<FILT, LPR>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y, best,
-                                   bestf, pf);
+          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+                                       best, bestf, pf);
           bm = bestf + mtf;
         }
       }
@@ -1773,19 +1813,24 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 // One ray wave: the wave record `we` (slot, tasks [task_start, task_start + count)
 // of `tasks`: the ray-wave table's record and the global task buffer in k_step2 /
 // k_rays).  `wave` only indexes the profiling stamps.
-template <int A, int LPR>
+// LV (lane-varying slots): the wave's tasks are the (env, agent, ray) tasks of its
+// 64-env block in env-major order -- 11 rays of ~6 envs, so lanes of one env share
+// their slot's cache lines -- and every lane reads its own env's slot.
+template <int A, int LPR, bool LV = false>
 __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
+  static_assert(!LV || LPR == 1, "lane-varying slots: one lane per ray");
 #ifdef RX_RAY_STAMPS
   unsigned long long rstamp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   rstamp[6] = wall_clock64();
   RAY_STAMP(0);
 #endif
   const int lane = threadIdx.x & 63;
-  const int k = uniform(we.track);
-  const int wp0 = uniform(a.tr.wp_off[k]);
-  const int W = uniform(a.tr.wp_off[k + 1]) - wp0;
-  const int S_ = 2 * W;
-  const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
+  const int kw = LV ? 0 : uniform(we.track);
+  int wp0 = 0, W = 0;
+  if constexpr (!LV) {
+    wp0 = uniform(a.tr.wp_off[kw]);
+    W = uniform(a.tr.wp_off[kw + 1]) - wp0;
+  }
   const int count = uniform(we.count);  // tasks of this wave (64 / LPR at most)
   if (count <= 0) return;
   // LPR lanes per task; lanes past the wave's tasks repeat its last one (their
@@ -1797,25 +1842,33 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   const int R = a.n_sensors;
   const int task = we.task_start + (own ? tl : count - 1);
   int env_local = 0, q, ray, pos;
-  if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
+  if (LV || a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
+    env_local = task / (A * R);
+    const int rem = task - env_local * (A * R);
+    q = rem / R;
+    ray = rem - q * R;
+  } else if (a.ray_order == 2) {  // sorted (agent, ray) tasks: direction- and position-binned waves
     const int t = ldc(tasks + task);
     const int iq = t / R;
     ray = t - iq * R;
     pos = iq / A;
     q = iq - pos * A;
-  } else if (a.ray_order == 0) {  // (env, agent, ray): 11 rays of ~6 envs per wave
-    env_local = task / (A * R);
-    const int rem = task - env_local * (A * R);
-    q = rem / R;
-    ray = rem - q * R;
   } else {  // ray-major: one (agent, ray) over consecutive (position-sorted) envs
-    const int ng = uniform(a.slot_nenv[k]);
+    const int ng = uniform(a.slot_nenv[kw]);
     const int qr = task / ng;
     env_local = task - qr * ng;
     q = qr / R;
     ray = qr - q * R;
   }
-  if (a.ray_order != 2) pos = we.perm_start + env_local;
+  if (LV || a.ray_order != 2) pos = we.perm_start + env_local;
+  int k = kw;
+  if constexpr (LV) {  // the lane's env's slot
+    k = a.pos_slot[pos];
+    wp0 = a.tr.wp_off[k];
+    W = a.tr.wp_off[k + 1] - wp0;
+  }
+  const int S_ = 2 * W;
+  const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
   const int i = A * pos + q;  // working state (position order); the obs row is A * perm[pos] + q
   const double ox = ldc(a.st.x + i), oy = ldc(a.st.y + i);
   const double theta = ldc(a.st.angle + i) + a.rel_angles[ray];  // racing_env.py:50
@@ -1828,7 +1881,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   float bestf = __builtin_inff();
   const int G = a.cull_chunk;
   if (G <= 0) {
-    ray_segments<false>(seg, 0, S_, ox, oy, v3x, v3y, best, bestf, seg_pref{});
+    ray_segments<false, LV>(seg, 0, S_, ox, oy, v3x, v3y, best, bestf, seg_pref{});
   } else {
     const int nch = (W + G - 1) / G;  // chunks per side
     const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
@@ -1851,11 +1904,11 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     // visit chunks outward from the wave's first car
     int w0 = (int)(ldc(a.st.progress + i) * (double)W + 0.5);
     w0 = w0 < 0 ? 0 : (w0 >= W ? W - 1 : w0);
-    const int c0 = uniform(w0 / G);
+    const int c0 = uni<LV>(w0 / G);
     // direction quadrant (sign bits of the f32 direction, as id2's signs): a
     // wave whose lanes all share it takes the quadrant-ordered box tables
     const int quad = (int)(__float_as_uint(csf) >> 31) | (int)((__float_as_uint(snf) >> 31) << 1);
-    const int quad0 = uniform(quad);
+    const int quad0 = uni<LV>(quad);  // LV: each lane takes its own quadrant's box block
     int scanned = 0, tested = 0;
     // segment pre-filter operands (seg_may_hit): |sx| + |sy| <= |cx| + |cy| + 2 rad for every boundary point
 #ifdef RX_RAY_STAMPS
@@ -1872,14 +1925,14 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     RAY_STAMP(3);
     auto scan = [&](auto filt) {
       constexpr bool F = decltype(filt)::value;
-      if (a.box_quadrants && __all(quad == quad0)) {
+      if (a.box_quadrants && (LV || __all(quad == quad0))) {
         const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
         const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
-        cull_scan<true, F, LPR>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x, v3y,
-                                best, bestf, tested, scanned, pf);
+        cull_scan<true, F, LPR, LV>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x,
+                                    v3y, best, bestf, tested, scanned, pf);
       } else {
-        cull_scan<false, F, LPR>(a, k, W, nch, seg, c0, 0, nlo * id2, nhi * id2, id2, mtf, ox, oy, v3x, v3y, best,
-                                 bestf, tested, scanned, pf);
+        cull_scan<false, F, LPR, LV>(a, k, W, nch, seg, c0, 0, nlo * id2, nhi * id2, id2, mtf, ox, oy, v3x, v3y,
+                                     best, bestf, tested, scanned, pf);
       }
     };
     if (a.seg_filter && a.tr.seg_f)
@@ -1893,8 +1946,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     rstamp[10] = (unsigned long long)cnt[1] | ((unsigned long long)cnt[2] << 32);  // exact tests | that lowered a best
     rstamp[11] = (unsigned long long)cnt[0];                                       // segments pre-filtered
 #else
-    if (a.io.counters && lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63)) {
-      atomicAdd(&a.io.counters[0], (unsigned long long)tested);
+    if (a.io.counters && (LV || lane == (__builtin_amdgcn_readfirstlane(threadIdx.x) & 63))) {
+      atomicAdd(&a.io.counters[0], (unsigned long long)tested);  // LV: every lane its own tests
       atomicAdd(&a.io.counters[1], (unsigned long long)scanned);
     }
 #endif
@@ -1944,10 +1997,10 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
   a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 
-template <int A, int LPR>
+template <int A, int LPR, bool LV = false>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
-  rays_wave<A, LPR>(a, a.ray_waves[wave], a.tasks, wave);
+  rays_wave<A, LPR, LV>(a, a.ray_waves[wave], a.tasks, wave);
 }
 
 // A ray wave of the table: at the schedule's LPR lanes per ray, or -- for the
@@ -1967,8 +2020,12 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
 #ifndef RX_RAY_PRIO_FROM
 #define RX_RAY_PRIO_FROM 70
 #endif
-template <int A, int LPR>
+template <int A, int LPR, bool LV = false>
 __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
+  if constexpr (LV) {  // no tail split, no dispatch-order priority (rx_assign: group-octet-major)
+    rays_body<A, 1, true>(a, wave);
+    return;
+  }
   if constexpr (A == 1 && RX_RAY_PRIO > 0) {
     if (wave * 100 >= a.n_ray_waves * RX_RAY_PRIO_FROM) __builtin_amdgcn_s_setprio(RX_RAY_PRIO);
   }
@@ -1984,11 +2041,13 @@ __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
   rays_body<A, LPR>(a, wave);
 }
 
-template <int A>
+template <int A, bool LV = false>
 __global__ __launch_bounds__(256) void k_rays(rx_kargs a) {
   const int wave = uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const unsigned long long prof_t0 = prof_start(a);
-  if (a.ray_lpr == 4)
+  if (LV)
+    rays_dispatch<A, 1, LV>(a, wave);
+  else if (a.ray_lpr == 4)
     rays_body<A, 4>(a, wave);
   else if (a.ray_lpr == 2)
     rays_body<A, 2>(a, wave);
@@ -2054,6 +2113,9 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 #ifndef RX_STEP2_MINW
 #define RX_STEP2_MINW 8  // min waves per SIMD: caps VGPRs at 64 so the raycast half keeps full occupancy (some spills in the REWARD half)
 #endif
+#ifndef RX_STEP2_MINW_LV
+#define RX_STEP2_MINW_LV 5  // lane-varying slots (k_step2<1, 1, 1, true>): 93 VGPRs, no spills (8 waves: 201 spilled VGPRs)
+#endif
 #ifndef RX_STEP2_MINW_2
 #define RX_STEP2_MINW_2 6  // two-car k_step2<2>: 80 VGPRs (fewer REWARD spills; 8 -> 6 waves: +9 % at 8,192 envs, +1 % at 65,536)
 #endif
@@ -2063,8 +2125,9 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 // the raycast's 64-VGPR cap (k_step2<1>: 36 B/lane of scratch) whichever
 // schedule ran.  For A = 2, RLPE 2 gives each car of an env its own lane in the
 // REWARD half (dyn2_env<REWARD, 2>).
-template <int A, int RLPE, int LPR>
-__global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void k_step2(rx_kargs a, int n_rw) {
+template <int A, int RLPE, int LPR, bool LV = false>
+__global__ __launch_bounds__(64, A == 1 ? (LV ? RX_STEP2_MINW_LV : RX_STEP2_MINW) : RX_STEP2_MINW_2) void k_step2(
+    rx_kargs a, int n_rw) {
   const int b = uniform((int)blockIdx.x);
   const unsigned long long prof_t0 = prof_start(a);
   if (b < n_rw) {
@@ -2080,7 +2143,7 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
       // block b = sub-block * n1 + dynamics wave, so a REWARD wave keeps the
       // XCD (b % 8) of its k_kin1 wave (n1 = n_dyn_waves rounded up to 8)
       const int n1 = n_rw / RLPE, w = b % n1, sb = b / n1;
-      dyn1_env<RLPE, RX_PART_REWARD>(a, w, ang, e, ep, RLPE == 1 ? 0 : sb);
+      dyn1_env<RLPE, RX_PART_REWARD, LV>(a, w, ang, e, ep, RLPE == 1 ? 0 : sb);
     } else if constexpr (RLPE == 2) {
       const int n1 = n_rw / 2, w = b % n1, sb = b / n1;  // as the single-agent REWARD half at 2 lanes
       dyn2_env<RX_PART_REWARD, 2>(a, w, ang, e, ep, sb);
@@ -2089,7 +2152,7 @@ __global__ __launch_bounds__(64, A == 1 ? RX_STEP2_MINW : RX_STEP2_MINW_2) void 
     }
     add_episode_stats(a, ep);
   } else {
-    rays_dispatch<A, LPR>(a, b - n_rw);
+    rays_dispatch<A, LPR, LV>(a, b - n_rw);
   }
   prof_end(a, b, prof_t0);
 }
@@ -2482,6 +2545,14 @@ extern "C" int rx_launch_split(const rx_kargs* a, int n_agents, int part, hipStr
     return (int)hipGetLastError();
   }
   const int n_rw = a->reward_lpe * ((a->n_dyn_waves + 7) / 8 * 8);
+  if (a->lane_tracks) {  // lane-varying slots (rx_assign: one lane per env and per ray, no task sort)
+    if (part == RX_SPLIT_KIN)
+      hipLaunchKernelGGL((k_dyn1<1, RX_PART_KIN, true>), dim3(a->n_dyn_waves), dim3(64), 0, s, *a);
+    else
+      hipLaunchKernelGGL((k_step2<1, 1, 1, true>), dim3(n_rw + (part == RX_SPLIT_REWARD ? 0 : a->n_ray_waves)),
+                         dim3(64), 0, s, *a, n_rw);
+    return (int)hipGetLastError();
+  }
   if (part == RX_SPLIT_KIN) {
     // one wave per workgroup: block b's k_kin1 wave lands on XCD b % 8, the XCD of
     // block b's REWARD and raycast waves in k_step2, so they read its stores from one L2
@@ -2504,7 +2575,9 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   if ((phases & RX_PHASE_DYNAMICS) && a->n_dyn_waves > 0) {
     const dim3 grd((a->n_dyn_waves + 3) / 4);
     const size_t lds = task_sort_lds_bytes(a, n_agents, 4);
-    if (n_agents == 1 && a->dyn_lpe == 64)
+    if (n_agents == 1 && a->lane_tracks)
+      hipLaunchKernelGGL((k_dyn1<1, RX_PART_FULL, true>), grd, blk, 0, s, *a);
+    else if (n_agents == 1 && a->dyn_lpe == 64)
       hipLaunchKernelGGL((k_dyn1<64, RX_PART_FULL>), grd, blk, lds, s, *a);
     else if (n_agents == 1 && a->dyn_lpe == 4)
       hipLaunchKernelGGL((k_dyn1<4, RX_PART_FULL>), grd, blk, lds, s, *a);
@@ -2524,7 +2597,9 @@ extern "C" int rx_launch_step(const rx_kargs* a, int n_agents, int phases, hipSt
   } else if ((phases & RX_PHASE_RAYS) && a->n_ray_waves > 0) {
     // one wave per workgroup: finer-grained dispatch fills the tail, and the XCD
     // placement of rx_assign's ray-wave order holds per wave
-    if (n_agents == 1)
+    if (n_agents == 1 && a->lane_tracks)
+      hipLaunchKernelGGL((k_rays<1, true>), dim3(a->n_ray_waves), dim3(64), 0, s, *a);
+    else if (n_agents == 1)
       hipLaunchKernelGGL(k_rays<1>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
     else
       hipLaunchKernelGGL(k_rays<2>, dim3(a->n_ray_waves), dim3(64), 0, s, *a);
