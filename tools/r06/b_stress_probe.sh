@@ -1,0 +1,29 @@
+#!/bin/bash
+# r06 b: stress-pool schedules (tools/r06/stress_probe.py), then PMC of the lane-varying k_step2:
+# HBM fetch (FETCH_SIZE), L2 hit/miss, and the SQ issue / wait breakdown (counters only, one pass each)
+set -o pipefail
+O=gpurun_out/r06b
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python tools/r06/stress_probe.py 65536 > $O/probe.jsonl 2> $O/probe.err || exit 1
+P="python tools/r06/stress_probe.py 65536 lane_tracks=1"
+i=0
+for ctrs in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_ANY" "GRBM_GUI_ACTIVE"; do
+  i=$((i + 1))
+  timeout -k 10 300 rocprofv3 --pmc $ctrs -d $O/pmc$i -o run --output-format csv -- $P > $O/pmc$i.log 2>&1 || { tail -20 $O/pmc$i.log; exit 1; }
+done
+python - $O <<'PY'
+import csv, glob, sys, collections, json
+root = sys.argv[1]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(root + "/pmc*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        n = r["Kernel_Name"]
+        for k in ("k_step2", "k_dyn1", "k_rays"):
+            if k in n:
+                key = k + ("_LV" if "ELb1E" in n else "")
+                acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {k: {c: round(sum(v) / len(v)) for c, v in sorted(d.items())} for k, d in acc.items()}
+json.dump(out, open(root + "/pmc_stress.json", "w"), indent=1)
+print(json.dumps(out, indent=1))
+PY
