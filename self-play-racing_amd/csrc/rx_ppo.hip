@@ -622,50 +622,74 @@ __device__ __forceinline__ void ppo_grad_trunk(const ppo_args& a, const float* _
 // Gradients are rounded to bf16 only where they are matrix operands, as the
 // fp32-vs-bf16 contract of rx.h says; accumulation and everything else is f32.
 // Same pass structure as the fp32 kernel (A forward + loss + images | B dW2, dH1
-// | C images | D dW1, dW3), 52 KB of LDS: three 4-wave workgroups per CU.
-// RX_PPO_BF_DB = 1 (A/B build): two barriers per pass instead of four -- the
-// dZ1 / H2 images separate from the dZ2 / H1 ones and [X | 1] / g double-buffered
-// by pass parity, so phase C's stores need no barrier before them and the next
-// pass's phase A none after phase D (79 KB of LDS: two workgroups per CU, all
-// that a minibatch's 512 workgroups fill).  Measured no faster (17.63 vs 17.56
-// us, profiles/r05/ab_bf16_barriers.json): the barriers are not what the
-// kernel waits on, so the default keeps the 52 KB layout.
-#ifndef RX_PPO_BF_DB
-#define RX_PPO_BF_DB 0
-#endif
+// | C images | D dW1, dW3), 47 KB of LDS: three 4-wave workgroups per CU.
+//
+// The images live in two regions of kRP rows x 96 bf16 (GradLdsB): A = dZ (cols
+// 0..63: dZ2, then dZ1) | [X | 1] (cols 64..95); B = H (cols 0..63: H1, then H2) |
+// its ones tile (64..79) | g (80..95).  The row stride is 48 dwords and every
+// row is swizzled (sw_off: 16-column block b at b ^ ((r >> 3) & 1), 4-column
+// chunk p at p ^ ((r >> 1) & 3)), which makes both of the kernel's LDS access
+// shapes bank-conflict-free (MI355X_MICROARCH.md §LDS): a packed row-chunk store
+// (ds_write_b64, groups of 16 lanes = 16 consecutive rows at one column, bank =
+// dword mod 32: row bit 0 -> bank bit 4 through the stride, bit 3 -> bit 3 through
+// the block swizzle, bits 1-2 -> bits 1-2 through the chunk swizzle) and the
+// transposed operand read (ds_read_b64_tr_b16, halves of 32 lanes = rows
+// {0..3, 8..11} + 32 s (+ 16) at one 16-column block, bank = dword mod 64: the
+// stride spreads rows 0..3 over 16-dword steps, the block swizzle moves rows
+// 8..11 by 8 dwords).  The plain [row][col] images of round 5 (strides 72 / 80 /
+// 48 / 24 bf16) ran 2- to 4-way conflicts on both: 38.5 % of the LDS-active
+// cycles (profiles/r05/pmc_ppo_bf16.json).  (Round 5's double-buffered image A/B,
+// RX_PPO_BF_DB, measured no faster and is gone with the plain layout.)
+constexpr int kIS = 96;  // image row stride (bf16): 48 dwords
 template <int D>
 struct GradLdsB {
-  static constexpr int DB = RX_PPO_BF_DB ? 2 : 1;  // image sets
-  static constexpr int ZS = 72, HS = 80, XS = 48, GS = RX_PPO_BF_DB ? 16 : 24;  // row strides (bf16)
   static constexpr int F1 = 0, F2 = F1 + 4 * 64 * 16, FT2 = F2 + 8 * 64 * 16, F3 = FT2 + 8 * 64 * 16,
                        B1 = F3 + 2 * 64 * 16, B2 = B1 + 64 * 4, W3 = B2 + 64 * 4, B3 = W3 + kNA * 64 * 4,
-                       IZ = B3 + 16, IH = IZ + DB * kRP * ZS * 2, IX = IH + DB * kRP * HS * 2,
-                       IG = IX + DB * kRP * XS * 2, KL = IG + DB * kRP * GS * 2, TOTAL = KL + 8 * kGW;
-  // image set k (k < DB) of each kind at its base + k * kRP * stride * 2 bytes
-  static_assert(IZ % 16 == 0 && IH % 16 == 0 && IX % 16 == 0 && IG % 16 == 0, "16-byte aligned images");
-  static_assert(TOTAL <= 80 * 1024, "two workgroups per CU");
+                       IA = B3 + 16, IB = IA + kRP * kIS * 2, KL = IB + kRP * kIS * 2, TOTAL = KL + 8 * kGW;
+  static constexpr int XC = 64, ONES = 64, GC = 80;  // column of [X | 1] in A, of the ones tile and g in B
+  static_assert(IA % 16 == 0 && IB % 16 == 0, "16-byte aligned images");
+  static_assert(TOTAL <= 53 * 1024, "three workgroups per CU");
 };
 
 using bf4 = __bf16 __attribute__((ext_vector_type(4)));
 using s4 = short __attribute__((ext_vector_type(4)));
-// 4 bf16 of one image row: the lane's 4 accumulator registers of a tile
-__device__ __forceinline__ void st_bf4(char* img, int off_elems, const f4& v) {
+// element offset of (row r, column c) in a swizzled image region (GradLdsB): the
+// 16-column block b of row r at block b ^ ((r >> 3) & 1), its 4-column chunk p at
+// chunk p ^ ((r >> 1) & 3); the 4 elements of a chunk stay contiguous (8 bytes)
+__device__ __forceinline__ int sw_off(int r, int c) {
+  return r * kIS + (((c >> 4) ^ ((r >> 3) & 1)) << 4) + ((((c >> 2) & 3) ^ ((r >> 1) & 3)) << 2) + (c & 3);
+}
+// 4 bf16 of one image row: the lane's 4 accumulator registers of a tile, at (row r, column c)
+__device__ __forceinline__ void st_bf4(char* img, int r, int c, const f4& v) {
   bf4 b;
   b[0] = (__bf16)v[0], b[1] = (__bf16)v[1], b[2] = (__bf16)v[2], b[3] = (__bf16)v[3];
-  *reinterpret_cast<bf4*>(img + 2 * off_elems) = b;
+  *reinterpret_cast<bf4*>(img + 2 * sw_off(r, c)) = b;
 }
-// The 16x16x32 operand of k-step s over an image [row][col] (stride S bf16):
+// The 16x16x32 operand of k-step s over an image region:
 // A[m = col c0 + lane & 15][k = row 32 s + 8 (lane >> 4) + j], two transposed reads
 // of 4 rows each (T10: lane 4q + p of a 16-lane group addresses row q, columns 4p..4p+3).
-template <int S>
-__device__ __forceinline__ bf8 tr_frag(const char* img, int s, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int e0 = (32 * s + 8 * g + (i >> 2)) * S + c0 + 4 * (i & 3);
+// The lane's row is 32 s + 8 g + (i >> 2) (g = lane >> 4, i = lane & 15), so its
+// swizzle terms are lane constants: block ^ (g & 1), chunk ^ ((i >> 3) & 1) (rows +4:
+// chunk ^ (((i >> 3) & 1) + 2)).  tr_lane holds the lane's byte offsets for an
+// even / odd block, low / high 4 rows; a read adds the compile-time 2 (32 s kIS + c0)
+// (the ds_read offset field), so the swizzle costs no per-read VALU or registers.
+struct tr_lane {
+  int lo_e, lo_o, hi_e, hi_o;
+};
+__device__ __forceinline__ tr_lane tr_lane_of(int lane) {
+  const int g = lane >> 4, i = lane & 15, j = i >> 2, g1 = g & 1, h = j >> 1;
+  const int lo = 2 * ((8 * g + j) * kIS + 16 * g1 + 4 * ((i & 3) ^ h));
+  const int hi = 2 * ((8 * g + j + 4) * kIS + 16 * g1 + 4 * ((i & 3) ^ (h + 2)));
+  return tr_lane{lo, lo - 64 * g1, hi, hi - 64 * g1};
+}
+__device__ __forceinline__ bf8 tr_frag(const char* img, int s, int c0, const tr_lane& tl) {
+  const int k = 2 * (32 * s * kIS + c0);  // c0: a multiple of 16
+  const bool odd = (c0 >> 4) & 1;
   typedef short __attribute__((ext_vector_type(4))) v4s;
   const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s*)(img + 2 * e0));
+      (__attribute__((address_space(3))) v4s*)(img + (odd ? tl.lo_o : tl.lo_e) + k));
   const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s*)(img + 2 * (e0 + 4 * S)));
+      (__attribute__((address_space(3))) v4s*)(img + (odd ? tl.hi_o : tl.hi_e) + k));
   bf8 r;
   const __bf16* pl = reinterpret_cast<const __bf16*>(&lo);
   const __bf16* ph = reinterpret_cast<const __bf16*>(&hi);
@@ -758,13 +782,11 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   float* fB2 = reinterpret_cast<float*>(lds + S::B2);
   float* fW3 = reinterpret_cast<float*>(lds + S::W3);
   float* fB3 = reinterpret_cast<float*>(lds + S::B3);
-  char* iZ = lds + S::IZ;
-  char* iH = lds + S::IH;
-  char* iX = lds + S::IX;
-  char* iG = lds + S::IG;
-  float* sW2 = reinterpret_cast<float*>(lds + S::IZ);  // scratch: W2 [64][kS2], then W1 [64][D]
+  char* iA = lds + S::IA;  // dZ | [X | 1]
+  char* iB = lds + S::IB;  // H | ones | g
+  float* sW2 = reinterpret_cast<float*>(lds + S::IA);  // scratch: W2 [64][kS2], then W1 [64][D]
   float* sW1 = sW2 + 64 * kS2;
-  static_assert(S::KL - S::IZ >= (64 * kS2 + 64 * D) * 4, "the staging scratch fits in the image region");
+  static_assert(S::KL - S::IA >= (64 * kS2 + 64 * D) * 4, "the staging scratch fits in the image regions");
 #pragma unroll
   for (int j = 0; j < kW1N; ++j)
     if (t0 + kGT * j < 64 * D) sW1[t0 + kGT * j] = w1v[j];
@@ -811,14 +833,12 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     F3[t0] = to_bf8(lo, hi);
   }
   __syncthreads();  // the scratch is dead: the images may be written
-  // constant image columns: H's ones tile (column 64 = 1, 65..79 = 0), G's zero columns 4..15
+  // constant image columns: H's ones tile (column 64 = 1, 65..79 = 0), g's zero columns 4..15
   // (read only after the next pass's first barrier)
-#pragma unroll
-  for (int k = 0; k < S::DB; ++k) {
-    const int r = t0 >> 2, c = 64 + 4 * (t0 & 3);  // 64 rows x 4 chunks of 4 columns
-    st_bf4(iH + k * kRP * S::HS * 2, r * S::HS + c,
-           c == 64 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
-    if ((t0 & 3) != 0) st_bf4(iG + k * kRP * S::GS * 2, r * S::GS + 4 * (t0 & 3), f4{0.0f, 0.0f, 0.0f, 0.0f});
+  {
+    const int r = t0 >> 2, c = 4 * (t0 & 3);  // 64 rows x 4 chunks of 4 columns
+    st_bf4(iB, r, S::ONES + c, c == 0 ? f4{1.0f, 0.0f, 0.0f, 0.0f} : f4{0.0f, 0.0f, 0.0f, 0.0f});
+    if (c != 0) st_bf4(iB, r, S::GC + c, f4{0.0f, 0.0f, 0.0f, 0.0f});
   }
   PPO_STAMP(1);
   f4 acc2[5], acc1[NT1], acc3 = {0.0f, 0.0f, 0.0f, 0.0f}, acc3b = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -828,14 +848,10 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
   for (int k = 0; k < NT1; ++k) acc1[k] = f4{0.0f, 0.0f, 0.0f, 0.0f};
   double kl = 0.0;
   const float* b3 = fB3;
-  int par = 0;  // pass parity: the [X | 1] / g image set of this pass (DB)
+  const tr_lane tl = tr_lane_of(lane);
   int pass_ = 0;
-  char* const iZ2 = iZ + (S::DB > 1 ? kRP * S::ZS * 2 : 0);  // dZ1 (DB) or dZ2 then dZ1
-  char* const iH2 = iH + (S::DB > 1 ? kRP * S::HS * 2 : 0);  // H2 (DB) or H1 then H2
   for (int64_t base = row0; base < row_end; base += kRP) {
     // ================================================================ A
-    char* const pX = iX + (S::DB > 1 ? par * kRP * S::XS * 2 : 0);
-    char* const pG = iG + (S::DB > 1 ? par * kRP * S::GS * 2 : 0);
     const int64_t src_nn = src_of(base + 2 * kRP);
     const RowIn nxt = load_row(src_n);
     const bool live = src >= 0;
@@ -844,8 +860,8 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       float xv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] = 8 * q + j == D ? 1.0f : cur.x[j];
-      *reinterpret_cast<bf8*>(pX + 2 * (rr * S::XS + 8 * q)) =
-          to_bf8(make_float4(xv[0], xv[1], xv[2], xv[3]), make_float4(xv[4], xv[5], xv[6], xv[7]));
+      st_bf4(iA, rr, S::XC + 8 * q, f4{xv[0], xv[1], xv[2], xv[3]});
+      st_bf4(iA, rr, S::XC + 8 * q + 4, f4{xv[4], xv[5], xv[6], xv[7]});
     }
     // forward: mlp_forward's bf16 arithmetic on the prebuilt fragments
     f4 H1[4], H2[4], y;
@@ -865,19 +881,19 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
       }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      st_bf4(iZ, rr * S::ZS + 16 * t + 4 * q, dZ[t]);
-      st_bf4(iH, rr * S::HS + 16 * t + 4 * q, H1[t]);
+      st_bf4(iA, rr, 16 * t + 4 * q, dZ[t]);
+      st_bf4(iB, rr, 16 * t + 4 * q, H1[t]);
     }
-    if (q == 0) st_bf4(pG, rr * S::GS, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
+    if (q == 0) st_bf4(iB, rr, S::GC, f4{g[0], NOUT > 1 ? g[NOUT - 1] : 0.0f, 0.0f, 0.0f});
     __syncthreads();
     PPO_STAMP(2 + 4 * pass_);
     // ================================================================ B
     // dW2 rows [16 wv, +16) x column tiles 0..3, db2 on tile 4 (the ones column)
 #pragma unroll
     for (int s = 0; s < kRP / 32; ++s) {
-      const bf8 av = tr_frag<S::ZS>(iZ, s, 16 * wv, lane);
+      const bf8 av = tr_frag(iA, s, 16 * wv, tl);
 #pragma unroll
-      for (int c = 0; c < 5; ++c) acc2[c] = mma16(av, tr_frag<S::HS>(iH, s, 16 * c, lane), acc2[c]);
+      for (int c = 0; c < 5; ++c) acc2[c] = mma16(av, tr_frag(iB, s, 16 * c, tl), acc2[c]);
     }
     // dH1 = W2^T dZ2 (B = dZ2 in registers, k = output unit), dZ1 = dH1 * (1 - H1^2)
     f4 dZ1[4];
@@ -892,13 +908,13 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
         for (int r = 0; r < 4; ++r) dZ1[mt][r] = z[r] * (1.0f - H1[mt][r] * H1[mt][r]);
       }
     }
-    if constexpr (S::DB == 1) __syncthreads();  // (DB: C writes the second image set)
+    __syncthreads();  // C overwrites dZ2 and H1
     PPO_STAMP(3 + 4 * pass_);
     // ================================================================ C
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      st_bf4(iZ2, rr * S::ZS + 16 * t + 4 * q, dZ1[t]);
-      st_bf4(iH2, rr * S::HS + 16 * t + 4 * q, H2[t]);
+      st_bf4(iA, rr, 16 * t + 4 * q, dZ1[t]);
+      st_bf4(iB, rr, 16 * t + 4 * q, H2[t]);
     }
     __syncthreads();
     PPO_STAMP(4 + 4 * pass_);
@@ -906,17 +922,16 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
     // dW1 (+ db1 at d = D) rows [16 wv, +16); dW3 column tile wv, db3 (wave 0) on the ones tile
 #pragma unroll
     for (int s = 0; s < kRP / 32; ++s) {
-      const bf8 av = tr_frag<S::ZS>(iZ2, s, 16 * wv, lane);
+      const bf8 av = tr_frag(iA, s, 16 * wv, tl);
 #pragma unroll
-      for (int c = 0; c < NT1; ++c) acc1[c] = mma16(av, tr_frag<S::XS>(pX, s, 16 * c, lane), acc1[c]);
-      const bf8 gv = tr_frag<S::GS>(pG, s, 0, lane);
-      acc3 = mma16(gv, tr_frag<S::HS>(iH2, s, 16 * wv, lane), acc3);
-      if (wv == 0) acc3b = mma16(gv, tr_frag<S::HS>(iH2, s, 64, lane), acc3b);
+      for (int c = 0; c < NT1; ++c) acc1[c] = mma16(av, tr_frag(iA, s, S::XC + 16 * c, tl), acc1[c]);
+      const bf8 gv = tr_frag(iB, s, S::GC, tl);
+      acc3 = mma16(gv, tr_frag(iB, s, 16 * wv, tl), acc3);
+      if (wv == 0) acc3b = mma16(gv, tr_frag(iB, s, S::ONES, tl), acc3b);
     }
-    if constexpr (S::DB == 1) __syncthreads();  // the next pass overwrites the images (DB: the other set)
+    __syncthreads();  // the next pass overwrites the images
     PPO_STAMP(5 + 4 * pass_);
     ++pass_;
-    par ^= 1;
     src = src_n;
     src_n = src_nn;
     cur = nxt;
@@ -962,13 +977,13 @@ __device__ __forceinline__ void ppo_grad_trunk_bf(const ppo_args& a, const float
 }
 
 // bf16 (RX_PPO_BF_FRAG = 1, the default): the fragment / transposed-image trunk
-// above, three workgroups per CU (52 KB of LDS, <= 168 VGPRs); 0 = the bf16 path
+// above, three workgroups per CU (47 KB of LDS, <= 168 VGPRs); 0 = the bf16 path
 // of ppo_grad_trunk (per-use conversions from the f32 LDS copy), kept for A/B.
 #ifndef RX_PPO_BF_FRAG
 #define RX_PPO_BF_FRAG 1
 #endif
 template <int D>
-__global__ __launch_bounds__(kGT, RX_PPO_BF_DB ? 2 : 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
+__global__ __launch_bounds__(kGT, 3) void k_ppo_grad_bf(ppo_args a, const float* __restrict__ W,
                                                         float* __restrict__ partial) {
   if (a.stop && *a.stop) return;  // KL early stop already hit: nothing to compute
   PPO_STAMP(0);

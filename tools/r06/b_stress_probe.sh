@@ -5,6 +5,7 @@ set -o pipefail
 O=gpurun_out/r06b
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_lane_tracks_gpu.py "tests/test_fullsize_gpu.py::test_stress_distinct_tracks_subset_bit_exact_vs_oracle" > $O/pytest_lane.txt 2>&1 || exit 1
 timeout -k 10 400 python tools/r06/stress_probe.py 65536 > $O/probe.jsonl 2> $O/probe.err || exit 1
 P="python tools/r06/stress_probe.py 65536 lane_tracks=1"
 i=0

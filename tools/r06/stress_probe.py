@@ -23,11 +23,12 @@ def main():
     from rx.track import TrackSet
     from rx.vector_env import RacingVectorEnv
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    workers = int(os.environ.get("RX_PROBE_WORKERS", "0")) or None  # 1: serial table build (under a profiler)
     scheds = sys.argv[2:] or ["lane_tracks=1", "lane_tracks=-1", "lane_tracks=-1,ray_lpr=4,reward_lpe=4",
                               "lane_tracks=-1,ray_lpr=4"]
     t0 = time.perf_counter()
     pool, widths = stress_pool(n)
-    ts = TrackSet.build(pool, widths)
+    ts = TrackSet.build(pool, widths, workers=workers)
     print(f"table {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -57,7 +58,7 @@ def main():
             env.step_device(acts[k % 64])
         torch.cuda.synchronize()
         el = (time.perf_counter() - t1) / 50
-        out = {"sched": sc, "n": n, "schedule": {k: v for k, v in env.schedule().items() if k in (
+        out = {"sched": sc, "n": n, "lib": os.path.basename(os.environ.get("RX_LIB_PATH", "librx.so")), "schedule": {k: v for k, v in env.schedule().items() if k in (
             "lane_tracks", "ray_lpr", "reward_lpe", "dyn_waves", "ray_waves")},
                "step_ms": {k: round(v[0], 4) for k, v in step.items()},
                "split_ms": {k: round(v[0], 4) for k, v in split.items()},
