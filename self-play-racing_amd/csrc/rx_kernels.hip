@@ -2001,7 +2001,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     // direction quadrant (sign bits of the f32 direction, as id2's signs): a
     // wave whose lanes all share it takes the quadrant-ordered box tables
     const int quad = (int)(__float_as_uint(csf) >> 31) | (int)((__float_as_uint(snf) >> 31) << 1);
-    const int quad0 = uni<LV>(quad);  // LV: each lane takes its own quadrant's box block
+    const int quad0 = uniform(quad);
     int scanned = 0, tested = 0;
     // segment pre-filter operands (seg_may_hit): |sx| + |sy| <= |cx| + |cy| + 2 rad for every boundary point
 #ifdef RX_RAY_STAMPS
@@ -2018,7 +2018,9 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     RAY_STAMP(3);
     auto scan = [&](auto filt) {
       constexpr bool F = decltype(filt)::value;
-      if (a.box_quadrants && (LV || __all(quad == quad0))) {
+      // LV: the plain box table (block 0) -- the lanes of an env then share its box lines
+      // whatever their quadrants (fewer lines per wave: stress pool 213 -> 200 us)
+      if (!LV && a.box_quadrants && __all(quad == quad0)) {
         const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
         const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
         cull_scan<true, F, LPR, LV>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x,
@@ -2028,7 +2030,11 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
                                      best, bestf, tested, scanned, pf);
       }
     };
-    if (a.seg_filter && a.tr.seg_f)
+    // LV: no float32 pre-filter -- with per-lane segment loads the filter's extra
+    // 16-byte load per segment costs more than the f64 tests it saves (stress pool,
+    // 65,536 envs: k_step2 247 -> 216 us, profiles/r06/d_lv_ab.jsonl), and leaving
+    // it out of the lane-varying kernels frees registers for a sixth wave per SIMD
+    if (!LV && a.seg_filter && a.tr.seg_f)
       scan(std::true_type{});
     else
       scan(std::false_type{});
@@ -2207,7 +2213,10 @@ __global__ __launch_bounds__(256) void k_rays_wide(rx_kargs a) {
 #define RX_STEP2_MINW 8  // min waves per SIMD: caps VGPRs at 64 so the raycast half keeps full occupancy (some spills in the REWARD half)
 #endif
 #ifndef RX_STEP2_MINW_LV
-#define RX_STEP2_MINW_LV 5  // lane-varying slots (k_step2<1, 1, 1, true>): 93 VGPRs, no spills (8 waves: 201 spilled VGPRs)
+// lane-varying slots (k_step2<1, 1, 1, true>): 6 waves per SIMD (80 VGPRs, 22 spilled) -- stress pool,
+// 65,536 envs, k_step2 216 / 213 / 227 us at 5 / 6 / 7 waves, 200 us at 6 with the plain box tables
+// (profiles/r06/e_lv_nf.jsonl)
+#define RX_STEP2_MINW_LV 6
 #endif
 #ifndef RX_STEP2_MINW_2
 #define RX_STEP2_MINW_2 6  // two-car k_step2<2>: 80 VGPRs (fewer REWARD spills; 8 -> 6 waves: +9 % at 8,192 envs, +1 % at 65,536)

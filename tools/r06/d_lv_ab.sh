@@ -6,6 +6,7 @@ O=gpurun_out/r06d
 mkdir -p $O
 export TMPDIR=/tmp
 L=self-play-racing_amd/rx/lib
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_ppo_golden.py -k bf16 > $O/pytest_g8_bf16.txt 2>&1
 timeout -k 10 300 python tools/r06/stress_probe.py 65536 lane_tracks=1 lane_tracks=1,seg_filter=-1 lane_tracks=1,box_quadrants=-1 >> $O/probe.jsonl 2>> $O/probe.err || exit 1
 for v in ww_rays ww_argmin minw6 minw4; do
   RX_LIB_PATH=$L/ab_$v.so timeout -k 10 200 python tools/r06/stress_probe.py 65536 lane_tracks=1 >> $O/probe.jsonl 2>> $O/probe.err || exit 1
