@@ -86,6 +86,7 @@ struct rx_env {
   DevBuf<float> chunk_box_f, super_box_f;  // outward-rounded float32 copies (raycast box tests) + 4 quadrant blocks
   int32_t n_chunk_boxes = 0, n_super_boxes = 0;
   DevBuf<float> seg_f;  // [2*Wtot][4] float32 (start.x, start.y, v2.x, v2.y): the raycast's segment pre-filter
+  DevBuf<rx_slot_hdr> slot_hdr;  // [n] per-slot headers (lane-varying kernels)
   // assignment
   bool assigned = false;
   DevBuf<int32_t> perm[2];  // the env order (perm[0]: env id at each position) and the re-sort's shadow
@@ -149,9 +150,13 @@ namespace {
 // Culling tables for every slot: chunks of G consecutive boundary segments
 // (per side), their end-point boxes, and per slot the bounding circle of all
 // boundary points and the longest segment (kernel margins).
-int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* seg) {
+int build_headers(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* meta,
+                  const std::vector<int32_t>& off, const std::vector<int32_t>& soff, const std::vector<int32_t>& woff,
+                  const std::vector<int32_t>& wsoff, const std::vector<double>& geo);
+int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* wp, const double* seg,
+                 const double* meta) {
   const int G = h->cfg.cull_chunk;
-  if (G <= 0) return RX_OK;
+  if (G <= 0) return build_headers(h, n_tracks, wp_off, meta, {}, {}, {}, {}, {});
   const int SG = h->cfg.cull_super;  // leaves per super-chunk (0 = one level)
   std::vector<int32_t> off(n_tracks + 1, 0), woff(n_tracks + 1, 0), soff(n_tracks + 1, 0), wsoff(n_tracks + 1, 0);
   std::vector<double> boxes, wboxes, sboxes, wsboxes, geo(4 * (size_t)n_tracks);
@@ -286,7 +291,28 @@ int build_chunks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const doubl
     if ((rc = upload(h->super_off, soff.data(), soff.size()))) return rc;
     if ((rc = upload(h->super_box, sboxes.data(), sboxes.size()))) return rc;
   }
-  return RX_OK;
+  return build_headers(h, n_tracks, wp_off, meta, off, soff, woff, wsoff, geo);
+}
+
+// The per-slot headers (rx_slot_hdr) from the host tables rx_upload_tracks and
+// build_chunks produced.
+int build_headers(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const double* meta,
+                  const std::vector<int32_t>& off, const std::vector<int32_t>& soff, const std::vector<int32_t>& woff,
+                  const std::vector<int32_t>& wsoff, const std::vector<double>& geo) {
+  std::vector<rx_slot_hdr> hd((size_t)n_tracks);
+  for (int k = 0; k < n_tracks; ++k) {
+    rx_slot_hdr& r = hd[k];
+    r.wp0 = wp_off[k];
+    r.W = wp_off[k + 1] - wp_off[k];
+    r.chunk_off = off.empty() ? 0 : off[k];
+    r.super_off = soff.empty() ? 0 : soff[k];
+    r.wchunk_off = woff.empty() ? 0 : woff[k];
+    r.wsuper_off = wsoff.empty() ? 0 : wsoff[k];
+    r.pad0 = r.pad1 = 0;
+    for (int i = 0; i < 4; ++i) r.geo[i] = geo.empty() ? 0.0 : geo[4 * (size_t)k + i];
+    for (int i = 0; i < 8; ++i) r.meta[i] = meta[8 * (size_t)k + i];
+  }
+  return upload(h->slot_hdr, hd.data(), hd.size());
 }
 }  // namespace
 
@@ -429,6 +455,7 @@ int rx_destroy(rx_env* h) {
   h->chunk_box_f.release();
   h->super_box_f.release();
   h->seg_f.release();
+  h->slot_hdr.release();
   h->dyn_waves.release();
   h->ray_waves.release();
   for (void* m : h->work_mem) (void)hipFree(m);
@@ -468,7 +495,7 @@ int rx_upload_tracks(rx_env* h, int32_t n_tracks, const int32_t* wp_off, const d
     if ((rc = upload(h->seg_f, sf.data(), sf.size()))) return rc;
   }
   if ((rc = upload(h->meta, meta, 8 * (size_t)n_tracks))) return rc;
-  if ((rc = build_chunks(h, n_tracks, wp_off, wp, seg))) return rc;
+  if ((rc = build_chunks(h, n_tracks, wp_off, wp, seg, meta))) return rc;
   h->wp_off_h.assign(wp_off, wp_off + n_tracks + 1);
   h->n_tracks = n_tracks;
   h->assigned = false;  // slots may have changed meaning: require rx_assign again
@@ -814,7 +841,8 @@ static void make_kargs(rx_env* h, const rx_io* io, int mode, const uint8_t* mask
   a.tr = rx_track_view{h->wp_off.p,    h->wp.p,        h->nrm.p,      h->seg.p,        h->meta.p,
                        h->chunk_off.p, h->chunk_box.p, h->slot_geo.p, h->wchunk_off.p, h->wchunk_box.p,
                        h->super_off.p, h->super_box.p, h->wsuper_off.p, h->wsuper_box.p,
-                       h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes, h->seg_f.p};
+                       h->chunk_box_f.p, h->super_box_f.p, h->n_chunk_boxes, h->n_super_boxes, h->seg_f.p,
+                       h->slot_hdr.p};
   a.st = h->work;
   a.st.track = h->st.track;                // read-only, env order
   a.st.speed_weight = h->st.speed_weight;  // read-only, env order (or nullptr)

@@ -20,6 +20,16 @@ struct rx_wave {
   int32_t count;
 };
 
+// Every per-slot scalar the lane-varying kernels read, in ONE 128-byte record (one
+// cache line per env instead of one per table: the slot's waypoint range, its culling
+// table offsets, bounding circle and meta).  Built by rx_upload_tracks.
+struct rx_slot_hdr {
+  int32_t wp0, W, chunk_off, super_off, wchunk_off, wsuper_off, pad0, pad1;
+  double geo[4];   // slot_geo: bounding-circle centre x, y, radius, longest segment
+  double meta[8];  // rx_upload_tracks meta row
+};
+static_assert(sizeof(rx_slot_hdr) == 128, "one cache line per slot");
+
 struct rx_track_view {
   const int32_t* wp_off;     // [n+1]
   const double* wp;          // [Wtot][2]
@@ -44,6 +54,7 @@ struct rx_track_view {
   int32_t n_chunk_boxes;     // boxes per block
   int32_t n_super_boxes;
   const float* seg_f;        // [2*Wtot][4] float32 copy of seg (culled raycast: segment pre-filter)
+  const rx_slot_hdr* hdr;    // [n] per-slot header (lane-varying kernels)
 };
 
 #ifndef RX_WP_CHUNK

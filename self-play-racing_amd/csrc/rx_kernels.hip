@@ -654,11 +654,12 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
   const int sub = threadIdx.x & (LPE - 1);
   // LV: the lane's own slot (the wave's 64 positions may hold 64 slots)
   const int k = LV ? (lane < we.count ? a.pos_slot[we.perm_start + lane] : 0) : uniform(we.track);
-  const int wp0 = uni<LV>(a.tr.wp_off[k]);
-  const int W = uni<LV>(a.tr.wp_off[k + 1]) - wp0;
+  const rx_slot_hdr* __restrict__ hd = a.tr.hdr + k;  // LV: every per-slot scalar from one line
+  const int wp0 = LV ? hd->wp0 : uniform(a.tr.wp_off[k]);
+  const int W = LV ? hd->W : uniform(a.tr.wp_off[k + 1]) - wp0;
   const double2* __restrict__ wp = sl ? sl->wp : reinterpret_cast<const double2*>(a.tr.wp) + wp0;
   const double2* __restrict__ nrm = sl ? sl->nrm : reinterpret_cast<const double2*>(a.tr.nrm) + wp0;
-  const double* __restrict__ meta = a.tr.meta + 8 * k;
+  const double* __restrict__ meta = LV ? hd->meta : a.tr.meta + 8 * k;
   const double width = meta[3];
   if (lane >= we.count) return;
   // p = the env's position in the wave order: the engine's working state is
@@ -732,8 +733,9 @@ __device__ __forceinline__ void dyn1_env(const rx_kargs& a, int wave, double* an
     } else if (a.cull_chunk > 0) {
       const int prev[1] = {prev_waypoint(c.progress, W)};
       const double ccx[1] = {c.x}, ccy[1] = {c.y};
-      argmin_culled<NPL, 1, LV>(wp, a.tr.wchunk_box + 4 * (size_t)uni<LV>(a.tr.wchunk_off[k]),
-                            a.tr.wsuper_box + 4 * (size_t)uni<LV>(a.tr.wsuper_off[k]), W, qx, qy, prev, ccx, ccy,
+      argmin_culled<NPL, 1, LV>(wp, a.tr.wchunk_box + 4 * (size_t)(LV ? hd->wchunk_off : uniform(a.tr.wchunk_off[k])),
+                            a.tr.wsuper_box + 4 * (size_t)(LV ? hd->wsuper_off : uniform(a.tr.wsuper_off[k])), W, qx,
+                            qy, prev, ccx, ccy,
                             a.argmin_window, idx, a.io.counters
 #ifdef RX_DYN_STAMPS
                             , stamp + 3
@@ -1524,9 +1526,13 @@ __global__ __launch_bounds__(256) void k_dyn2(rx_kargs a) {
 //   valid  <=> D > 1e-10
 //   t >= 0 <=> C >= 0          (no underflow: |C| >= 1e-32 when nonzero here)
 //   s >= 0 <=> N >= 0
-//   s <= 1 <=> round(N/D) <= 1 <=> N/D <= 1 + 2^-53 <=> fl(N - D) <= D*2^-53
-// (the subtraction is exact by Sterbenz for D/2 <= N <= 2D, and outside that
-// range its rounding cannot cross the threshold).  Only hit segments divide.
+//   s <= 1 <=> round(N/D) <= 1 <=> N <= D
+// (both are doubles and D > 1e-10 is normal: N > D means N >= D + ulp(D) >
+// D (1 + 2^-53), so N/D lies strictly above the rounding midpoint 1 + 2^-53 and
+// rounds up to 1 + 2^-52; N <= D gives N/D <= 1 exactly.  Round 6: one compare
+// where rounds 1-5 tested fl(N - D) <= D 2^-53, the same predicate in 3 VALU;
+// tests/test_prefilter_cpu.py checks the equivalence on 4 M adversarial pairs).
+// Only hit segments divide.
 // The sign flips are one XOR of dotp's sign bit into the high words (not a
 // compare + two selects): they differ from `dotp < 0 ? -x : x` only for dotp =
 // -0.0 or NaN, where D > 1e-10 is false and no hit is reported either way.
@@ -1548,7 +1554,7 @@ __device__ __forceinline__ void seg_test(const double4 g, double ox, double oy, 
   const long long sgn = __double_as_longlong(dotp) & (long long)0x8000000000000000ull;
   const double C = __longlong_as_double(__double_as_longlong(cross) ^ sgn);
   const double N = __longlong_as_double(__double_as_longlong(dot) ^ sgn);
-  const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & ((N - D) <= D * 0x1p-53);
+  const bool hit = (D > 1e-10) & (C >= 0.0) & (N >= 0.0) & (N <= D);
   if (hit) {
     const double t = C / D;
     best = t < best ? t : best;
@@ -1570,7 +1576,7 @@ typedef float rx_f2 __attribute__((ext_vector_type(2)));
 // exact one by ~2^-50 (M1 + L).  So a segment this test rejects, with
 // e2 = 2^-17 (M1 + L + 1) >= 5.8x that bound, has a and a - p of one strict
 // sign by a margin >= 2^-18 (M1 + L): the f64 test then sees N < 0 or
-// fl(N - D) > D 2^-53 and reports no hit.  Rejecting it changes nothing; the
+// N > D and reports no hit.  Rejecting it changes nothing; the
 // wave runs the exact test on a segment iff some lane may hit it.
 struct seg_pref {
   const float4* __restrict__ segf;  // the slot's float32 segments
@@ -1786,7 +1792,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
                                           int& scanned, const seg_pref& pf) {
   const int G = a.cull_chunk;
   const float* __restrict__ fboxes =
-      a.tr.chunk_box_f + 4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)uni<LV>(a.tr.chunk_off[k]));
+      a.tr.chunk_box_f +
+      4 * ((size_t)block * a.tr.n_chunk_boxes + (size_t)(LV ? a.tr.hdr[k].chunk_off : uniform(a.tr.chunk_off[k])));
   float bm = bestf + mtf;  // refreshed with bestf after every leaf scan
   auto needed = [&](const float* box) {
     return FAST ? chunk_needed_q<LV>(box, n1, n2, id2, mtf, bm) : chunk_needed_f<LV>(box, n1, n2, id2, mtf, bm);
@@ -1817,7 +1824,8 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
   // contains the segments).
   const int nsup = (nch + SG - 1) / SG;
   const float* __restrict__ sboxes =
-      a.tr.super_box_f + 4 * ((size_t)block * a.tr.n_super_boxes + (size_t)uni<LV>(a.tr.super_off[k]));
+      a.tr.super_box_f +
+      4 * ((size_t)block * a.tr.n_super_boxes + (size_t)(LV ? a.tr.hdr[k].super_off : uniform(a.tr.super_off[k])));
   const int u0 = uni<LV>(c0 / SG);
   if constexpr (LV && RX_LV_WW_RAYS) {
     // Lane-varying slots: "while-while" traversal.  Each lane advances its own
@@ -1957,8 +1965,8 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
   int k = kw;
   if constexpr (LV) {  // the lane's env's slot
     k = a.pos_slot[pos];
-    wp0 = a.tr.wp_off[k];
-    W = a.tr.wp_off[k + 1] - wp0;
+    wp0 = a.tr.hdr[k].wp0;
+    W = a.tr.hdr[k].W;
   }
   const int S_ = 2 * W;
   const double4* __restrict__ seg = reinterpret_cast<const double4*>(a.tr.seg) + 2 * wp0;
@@ -1977,7 +1985,7 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
     ray_segments<false, LV>(seg, 0, S_, ox, oy, v3x, v3y, best, bestf, seg_pref{});
   } else {
     const int nch = (W + G - 1) / G;  // chunks per side
-    const double* __restrict__ sg = a.tr.slot_geo + 4 * k;
+    const double* __restrict__ sg = LV ? a.tr.hdr[k].geo : a.tr.slot_geo + 4 * k;
     const double cx = sg[0], cy = sg[1], rad = sg[2], L = sg[3];
     const double ddx = ox - cx, ddy = oy - cy;
     const double Rr = __builtin_sqrt(ddx * ddx + ddy * ddy) + rad;  // >= |o - p| for every boundary point p

@@ -116,3 +116,24 @@ def test_prefilter_endpoint_exactly_on_the_ray():
     keep = prefilter(ox, oy, sx, sy, v2x, v2y, v3x, v3y, e2)
     assert hit.sum() > 10_000
     assert not (hit & ~keep).any()
+
+
+def test_s_le_1_is_n_le_d():
+    """rx_kernels.hip seg_test's division-free s <= 1: with D = |dotp| > 1e-10 and
+    N = sgn(dotp) dot (doubles), round(N / D) <= 1 exactly when N <= D -- the
+    reference computes s = dot / dotp (environment/track.py:191-196) and tests
+    s <= 1.  Checked on 4 M pairs: N within +-4 ulps of D over 16 decades of D,
+    random N around D, and D a power of two (the tightest ulp(D) / D)."""
+    rng = np.random.default_rng(3)
+    n = 1_000_000
+    D = np.exp(rng.uniform(np.log(1e-10), np.log(1e6), n))
+    k = rng.integers(-4, 5, n)
+    N = D.copy()
+    for step in range(1, 5):
+        N = np.where(k >= step, np.nextafter(N, np.inf), N)
+        N = np.where(k <= -step, np.nextafter(N, -np.inf), N)
+    P2 = 2.0 ** rng.integers(-33, 20, n).astype(np.float64)
+    for NN, DD in ((N, D), (D * rng.uniform(0.5, 1.5, n), D), (np.nextafter(P2, np.inf), P2),
+                   (np.nextafter(P2, -np.inf), P2)):
+        assert np.array_equal(NN / DD <= 1.0, NN <= DD)
+        assert np.array_equal(-NN / DD <= 1.0, -NN <= DD)  # the sign-flipped operand as well
