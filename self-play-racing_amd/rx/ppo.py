@@ -166,7 +166,13 @@ class PPO:
         rx_policy_act kernel that computed the rollout's values (one launch
         instead of the critic's torch GEMMs and activations), with a zero noise
         block (no RNG draw) and scratch action / log-prob rows; torch's forward
-        otherwise or with config["fused_next_value"] = False."""
+        otherwise or with config["fused_next_value"] = False.  With
+        config["policy_dtype"] = "bf16" the bootstrap value is the bf16 critic's,
+        like every rollout value GAE combines it with (values[t] came from the
+        same bf16 kernel), so A_T's delta mixes values of ONE precision; the fp32
+        torch critic the reference uses (agent/ppo.py:224) differs from it by the
+        bf16 forward's rounding (tests/test_bf16_gpu.py's 2e-2 bound), and
+        fused_next_value = False restores it."""
         fp = self._fused_policy(next_obs.unsqueeze(0)) if self.config.get("fused_next_value", True) else None
         if fp is None:
             return self.agent.get_value(next_obs).flatten()
