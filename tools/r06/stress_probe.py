@@ -36,7 +36,9 @@ def main():
         torch.tensor([-1.0, 0.0], device=dev)
     for sc in scheds:
         sched = {k: int(v) for k, v in (kv.split("=") for kv in sc.split(",") if kv)}
-        env = RacingVectorEnv(pool, widths, device=dev, autoreset="next_step", track_set=ts, sched=sched)
+        # cull_chunk / cull_super are table-build parameters (rx_config), not schedule fields
+        geo = {k: sched.pop(k) for k in ("cull_chunk", "cull_super") if k in sched}
+        env = RacingVectorEnv(pool, widths, device=dev, autoreset="next_step", track_set=ts, sched=sched, **geo)
         env.reset_device()
         for k in range(100):
             env.step_device(acts[k % 64])
