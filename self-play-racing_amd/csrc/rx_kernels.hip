@@ -1781,6 +1781,21 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
   return slab_keep(lo, hi, bm);
 }
 
+// Lane-varying slots (RX_LEAF_BATCH): a kept super's 8 leaf boxes are tested as
+// one batch against the bound of now -- the 8 per-lane box loads in flight
+// together, one wait, instead of a load -> test -> branch chain per leaf.  The
+// bound only falls (after a scan), so a leaf the batch rejects for every lane is
+// rejected at its turn too; a candidate is re-tested exactly once a scan has
+// lowered the bound since the batch.  The leaves scanned, their order, and so
+// every result, are those of the one-at-a-time loop.  Stress pool, 65,536 envs:
+// k_step2 196.9 -> 148.3 us.  Slot-uniform waves keep the one-at-a-time loop:
+// their scalar loads hit the scalar cache, and the re-tests and the batch's SGPRs
+// cost more than the chain (seed-1 pool 56.8 -> 60.7 us, 4,096 envs 20.3 ->
+// 22.2 us); batching both sides' super boxes as well was slower (156 us).
+// profiles/r06/j_*, k_*.
+#ifndef RX_LEAF_BATCH
+#define RX_LEAF_BATCH 1
+#endif
 // The culled scan of one lane's ray over slot k's chunks (cull_chunk G > 0),
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
 // `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far) * id;
@@ -1870,6 +1885,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
     }
     return;
   }
+  constexpr bool BATCH = LV && RX_LEAF_BATCH;
   for (int s = 0; s < nsup; ++s) {
     const int off = (s + 1) >> 1;
     const bool back = (s & 1) != 0;
@@ -1880,6 +1896,32 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
     for (int side = 0; side < 2; ++side) {
       ++tested;
       if (!vote<LV>(needed(sboxes + 4 * (side * nsup + u)))) continue;
+      if (BATCH && SG == 8) {
+        unsigned m = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int qq = q < nl ? q : nl - 1;
+          const int c = l0 + (back ? nl - 1 - qq : qq);
+          if (vote<LV>(needed(fboxes + 4 * (side * nch + c))) && q < nl) m |= 1u << q;
+        }
+        tested += nl;
+        bool dirty = false;  // a scan has lowered bm since the batch
+        while (m) {
+          const int q = __builtin_ctz(m);
+          m &= m - 1;
+          const int c = l0 + (back ? nl - 1 - q : q);
+          if (dirty) {
+            ++tested;
+            if (!vote<LV>(needed(fboxes + 4 * (side * nch + c)))) continue;
+          }
+          ++scanned;
+          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+                                       best, bestf, pf);
+          bm = bestf + mtf;
+          dirty = true;
+        }
+        continue;
+      }
       for (int q = 0; q < nl; ++q) {
         const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
         ++tested;
