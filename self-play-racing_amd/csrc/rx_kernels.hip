@@ -114,15 +114,6 @@ __device__ __forceinline__ int uni(int v) {
   else
     return uniform(v);
 }
-// A/B knobs (DESIGN.md §3 "Lane-varying track slots"): the "while-while" form of the
-// lane-varying raycast / closest-waypoint traversals (each lane advances to its next
-// leaf, then all lanes holding one scan together) instead of the lock-step visit.
-#ifndef RX_LV_WW_RAYS
-#define RX_LV_WW_RAYS 0
-#endif
-#ifndef RX_LV_WW_ARGMIN
-#define RX_LV_WW_ARGMIN 0
-#endif
 template <bool LV>
 __device__ __forceinline__ bool vote(bool b) {
   if constexpr (LV)
@@ -296,48 +287,7 @@ __device__ __forceinline__ void argmin_culled(const double2* __restrict__ wp, co
 #endif
   const int u0 = uni<LV>(prev[0] / (RX_WP_CHUNK * RX_WP_SUPER));
   int scanned = 0, tested = nws;
-  if constexpr (LV && RX_LV_WW_ARGMIN) {
-    // lane-varying slots: the "while-while" form of the visit below (cull_scan's
-    // comment): each lane tests its kept supers' leaves until it holds one to
-    // scan, then every lane holding a leaf scans it at once
-    int s = 0, q = 0;  // next visit: leaf q of the s-th super in visiting order
-    while (true) {
-      int i0 = -1;
-      while (s < nws && i0 < 0) {
-        const int off = (s + 1) >> 1;
-        const bool back = (s & 1) != 0;
-        int u = back ? u0 - off : u0 + off;
-        u = u < 0 ? u + nws : (u >= nws ? u - nws : u);
-        if (!((smask >> u) & 1ull)) {
-          ++s;
-          continue;
-        }
-        const int l0 = u * RX_WP_SUPER, nl = min(nwc, l0 + RX_WP_SUPER) - l0;
-        const int c = l0 + (back ? nl - 1 - q : q);
-        ++tested;
-        if (box_may_hold_c<NC, true>(wbox + 4 * c, cxs, cys, T)) i0 = c * RX_WP_CHUNK;
-        if (++q >= nl) {
-          q = 0;
-          ++s;
-        }
-      }
-      if (!__any(i0 >= 0)) break;
-      if (i0 >= 0) {
-        ++scanned;
-        const int i1 = min(W, i0 + RX_WP_CHUNK);
-        for (int i = i0; i < i1; ++i) {
-          const double2 w = wp[i];
-#pragma unroll
-          for (int p = 0; p < NP; ++p) {
-            const double dx = w.x - px[p], dy = w.y - py[p];
-            argmin_take(dx * dx + dy * dy, i, best[p], idx[p]);
-          }
-        }
-        car_thresholds<NP, NC>(best, T, active);
-      }
-    }
-  }
-  for (int s = 0; !(LV && RX_LV_WW_ARGMIN) && s < nws; ++s) {
+  for (int s = 0; s < nws; ++s) {
     const int off = (s + 1) >> 1;
     const bool back = (s & 1) != 0;
     int u = back ? u0 - off : u0 + off;
@@ -1842,49 +1792,6 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
       a.tr.super_box_f +
       4 * ((size_t)block * a.tr.n_super_boxes + (size_t)(LV ? a.tr.hdr[k].super_off : uniform(a.tr.super_off[k])));
   const int u0 = uni<LV>(c0 / SG);
-  if constexpr (LV && RX_LV_WW_RAYS) {
-    // Lane-varying slots: "while-while" traversal.  Each lane advances its own
-    // visit cursor -- the same order as below: supers outward, per super both
-    // sides, a kept super's leaves -- testing boxes until it holds a leaf to scan
-    // or has visited everything; then every lane holding a leaf scans it at once.
-    // A wave then runs about max-over-lanes leaf scans, not one per visit step at
-    // which some lane scans (its lanes' slots, cars and hits all differ).  Each
-    // lane visits, tests and scans exactly what the loop below would for it alone.
-    int s = 0, side = 0, q = -1;  // next visit: super (s, side) when q < 0, else that super's leaf q
-    while (true) {
-      int j0 = -1, j1 = 0;
-      while (s < nsup && j0 < 0) {
-        const int off = (s + 1) >> 1;
-        const bool back = (s & 1) != 0;
-        int u = back ? u0 - off : u0 + off;
-        u = u < 0 ? u + nsup : (u >= nsup ? u - nsup : u);
-        const int l0 = u * SG, nl = min(nch, l0 + SG) - l0;
-        ++tested;
-        if (q < 0) {
-          q = needed(sboxes + 4 * (side * nsup + u)) ? 0 : nl;
-        } else {
-          const int c = l0 + (back ? nl - 1 - q : q);  // forward supers ascending, backward ones descending
-          if (needed(fboxes + 4 * (side * nch + c))) {
-            j0 = side * W + c * G;
-            j1 = side * W + min(W, (c + 1) * G);
-          }
-          ++q;
-        }
-        if (q >= nl) {  // this super's side done: the other side, then the next super
-          q = -1;
-          side ^= 1;
-          s += side == 0 ? 1 : 0;
-        }
-      }
-      if (!__any(j0 >= 0)) break;
-      if (j0 >= 0) {
-        ++scanned;
-        ray_segments<FILT, true>(seg, j0, j1, ox, oy, v3x, v3y, best, bestf, pf);
-        bm = bestf + mtf;
-      }
-    }
-    return;
-  }
   constexpr bool BATCH = LV && RX_LEAF_BATCH;
   for (int s = 0; s < nsup; ++s) {
     const int off = (s + 1) >> 1;
