@@ -220,30 +220,43 @@ __global__ __launch_bounds__(kBlock) void k_state_sync(int n, const int32_t* __r
 
 // rx_random_permutation: a pseudo-random permutation of [0, n) in one
 // launch (the device minibatch shuffle, config["shuffle"] = "device").  A
-// 4-round balanced Feistel network on 2h bits (2^(2h) >= n) is a bijection of
-// [0, 2^(2h)); cycle-walking (apply it again while the value is >= n) turns it
-// into a bijection of [0, n), at most 4 walks on average since 2^(2h) < 4n.
+// 4-round UNBALANCED Feistel network on bits = ceil(log2 n) bits (halves of
+// a = bits / 2 and b = bits - a bits; round k maps the current right half
+// through F into the width of the left one, then the halves swap, so after the
+// even number of rounds the widths are back) is a bijection of [0, 2^bits);
+// cycle-walking (apply it again while the value is >= n) turns it into a
+// bijection of [0, n), fewer than 2 walks on average since 2^bits < 2n, none
+// when n is a power of two (configs[1]: n = 2^19).  Round 6: the balanced
+// network of rounds 3-5 ran on 2 ceil(bits / 2) bits (2^20 for 2^19 rows, two
+// walks on average and a wave waiting for its longest lane's chain).
 // Round function: the splitmix64 finalizer of (half ^ round key).
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
-__global__ __launch_bounds__(kBlock) void k_feistel_perm(int64_t n, int h, uint64_t seed, int64_t* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void k_feistel_perm(int64_t n, int bits, uint64_t seed,
+                                                          int64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint64_t mask = (1ull << h) - 1ull;
+  const int a = bits >> 1, b = bits - a;  // left / right widths of the input
+  uint64_t key[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) key[k] = mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1));
   uint64_t x = (uint64_t)i;
   do {
-    uint64_t l = x >> h, r = x & mask;
+    int wl = a, wr = b;
+    uint64_t l = x >> wr, r = x & ((1ull << wr) - 1ull);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint64_t f = mix64(r ^ mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1))) & mask;
-      const uint64_t t = l ^ f;
+      const uint64_t t = l ^ (mix64(r ^ key[k]) & ((1ull << wl) - 1ull));
       l = r;
       r = t;
+      const int w = wl;
+      wl = wr;
+      wr = w;
     }
-    x = (l << h) | r;
+    x = (l << wr) | r;
   } while (x >= (uint64_t)n);
   out[i] = (int64_t)x;
 }
@@ -298,9 +311,8 @@ extern "C" int rx_state_sync(const rx_state* work, const rx_state* user, const i
 extern "C" int rx_launch_permutation(int64_t n, uint64_t seed, int64_t* out, hipStream_t s) {
   if (n <= 0) return 0;
   int bits = 1;
-  while (bits < 62 && (1ll << bits) < n) ++bits;
-  const int h = (bits + 1) / 2;  // 2h >= bits, so 2^(2h) >= n and < 4n (cycle-walk length)
+  while (bits < 62 && (1ll << bits) < n) ++bits;  // 2^bits >= n and < 2n (cycle-walk length)
   const int64_t grid = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_feistel_perm, dim3((unsigned)grid), dim3(kBlock), 0, s, n, h, seed, out);
+  hipLaunchKernelGGL(k_feistel_perm, dim3((unsigned)grid), dim3(kBlock), 0, s, n, bits, seed, out);
   return (int)hipGetLastError();
 }

@@ -546,11 +546,7 @@ class PPO:
             rng.append(torch.get_rng_state())
             self._device_permutation(ent.perms[e])
         f.epochs_stats(ent.perms, ent.stats_all)
-        run = self._epoch_nostats(ent)
-        for e in range(E):
-            ent.perm.copy_(ent.perms[e])
-            f.stats.copy_(ent.stats_all[e].reshape(-1))
-            run()
+        self._epochs_all(ent, E)()
         if bool(ent.stop.item()):
             taken = int(round(float((self._flat.step_t - steps0).item())))
             epoch = min(taken // n_mb, E - 1)
@@ -558,22 +554,32 @@ class PPO:
                 torch.set_rng_state(rng[epoch + 1])
             self._early_stop_msg(epoch, float(ent.kl.item()))
 
-    def _epoch_nostats(self, ent):
-        """The epoch's minibatch steps without its advantage-statistics launch
-        (the stats rows are copied in by _update_epochs_async), as a graph when
-        the epoch runner captures one."""
-        run = ent.__dict__.get("run_nostats")
+    def _epochs_all(self, ent, E):
+        """All E epochs' minibatch steps, epoch e reading its rows of ent.perms /
+        ent.stats_all in place (FusedMinibatchGrad.epoch_view: no per-epoch copy
+        into the runner's buffers) -- ONE HIP graph for the whole update when the
+        epoch runner captures graphs (round 6: was a 4 MB perm copy, a stats copy
+        and a graph replay per epoch)."""
+        run = ent.__dict__.get("run_all")
         if run is None:
+            f = ent.fused
+            views = [f.epoch_view(ent.perms[e], ent.stats_all[e]) for e in range(E)]
+
+            def steps():
+                for e in range(E):
+                    for m in range(f.n_mb):
+                        f.update(m, ent.stop, ent.kl, batch=views[e])
             if ent.graph is not None:
                 g = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(ent.perm.device)
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                    ent.fused.epoch(ent.stop, ent.kl, stats=False)
+                    steps()
                 run = g.replay
-                ent.graph_nostats = g
+                ent.graph_all = g
             else:
-                run = lambda: ent.fused.epoch(ent.stop, ent.kl, stats=False)  # noqa: E731
-            ent.run_nostats = run
+                run = steps
+            ent.views = views
+            ent.run_all = run
         return run
 
     def _update_epochs(self, b, fused, capture):

@@ -96,9 +96,10 @@ class FusedMinibatchGrad:
                                          _lib.ptr(kl_at_stop), s), "rx_ppo_kl_check")
             flat.step(stop=stop)
 
-    def update(self, m, stop, kl_at_stop, stream=None):
+    def update(self, m, stop, kl_at_stop, stream=None, batch=None):
         """One optimizer step on minibatch m (rx_ppo_minibatch_update: gradient,
-        reduce + clip norms + step count, Adam: three launches)."""
+        reduce + clip norms + step count, Adam: three launches); ``batch``: a view
+        of self.batch with another epoch's perm / stats rows (epoch_view)."""
         f = self.flat
         ws = self.__dict__.get("adam_ws")
         if ws is None:
@@ -108,7 +109,7 @@ class FusedMinibatchGrad:
             # zero-filled: its last word is the fused launch's arrival counter (rx.h, ABI v22)
             ws = self.adam_ws = torch.zeros(n, dtype=torch.float32, device=self.stats.device)
         _lib.check(self.L.rx_ppo_minibatch_update(
-            self.batch, int(m), f.cfg, _lib.ptr(f.flat_param), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
+            self.batch if batch is None else batch, int(m), f.cfg, _lib.ptr(f.flat_param), _lib.ptr(self.ws_f), _lib.ptr(self.ws_d),
             _lib.ptr(f.flat_grad), _lib.ptr(f.exp_avg), _lib.ptr(f.exp_avg_sq), _lib.ptr(f.step_t), _lib.ptr(f.lr_t),
             _lib.ptr(stop), _lib.ptr(kl_at_stop), _lib.ptr(ws), _lib.stream_ptr(stream)), "rx_ppo_minibatch_update")
 
@@ -120,6 +121,16 @@ class FusedMinibatchGrad:
             self.adv_stats()
         for m in range(self.n_mb):
             self.update(m, stop, kl_at_stop)
+
+    def epoch_view(self, perm, stats):
+        """self.batch reading its minibatch rows from ``perm`` (int64 [B]) and its
+        advantage statistics from ``stats`` (float32 [n_mb, 2]) in place -- one
+        epoch's rows of the [E, B] / [E, n_mb, 2] buffers of epochs_stats, with no
+        copy into self.batch's own buffers.  The caller keeps both alive."""
+        b = RxPPOBatch_copy(self.batch)
+        b.perm = _lib.ptr(perm)
+        b.adv_stats = _lib.ptr(stats)
+        return b
 
     def epochs_stats(self, perms, stats_out, stream=None):
         """Advantage statistics of E epochs in ONE rx_ppo_adv_stats_ws call:
