@@ -37,13 +37,13 @@ PASSES = [
     ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
      "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32"],
 ]
-KERNELS = ("k_window_args", "k_window", "k_step2", "k_kin1", "k_kin2", "k_rays", "k_dyn1", "k_dyn2", "k_gae",
+KERNELS = ("k_step2", "k_kin1", "k_kin2", "k_rays", "k_dyn1", "k_dyn2", "k_gae",
            "k_sort_hist", "k_sort_scan",
            "k_sort_scatter", "k_state_copy", "k_state_sync", "k_ppo_grad", "k_policy_act")
 
 
 def short(name):
-    if "k_dyn1<1, 1>" in name or "k_kin1p" in name:  # the split step's k_kin1 (k_kin1p: its sorting launches)
+    if "k_dyn1<1, 1>" in name or "k_dyn1<1, 1, " in name:  # the split step's k_kin1 (PART = KIN)
         return "k_kin1"
     if "k_dyn2<1>" in name:
         return "k_kin2"
@@ -100,12 +100,10 @@ def main():
     ap.add_argument("--timeout", type=int, default=240)
     ap.add_argument("--cmd", default=None, help="profile this command instead of bench.py (e.g. tools/bench_ppo.py ...)")
     ap.add_argument("--passes", default=None, help="counter passes 'C1,C2;C3,...' instead of the default four")
-    ap.add_argument("--window-steps", type=int, default=8,
-                    help="steps per k_window launch of the kept dispatches: the bench's instrumented windows are "
-                         "whole re-sort intervals (8 at 65,536 envs)")
     ap.add_argument("--bench-args", default="--steps 24 --burn-in 100 --warmup 0 --profile-steps 128 "
                                             "--no-cpu-baseline --async-probe-groups 0 --ppo-updates 0 "
-                                            "--no-time-to-90 --selfplay-updates 0 --counter-steps 0")
+                                            "--no-time-to-90 --selfplay-updates 0 --counter-steps 0 --stress off "
+                                            "--rccl-world1 off")
     args = ap.parse_args()
     cmd = [sys.executable, "bench.py", "--envs-per-gpu", str(args.envs)] + args.bench_args.split()
     if args.cmd:
@@ -142,8 +140,6 @@ def main():
             if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
                 cs["hbm_bytes_per_launch"] = cs["FETCH_SIZE"] + cs["WRITE_SIZE"]
                 cs["hbm_bytes_per_launch_fetch_x2"] = 2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]
-            if k == "k_window":
-                cs["steps_per_launch"] = args.window_steps
             if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs and cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"] > 0:
                 cs["l2_hit_rate"] = cs["TCC_HIT_sum"] / (cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"])
             res[name] = cs
