@@ -31,7 +31,7 @@ to last wave end, the span rocprofv3 reports) give the kernel durations.
 Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant production
 kernel, k_step2 (REWARD half beside the raycast), with its algorithmic bytes;
 ``compute_roofline`` is its VALU busy fraction from the committed steady-state
-PMC counts (profiles/r05/pmc_steady.json, same launch size); ``cpu_baseline``
+PMC counts (profiles/r06/pmc_steady.json, same launch size); ``cpu_baseline``
 times oracle/np_env.py -- the reference's NumPy step restated (bit-exact vs
 the reference's golden vectors) -- on this host's cores; ``time_to_90`` is the
 second half of the metric (PPO wall-clock to 90 % success, evaluate.py
@@ -60,7 +60,7 @@ RAYS_BYTES_PER_ENV = 24 + 11 * 4   # k_rays algorithmic HBM bytes/env: read x,y,
 # 11 f32 obs = 44 B
 STEP2_BYTES_PER_ENV = 74 + 38 + 44
 STEP_BYTES_PER_ENV = 218           # whole step, SURVEY.md §8(d)
-PMC_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_steady.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_steady.json")
 
 
 def load_pmc(n):
