@@ -27,7 +27,7 @@ cat $OUT/bench_ppo.jsonl
 echo R06Z_MAIN_DONE
 export RX_BENCH_MARKS=1
 cd /tmp && timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/drvprof -o run -- \
-  python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver20_rocprof.jsonl 2> $OUT/bench_driver20_rocprof.err \
+  python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 20 --warmup 5 --stress off > $OUT/bench_driver20_rocprof.jsonl 2> $OUT/bench_driver20_rocprof.err \
   || { tail -20 $OUT/bench_driver20_rocprof.err; exit 1; }
 cd $GRAFT_REPO_ROOT; unset RX_BENCH_MARKS
 cp $(find /tmp/drvprof -name '*kernel_stats.csv' | head -1) $OUT/bench_driver20_kernel_stats.csv
