@@ -1621,6 +1621,9 @@ __device__ __forceinline__ double quad_dpp(double v) {
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+#ifndef RX_LPR_PREFETCH
+#define RX_LPR_PREFETCH 1
+#endif
 // One scanned leaf's segments [j0, j1) for the lanes of a wave.  LPR = 1: each
 // lane tests all of them for its ray (ray_segments).  LPR = 2 or 4 (few envs:
 // the raycast is a latency chain, rx_assign): LPR adjacent lanes of a quad
@@ -1628,7 +1631,7 @@ __device__ __forceinline__ double quad_dpp(double v) {
 // LPR, ...), then take the minimum of their bests, so every lane goes on with
 // the ray's best -- the minimum over the leaf's exact hits, whoever tested
 // which segment.
-template <bool FILT, int LPR, bool LV = false>
+template <bool FILT, int LPR, bool LV = false, bool PF = false>
 __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, int j0, int j1, double ox, double oy,
                                               double v3x, double v3y, double& best, float& bestf, const seg_pref& pf) {
   if constexpr (LPR == 1) {
@@ -1637,12 +1640,35 @@ __device__ __forceinline__ void leaf_segments(const double4* __restrict__ seg, i
     static_assert(!LV, "lane-varying slots: one lane per ray");
     static_assert(LPR == 2 || LPR == 4, "2 or 4 lanes per ray");
     const int sub = threadIdx.x & (LPR - 1);
-    for (int jb = j0; jb < j1; jb += LPR) {
-      const int j = jb + sub < j1 ? jb + sub : j0;
-      const double4 g = seg[j];
-      bool may = jb + sub < j1;
-      if constexpr (FILT) may = may && seg_may_hit(pf.segf[j], pf);
-      if (may) seg_test(g, ox, oy, v3x, v3y, best);
+    constexpr int PER = 8 / LPR;  // a lane's segments of a leaf of <= 8
+    // PF: kernels scheduled at LPR lanes per ray (not the 1-lane kernels' tail split,
+    // whose register budget the extra live loads would blow)
+    if (PF && RX_LPR_PREFETCH && j1 - j0 <= 8) {
+      // every segment of the lane's share loaded before the first test (one memory
+      // round trip per leaf, not one per segment: the test's divergent branch kept
+      // the compiler from hoisting the next load)
+      double4 g[PER];
+      float4 f[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int j = j0 + sub + LPR * k < j1 ? j0 + sub + LPR * k : j0;
+        g[k] = seg[j];
+        if constexpr (FILT) f[k] = pf.segf[j];
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        bool may = j0 + sub + LPR * k < j1;
+        if constexpr (FILT) may = may && seg_may_hit(f[k], pf);
+        if (may) seg_test(g[k], ox, oy, v3x, v3y, best);
+      }
+    } else {
+      for (int jb = j0; jb < j1; jb += LPR) {
+        const int j = jb + sub < j1 ? jb + sub : j0;
+        const double4 g = seg[j];
+        bool may = jb + sub < j1;
+        if constexpr (FILT) may = may && seg_may_hit(pf.segf[j], pf);
+        if (may) seg_test(g, ox, oy, v3x, v3y, best);
+      }
     }
     best = __builtin_fmin(best, quad_dpp<0xB1>(best));
     if constexpr (LPR == 4) best = __builtin_fmin(best, quad_dpp<0x4E>(best));
@@ -1750,7 +1776,7 @@ __device__ __forceinline__ bool chunk_needed_q(const float* __restrict__ box, rx
 // visiting them outward from chunk c0.  FAST: quadrant-ordered box block
 // `block` (1..4) with chunk_needed_q and offsets (n1, n2) = (near, far) * id;
 // otherwise block 0 with chunk_needed_f and (n1, n2) = (nlo, nhi) * id.
-template <bool FAST, bool FILT, int LPR, bool LV = false>
+template <bool FAST, bool FILT, int LPR, bool LV = false, bool PF = false>
 __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int nch, const double4* __restrict__ seg,
                                           int c0, int block, rx_f2 n1, rx_f2 n2, rx_f2 id2, float mtf, double ox,
                                           double oy, double v3x, double v3y, double& best, float& bestf, int& tested,
@@ -1774,7 +1800,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (vote<LV>(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+          leaf_segments<FILT, LPR, LV, PF>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
                                        best, bestf, pf);
           bm = bestf + mtf;
         }
@@ -1822,7 +1848,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
             if (!vote<LV>(needed(fboxes + 4 * (side * nch + c)))) continue;
           }
           ++scanned;
-          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+          leaf_segments<FILT, LPR, LV, PF>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
                                        best, bestf, pf);
           bm = bestf + mtf;
           dirty = true;
@@ -1834,7 +1860,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
         ++tested;
         if (vote<LV>(needed(fboxes + 4 * (side * nch + c)))) {
           ++scanned;
-          leaf_segments<FILT, LPR, LV>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
+          leaf_segments<FILT, LPR, LV, PF>(seg, side * W + c * G, side * W + min(W, (c + 1) * G), ox, oy, v3x, v3y,
                                        best, bestf, pf);
           bm = bestf + mtf;
         }
@@ -1866,7 +1892,7 @@ __device__ __forceinline__ void cull_scan(const rx_kargs& a, int k, int W, int n
 // LV (lane-varying slots): the wave's tasks are the (env, agent, ray) tasks of its
 // 64-env block in env-major order -- 11 rays of ~6 envs, so lanes of one env share
 // their slot's cache lines -- and every lane reads its own env's slot.
-template <int A, int LPR, bool LV = false>
+template <int A, int LPR, bool LV = false, bool PF = false>
 __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, const int32_t* tasks, int wave) {
   static_assert(!LV || LPR == 1, "lane-varying slots: one lane per ray");
 #ifdef RX_RAY_STAMPS
@@ -1980,10 +2006,10 @@ __device__ __forceinline__ void rays_wave(const rx_kargs& a, const rx_wave we, c
       if (!LV && a.box_quadrants && __all(quad == quad0)) {
         const rx_f2 nn = {(quad0 & 1) ? nhi.x : nlo.x, (quad0 & 2) ? nhi.y : nlo.y};
         const rx_f2 nf = {(quad0 & 1) ? nlo.x : nhi.x, (quad0 & 2) ? nlo.y : nhi.y};
-        cull_scan<true, F, LPR, LV>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x,
+        cull_scan<true, F, LPR, LV, PF>(a, k, W, nch, seg, c0, quad0 + 1, nn * id2, nf * id2, id2, mtf, ox, oy, v3x,
                                     v3y, best, bestf, tested, scanned, pf);
       } else {
-        cull_scan<false, F, LPR, LV>(a, k, W, nch, seg, c0, 0, nlo * id2, nhi * id2, id2, mtf, ox, oy, v3x, v3y,
+        cull_scan<false, F, LPR, LV, PF>(a, k, W, nch, seg, c0, 0, nlo * id2, nhi * id2, id2, mtf, ox, oy, v3x, v3y,
                                      best, bestf, tested, scanned, pf);
       }
     };
@@ -2053,10 +2079,10 @@ __device__ __forceinline__ void ray_finish(const rx_kargs& a, int pos, int q, in
   a.io.obs[(size_t)(A * e + q) * a.D + ray] = (float)dist / 50.0f;  // racing_env.py:46,51,53
 }
 
-template <int A, int LPR, bool LV = false>
+template <int A, int LPR, bool LV = false, bool PF = false>
 __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
   if (wave >= a.n_ray_waves) return;
-  rays_wave<A, LPR, LV>(a, a.ray_waves[wave], a.tasks, wave);
+  rays_wave<A, LPR, LV, PF>(a, a.ray_waves[wave], a.tasks, wave);
 }
 
 // A ray wave of the table: at the schedule's LPR lanes per ray, or -- for the
@@ -2076,7 +2102,7 @@ __device__ __forceinline__ void rays_body(const rx_kargs& a, int wave) {
 #ifndef RX_RAY_PRIO_FROM
 #define RX_RAY_PRIO_FROM 70
 #endif
-template <int A, int LPR, bool LV = false>
+template <int A, int LPR, bool LV = false, bool PF = false>
 __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
   if constexpr (LV) {  // no tail split, no dispatch-order priority (rx_assign: group-octet-major)
     rays_body<A, 1, true>(a, wave);
@@ -2088,13 +2114,13 @@ __device__ __forceinline__ void rays_dispatch(const rx_kargs& a, int wave) {
   if constexpr (LPR == 1) {
     if (a.ray_tail_from >= 0 && wave >= a.ray_tail_from) {
       if (a.ray_tail_lpr == 4)
-        rays_body<A, 4>(a, wave);
+        rays_body<A, 4, false, false>(a, wave);
       else
-        rays_body<A, 2>(a, wave);
+        rays_body<A, 2, false, false>(a, wave);
       return;
     }
   }
-  rays_body<A, LPR>(a, wave);
+  rays_body<A, LPR, false, PF>(a, wave);
 }
 
 template <int A, bool LV = false>
@@ -2211,7 +2237,7 @@ __global__ __launch_bounds__(64, A == 1 ? (LV ? RX_STEP2_MINW_LV : RX_STEP2_MINW
     }
     add_episode_stats(a, ep);
   } else {
-    rays_dispatch<A, LPR, LV>(a, b - n_rw);
+    rays_dispatch<A, LPR, LV, LPR == 4>(a, b - n_rw);  // PF: prefetched leaf scans at 4 lanes per ray
   }
   prof_end(a, b, prof_t0);
 }
