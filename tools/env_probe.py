@@ -41,5 +41,14 @@ for k in range(steps):
         env.profile(0)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
+prof = env.profile_read()
+split = None
+if os.environ.get("PROBE_SPLIT") == "1":  # REWARD half alone + the raycast alone (rx_step_phases 1, 2)
+    env.profile(1)
+    for k in range(16):
+        env.step_device(bank[k % 64], phases=1)
+        env.step_device(bank[k % 64], phases=2)
+    env.profile(0)
+    split = {k: round(v[0] * 1e3, 1) for k, v in env.profile_read().items()}
 print(json.dumps({"contig": os.environ.get("PROBE_CONTIG", "0"), "sort": os.environ.get("PROBE_SORT", "16"), "N": N, "agents": A, "env_steps_per_s": round(N * steps / dt), "us_per_step": round(dt / steps * 1e6, 1),
-                  "kernels_us": {k: round(v[0] * 1e3, 1) for k, v in env.profile_read().items()}}))
+                  "kernels_us": {k: round(v[0] * 1e3, 1) for k, v in prof.items()}, "split_us": split}))
