@@ -482,7 +482,8 @@ int rx_ppo_kl_check(const float* kl, float kl_target, uint8_t* stop, float* kl_a
 /* ABI v16.  The minibatch shuffle of PPO.ppo_update (agent/ppo.py:165-171,
  * np.random.shuffle(b_inds)) on the device, for config shuffle = "device": out
  * [n] int64 receives a pseudo-random permutation of 0 .. n-1 keyed by seed
- * (4-round Feistel network, cycle-walked to [0, n)); one launch, no host
+ * (4-round unbalanced Feistel network on ceil(log2 n) bits, cycle-walked to
+ * [0, n)); one launch, no host
  * round trip.  Same seed, same permutation. */
 int rx_random_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream);
 
